@@ -1,0 +1,141 @@
+"""Loader for the native engine library (libaclswarm_amd.so, built in-tree).
+
+There is no fallback: if the HIP library is missing the import of any compute
+entry point raises. Build it with `python -c "import __graft_entry__ as g;
+g.build()"` (or `python -m aclswarm_amd.build`).
+"""
+import ctypes as ct
+import os
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                        "libaclswarm_amd.so")
+
+ACL_OK = 0
+
+FLAG_VALID = 0x01
+FLAG_AGREE = 0x02
+FLAG_CHANGED = 0x04
+FLAG_NONFINITE = 0x08
+FLAG_BAD_INPUT = 0x10
+FLAG_CA_ACTIVE = 0x20
+
+STATUS_DTYPE = np.dtype([("flags", "<u4"), ("eff_rounds", "<u2"),
+                         ("rounds", "<u2"), ("n_invalid", "<u2"),
+                         ("n_ca", "<u2"), ("reserved", "<u4")])
+
+# every symbol include/aclswarm_amd.h declares
+EXPORTS = (
+    "acl_default_cntrl_gains", "acl_default_safety_params", "acl_default_admm_params",
+    "acl_max_vehicles", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
+    "acl_pack_gains", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
+    "acl_malloc", "acl_free", "acl_memcpy_h2d", "acl_memcpy_d2h", "acl_memset",
+    "acl_stream_synchronize", "acl_last_error",
+)
+
+
+class CntrlGains(ct.Structure):
+    """DistCntrl::Gains (aclswarm/include/aclswarm/distcntrl.h:36-45)."""
+    _fields_ = [(n, ct.c_double) for n in
+                ("K1_xy", "K2_xy", "K1_z", "K2_z", "e_xy_thr", "e_z_thr", "kp", "kd")]
+
+
+class SafetyParams(ct.Structure):
+    """Safety velocity/avoidance parameters (aclswarm/src/safety.cpp:49-52)."""
+    _fields_ = [(n, ct.c_double) for n in
+                ("max_vel_xy", "max_vel_z", "d_avoid_thresh", "r_keep_out")]
+
+
+class AdmmParams(ct.Structure):
+    """admm::Params (aclswarm/lib/admm/include/admm/solver.h:18-31)."""
+    _fields_ = [("verbose", ct.c_int32), ("thrSparseZero", ct.c_double),
+                ("thrPlanar", ct.c_double), ("epsEig", ct.c_double),
+                ("mu", ct.c_double), ("thresh", ct.c_double),
+                ("threshTr", ct.c_double), ("maxItr", ct.c_int32)]
+
+
+class Formations(ct.Structure):
+    _fields_ = [("n", ct.c_int32), ("n_formations", ct.c_int32),
+                ("p", ct.c_void_p), ("adj", ct.c_void_p), ("gains", ct.c_void_p),
+                ("gain_off", ct.c_void_p)]
+
+
+class SolveArgs(ct.Structure):
+    _fields_ = [("B", ct.c_int32), ("fidx", ct.c_void_p), ("q", ct.c_void_p),
+                ("vel", ct.c_void_p), ("P_in", ct.c_void_p), ("P_out", ct.c_void_p),
+                ("status", ct.c_void_p), ("u", ct.c_void_p), ("u_safe", ct.c_void_p),
+                ("ca_flag", ct.c_void_p), ("who", ct.c_void_p),
+                ("cntrl", CntrlGains), ("safety", SafetyParams),
+                ("early_exit", ct.c_int32), ("do_control", ct.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libaclswarm_amd.so; raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"aclswarm_amd: native library {LIB_PATH} is missing. Build it with "
+            "`python -m aclswarm_amd.build` (hipcc --offload-arch=gfx950).")
+    L = ct.CDLL(LIB_PATH)
+    VP, I32, I64, SZ = ct.c_void_p, ct.c_int32, ct.c_int64, ct.c_size_t
+    L.acl_default_cntrl_gains.argtypes = [ct.POINTER(CntrlGains)]
+    L.acl_default_safety_params.argtypes = [ct.POINTER(SafetyParams)]
+    L.acl_default_admm_params.argtypes = [ct.POINTER(AdmmParams)]
+    L.acl_max_vehicles.restype = I32
+    L.acl_solve_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(SolveArgs), VP]
+    L.acl_solve_batch.restype = ct.c_int
+    L.acl_count_edges.argtypes = [I32, VP]
+    L.acl_count_edges.restype = I64
+    L.acl_pack_adjacency.argtypes = [I32, VP, VP]
+    L.acl_pack_adjacency.restype = ct.c_int
+    L.acl_pack_gains.argtypes = [I32, VP, VP, VP]
+    L.acl_pack_gains.restype = ct.c_int
+    L.acl_admm_solve_batch.argtypes = [I32, I32, VP, VP, VP, VP, ct.POINTER(AdmmParams), VP]
+    L.acl_admm_solve_batch.restype = ct.c_int
+    L.acl_device_count.restype = I32
+    L.acl_set_device.argtypes = [I32]
+    L.acl_set_device.restype = ct.c_int
+    L.acl_malloc.argtypes = [ct.POINTER(VP), SZ]
+    L.acl_malloc.restype = ct.c_int
+    L.acl_free.argtypes = [VP]
+    L.acl_free.restype = ct.c_int
+    for fn in ("acl_memcpy_h2d", "acl_memcpy_d2h"):
+        getattr(L, fn).argtypes = [VP, VP, SZ, VP]
+        getattr(L, fn).restype = ct.c_int
+    L.acl_memset.argtypes = [VP, ct.c_int, SZ, VP]
+    L.acl_memset.restype = ct.c_int
+    L.acl_stream_synchronize.argtypes = [VP]
+    L.acl_stream_synchronize.restype = ct.c_int
+    L.acl_last_error.restype = ct.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc, what="aclswarm_amd"):
+    if rc != ACL_OK:
+        msg = lib().acl_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def default_gains():
+    g = CntrlGains()
+    lib().acl_default_cntrl_gains(ct.byref(g))
+    return g
+
+
+def default_safety():
+    s = SafetyParams()
+    lib().acl_default_safety_params(ct.byref(s))
+    return s
+
+
+def default_admm_params():
+    a = AdmmParams()
+    lib().acl_default_admm_params(ct.byref(a))
+    return a

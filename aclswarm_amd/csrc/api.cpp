@@ -1,0 +1,114 @@
+// api.cpp -- host side of the C ABI: defaults, error string, packing of the
+// reference's Eigen layouts into the device layout, device-memory helpers.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/aclswarm_amd.h"
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+extern "C" acl_status_t acl__set_error(const char* msg) {
+  g_last_error = msg ? msg : "";
+  return ACL_ERR_INVALID_ARG;
+}
+
+static acl_status_t hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return ACL_OK;
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return ACL_ERR_HIP;
+}
+
+extern "C" const char* acl_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" void acl_default_cntrl_gains(acl_cntrl_gains_t* g) {
+  // aclswarm/launch/coordination.launch:32-39
+  g->K1_xy = 0.1; g->K2_xy = 0.1; g->K1_z = 0.5; g->K2_z = 0.3;
+  g->e_xy_thr = 0.3; g->e_z_thr = 0.1; g->kp = 1.5; g->kd = 0.5;
+}
+
+extern "C" void acl_default_safety_params(acl_safety_params_t* s) {
+  // aclswarm/src/safety.cpp:49-52
+  s->max_vel_xy = 0.5; s->max_vel_z = 0.3; s->d_avoid_thresh = 1.5; s->r_keep_out = 1.2;
+}
+
+extern "C" void acl_default_admm_params(acl_admm_params_t* a) {
+  // aclswarm/lib/admm/include/admm/solver.h:18-31
+  a->verbose = 0; a->thrSparseZero = 1e-8; a->thrPlanar = 1e-2; a->epsEig = 1e-5;
+  a->mu = 1.0; a->thresh = 1e-4; a->threshTr = 0.10; a->maxItr = 10;
+}
+
+// ---- packing -------------------------------------------------------------
+
+extern "C" int64_t acl_count_edges(int32_t n, const uint8_t* adj) {
+  if (n < 1 || !adj) return -1;
+  int64_t e = 0;
+  for (int64_t k = 0; k < (int64_t)n * n; ++k) e += adj[k] != 0;
+  return e;
+}
+
+extern "C" acl_status_t acl_pack_adjacency(int32_t n, const uint8_t* adj, uint64_t* out) {
+  if (n < 1 || !adj || !out) return acl__set_error("acl_pack_adjacency: bad argument");
+  const int W = (n + 63) / 64;
+  std::memset(out, 0, sizeof(uint64_t) * (size_t)n * W);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j)
+      if (adj[(size_t)j * n + i])  // column-major AdjMat(i,j)
+        out[(size_t)i * W + j / 64] |= 1ull << (j % 64);
+  return ACL_OK;
+}
+
+extern "C" acl_status_t acl_pack_gains(int32_t n, const uint8_t* adj, const double* gains,
+                                       double* out) {
+  if (n < 1 || !adj || !gains || !out) return acl__set_error("acl_pack_gains: bad argument");
+  const int64_t E = acl_count_edges(n, adj);
+  const size_t ld = (size_t)3 * n;  // column-major leading dimension
+  int64_t e = 0;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      if (!adj[(size_t)j * n + i]) continue;
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+          out[(size_t)(3 * r + c) * E + e] = gains[(3 * (size_t)j + c) * ld + 3 * (size_t)i + r];
+      ++e;
+    }
+  return ACL_OK;
+}
+
+// ---- device memory -------------------------------------------------------
+
+extern "C" int32_t acl_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+extern "C" acl_status_t acl_set_device(int32_t d) { return hip_check(hipSetDevice(d), "hipSetDevice"); }
+
+extern "C" acl_status_t acl_malloc(void** ptr, size_t bytes) {
+  return hip_check(hipMalloc(ptr, bytes), "hipMalloc");
+}
+
+extern "C" acl_status_t acl_free(void* ptr) { return hip_check(hipFree(ptr), "hipFree"); }
+
+extern "C" acl_status_t acl_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+  return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream),
+                   "hipMemcpyAsync(H2D)");
+}
+
+extern "C" acl_status_t acl_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+  return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream),
+                   "hipMemcpyAsync(D2H)");
+}
+
+extern "C" acl_status_t acl_memset(void* dst, int value, size_t bytes, void* stream) {
+  return hip_check(hipMemsetAsync(dst, value, bytes, (hipStream_t)stream), "hipMemsetAsync");
+}
+
+extern "C" acl_status_t acl_stream_synchronize(void* stream) {
+  return hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+}

@@ -1,0 +1,190 @@
+// umeyama_dev.h -- device-side 2-D Umeyama alignment for the CBAA kernel.
+//
+// Auctioneer::alignFormation (aclswarm/src/auctioneer.cpp:347-415) calls
+// Eigen::umeyama(p_xy, q_xy, false) on the vehicle's closed formation
+// neighbourhood. Eigen (unpinned, "3.2.2 or later", CMakeLists.txt:30-32) is
+// not in the image; DESIGN.md §3 states the Eigen 3.3.4 algorithm this file
+// implements. Every expression keeps Eigen's operation order; the library is
+// compiled with -ffp-contract=off so no FMA contraction changes a rounding.
+// One thread computes one vehicle's (R, t) in registers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <float.h>
+
+namespace acl_amd {
+
+// apply_rotation_in_the_plane(row p, row q, (c,s)) on a column-major 2x2
+// (MatrixBase::applyOnTheLeft); the c==1 && s==0 early return is kept.
+__device__ __forceinline__ void rot_rows(double* W, int p, int q, double c, double s) {
+  if (c == 1.0 && s == 0.0) return;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const double xi = W[p + 2 * k], yi = W[q + 2 * k];
+    W[p + 2 * k] = c * xi + s * yi;
+    W[q + 2 * k] = -s * xi + c * yi;
+  }
+}
+
+// apply_rotation_in_the_plane(col p, col q, (c,s)) (applyOnTheRight).
+__device__ __forceinline__ void rot_cols(double* M, int p, int q, double c, double s) {
+  if (c == 1.0 && s == 0.0) return;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const double xi = M[k + 2 * p], yi = M[k + 2 * q];
+    M[k + 2 * p] = c * xi + s * yi;
+    M[k + 2 * q] = -s * xi + c * yi;
+  }
+}
+
+// JacobiRotation::makeJacobi(x, y, z), real case.
+__device__ __forceinline__ void make_jacobi(double x, double y, double z, double& c, double& s) {
+  const double deno = 2.0 * fabs(y);
+  if (deno < DBL_MIN) {
+    c = 1.0;
+    s = 0.0;
+    return;
+  }
+  const double tau = (x - z) / deno;
+  const double w = sqrt(tau * tau + 1.0);
+  const double t = (tau > 0.0) ? 1.0 / (tau + w) : 1.0 / (tau - w);
+  const double sign_t = t > 0.0 ? 1.0 : -1.0;
+  const double n = 1.0 / sqrt(t * t + 1.0);
+  s = -sign_t * (y / fabs(y)) * fabs(t) * n;
+  c = n;
+}
+
+// PartialPivLU determinant of a dynamic 2x2 (only its sign is consumed).
+__device__ __forceinline__ double det2_lu(const double* A) {
+  double a00 = A[0], a10 = A[1], a01 = A[2], a11 = A[3];
+  double sign = 1.0;
+  const double b0 = fabs(a00), b1 = fabs(a10);
+  const bool piv = b1 > b0;
+  const double biggest = piv ? b1 : b0;
+  if (biggest != 0.0) {
+    if (piv) {
+      double t = a00; a00 = a10; a10 = t;
+      t = a01; a01 = a11; a11 = t;
+      sign = -1.0;
+    }
+    a10 = a10 / a00;
+  }
+  a11 = a11 - a10 * a01;
+  return (a00 * a11) * sign;
+}
+
+// JacobiSVD<MatrixXd>(A, ComputeFullU | ComputeFullV) for 2x2 A (column-major).
+// Returns false when A is not finite (Eigen: InvalidInput).
+__device__ inline bool jacobi_svd2(const double* A, double* U, double* sv, double* V) {
+  const double precision = 2.0 * DBL_EPSILON;
+  const double considerAsZero = DBL_MIN;
+  double scale = fabs(A[0]);
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    const double a = fabs(A[i]);
+    if (a > scale || isnan(a)) scale = a;
+  }
+  if (!isfinite(scale)) return false;
+  if (scale == 0.0) scale = 1.0;
+  double W[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) W[i] = A[i] / scale;
+  U[0] = 1.0; U[1] = 0.0; U[2] = 0.0; U[3] = 1.0;
+  V[0] = 1.0; V[1] = 0.0; V[2] = 0.0; V[3] = 1.0;
+  double maxDiag = fabs(W[0]);
+  if (maxDiag < fabs(W[3])) maxDiag = fabs(W[3]);
+  // Each sweep of a 2x2 is one (p=1, q=0) rotation; the loop ends when the
+  // off-diagonal is below threshold (at most a few sweeps; bounded for safety).
+  for (int sweep = 0; sweep < 64; ++sweep) {
+    double threshold = precision * maxDiag;
+    if (threshold < considerAsZero) threshold = considerAsZero;
+    if (!(fabs(W[1]) > threshold || fabs(W[2]) > threshold)) break;
+    // real_2x2_jacobi_svd(W, 1, 0): m = [W11 W10; W01 W00]
+    double m[4];
+    m[0] = W[3];
+    m[2] = W[1];
+    m[1] = W[2];
+    m[3] = W[0];
+    double c1, s1;
+    const double t = m[0] + m[3];
+    const double d = m[1] - m[2];
+    if (fabs(d) < DBL_MIN) {
+      s1 = 0.0;
+      c1 = 1.0;
+    } else {
+      const double u = t / d;
+      const double tmp = sqrt(1.0 + u * u);
+      s1 = 1.0 / tmp;
+      c1 = u / tmp;
+    }
+    rot_rows(m, 0, 1, c1, s1);
+    double cr, sr;
+    make_jacobi(m[0], m[2], m[3], cr, sr);
+    const double ocs = -sr;
+    const double cl = c1 * cr - s1 * ocs;
+    const double sl = c1 * ocs + s1 * cr;
+    rot_rows(W, 1, 0, cl, sl);
+    rot_cols(U, 1, 0, cl, sl);
+    rot_cols(W, 1, 0, cr, -sr);
+    rot_cols(V, 1, 0, cr, -sr);
+    double md = fabs(W[3]);
+    if (md < fabs(W[0])) md = fabs(W[0]);
+    if (maxDiag < md) maxDiag = md;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double a = W[i * 3];
+    sv[i] = fabs(a);
+    if (a < 0.0) {
+      U[2 * i] = -U[2 * i];
+      U[2 * i + 1] = -U[2 * i + 1];
+    }
+  }
+  sv[0] *= scale;
+  sv[1] *= scale;
+  const bool pos = sv[1] > sv[0];
+  const double mx = pos ? sv[1] : sv[0];
+  if (mx != 0.0 && pos) {
+    double t = sv[0]; sv[0] = sv[1]; sv[1] = t;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      t = U[k]; U[k] = U[2 + k]; U[2 + k] = t;
+      t = V[k]; V[k] = V[2 + k]; V[2 + k] = t;
+    }
+  }
+  return true;
+}
+
+// Finishes Eigen::umeyama (3.3.x rank rule) from the means and the
+// accumulated cross-covariance. R row-major 2x2, t[2].
+__device__ inline bool umeyama_finish(const double* S, const double* sm, const double* dm,
+                                      double* R, double* t) {
+  double U[4], V[4], sv[2];
+  if (!jacobi_svd2(S, U, sv, V)) {
+    const double nan = __builtin_nan("");
+    R[0] = R[1] = R[2] = R[3] = nan;
+    t[0] = t[1] = nan;
+    return false;
+  }
+  double s1 = (det2_lu(S) < 0.0) ? -1.0 : 1.0;
+  int rank = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    if (!(fabs(sv[i]) <= fabs(sv[0]) * 1e-12)) ++rank;
+  if (rank == 1) s1 = (det2_lu(U) * det2_lu(V) > 0.0) ? 1.0 : -1.0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      R[2 * i + j] = (U[i] * 1.0) * V[j] + (U[i + 2] * s1) * V[j + 2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    double ti = dm[i];
+    ti = ti + R[2 * i + 0] * (-sm[0]);
+    ti = ti + R[2 * i + 1] * (-sm[1]);
+    t[i] = ti;
+  }
+  return true;
+}
+
+}  // namespace acl_amd

@@ -1,0 +1,121 @@
+"""Host-side driver of the batched engine (device memory via torch tensors).
+
+The C ABI (include/aclswarm_amd.h) takes raw device pointers; this module
+packs the reference's formation data (points / adjmat / GainMat, the fields of
+DistCntrl::Formation, aclswarm/include/aclswarm/distcntrl.h:26-34) into the
+device layout and calls acl_solve_batch on the current torch stream.
+"""
+import ctypes as ct
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+def _ptr(t):
+    return ct.c_void_p(t.data_ptr()) if t is not None else ct.c_void_p(0)
+
+
+def pack_formation_host(points, adj, gains=None):
+    """One formation -> (p [n][3], adj bits [n][W] u64, gain planes [9*E] f64).
+
+    points [n][3]; adj [n][n] with adj[i][j] = adjmat(i,j); gains [3n][3n]
+    with gains[r][c] = GainMat(r,c). Uses the ABI's packers, which take the
+    reference's column-major Eigen layouts.
+    """
+    lib = L.lib()
+    points = np.ascontiguousarray(points, dtype=np.float64)
+    n = points.shape[0]
+    adj_cm = np.ascontiguousarray(np.asarray(adj, dtype=np.uint8).T)
+    W = (n + 63) // 64
+    bits = np.zeros((n, W), np.uint64)
+    L.check(lib.acl_pack_adjacency(n, adj_cm.ctypes.data, bits.ctypes.data), "pack_adjacency")
+    E = int(lib.acl_count_edges(n, adj_cm.ctypes.data))
+    planes = np.zeros(9 * E, np.float64)
+    if gains is not None:
+        g_cm = np.ascontiguousarray(np.asarray(gains, dtype=np.float64).T)
+        L.check(lib.acl_pack_gains(n, adj_cm.ctypes.data, g_cm.ctypes.data,
+                                   planes.ctypes.data), "pack_gains")
+    return points, bits, planes, E
+
+
+class FormationTable:
+    """Device formation table (acl_formations_t): F formations of n points."""
+
+    def __init__(self, n, p, adj_bits, gains, gain_off):
+        self.n = int(n)
+        self.p = p
+        self.adj = adj_bits
+        self.gains = gains
+        self.gain_off = gain_off
+        self.F = int(p.shape[0])
+
+    @classmethod
+    def from_host(cls, points, adjs, gains=None, device="cuda"):
+        F = len(points)
+        ps, bs, gs, offs = [], [], [], []
+        off = 0
+        for f in range(F):
+            p, b, g, E = pack_formation_host(points[f], adjs[f],
+                                             None if gains is None else gains[f])
+            ps.append(p); bs.append(b); gs.append(g); offs.append(off)
+            off += E
+        n = ps[0].shape[0]
+        p = torch.from_numpy(np.stack(ps)).to(device)
+        bits = torch.from_numpy(np.stack(bs).view(np.int64)).to(device)
+        g = torch.from_numpy(np.concatenate(gs) if gs else np.zeros(0)).to(device)
+        goff = torch.tensor(offs, dtype=torch.int64, device=device)
+        return cls(n, p, bits, g, goff)
+
+    def struct(self):
+        return L.Formations(self.n, self.F, self.p.data_ptr(), self.adj.data_ptr(),
+                            self.gains.data_ptr() if self.gains.numel() else 0,
+                            self.gain_off.data_ptr())
+
+
+def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
+          do_control=True, want_who=False, out=None, stream=None):
+    """Run acl_solve_batch for B = q.shape[0] swarms. All tensors on device.
+
+    fidx [B] int32, q/vel [B][n][3] f64, P_in [B][n] int16 (uint16 bits).
+    Returns a dict of device tensors: P_out, status (raw 16-byte records as
+    uint8 [B][16]), u, u_safe, ca_flag, who (if requested).
+    """
+    lib = L.lib()
+    B, n = int(q.shape[0]), table.n
+    dev = q.device
+    if out is None:
+        out = {
+            "P_out": torch.empty((B, n), dtype=torch.int16, device=dev),
+            "status": torch.empty((B, 16), dtype=torch.uint8, device=dev),
+            "u": torch.empty((B, n, 3), dtype=torch.float64, device=dev),
+            "u_safe": torch.empty((B, n, 3), dtype=torch.float64, device=dev),
+            "ca_flag": torch.empty((B, n), dtype=torch.uint8, device=dev),
+        }
+        if want_who:
+            out["who"] = torch.empty((B, n, n), dtype=torch.int16, device=dev)
+    a = L.SolveArgs()
+    a.B = B
+    a.fidx = fidx.data_ptr(); a.q = q.data_ptr(); a.vel = vel.data_ptr()
+    a.P_in = P_in.data_ptr(); a.P_out = out["P_out"].data_ptr()
+    a.status = out["status"].data_ptr()
+    a.u = out["u"].data_ptr() if out.get("u") is not None else None
+    a.u_safe = out["u_safe"].data_ptr() if out.get("u_safe") is not None else None
+    a.ca_flag = out["ca_flag"].data_ptr() if out.get("ca_flag") is not None else None
+    a.who = out["who"].data_ptr() if out.get("who") is not None else None
+    a.cntrl = cntrl or L.default_gains()
+    a.safety = safety or L.default_safety()
+    a.early_exit = int(bool(early_exit))
+    a.do_control = int(bool(do_control))
+    F = table.struct()
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    L.check(lib.acl_solve_batch(ct.byref(F), ct.byref(a), ct.c_void_p(stream)), "acl_solve_batch")
+    return out
+
+
+def status_to_numpy(status_u8):
+    """[B][16] uint8 device/host tensor -> structured numpy array."""
+    arr = status_u8.detach().cpu().numpy()
+    return np.ascontiguousarray(arr).view(L.STATUS_DTYPE).reshape(-1)

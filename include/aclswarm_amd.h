@@ -1,0 +1,226 @@
+/*
+ * aclswarm_amd.h -- C ABI of the MI355X-native batched swarm-decision engine.
+ *
+ * This is the drop-in boundary for aclswarm's per-vehicle decision loop
+ * (reference: gitshitou/aclswarm). Every entry point is plain C: device or
+ * host pointers plus sizes, no C++/Eigen/torch types. Each declaration cites
+ * the reference interface it replaces (paths relative to the reference root).
+ *
+ *   reference                                    this ABI
+ *   -------------------------------------------  ----------------------------------
+ *   Auctioneer::setFormation/start/.../          acl_solve_batch (auction part):
+ *     processBid -> consensus -> P               B swarms x N vehicles in one call
+ *     (aclswarm/src/auctioneer.cpp:42-306)
+ *   DistCntrl::setFormation + compute            acl_solve_batch (control part)
+ *     (aclswarm/src/distcntrl.cpp:28-102)
+ *   Safety::cmdinCb saturation +                 acl_solve_batch (safety part)
+ *     Safety::collisionAvoidance
+ *     (aclswarm/src/safety.cpp:172-197,412-541)
+ *   admm::Solver::solve                          acl_admm_solve_batch
+ *     (aclswarm/lib/admm/src/solver.cpp:28-79)
+ *   utils::pdistmat (aclswarm/include/aclswarm/utils.h:137-147)
+ *                                                computed on device from p
+ *
+ * Layouts. The batched engine uses its own device layout, documented per
+ * field below (row-major "xyz per vehicle" points, adjacency bitmasks, gain
+ * blocks as 9 coalesced edge planes). acl_pack_* convert the reference's
+ * column-major Eigen layouts (PtsMat n x 3, AdjMat n x n u8, GainMat 3n x 3n)
+ * into it on the host.
+ *
+ * Index width. The reference uses uint8_t vehicle indices
+ * (utils.h:25-30, vehidx_t), so N <= 255. The ABI widens indices to
+ * uint16_t; for N <= 255 the semantics are identical ("who == -1" casts to
+ * 0xFFFF here instead of 0xFF).
+ *
+ * Errors. The reference has no error channel (asserts compiled out in
+ * Release, aclswarm/CMakeLists.txt:7-10); an invalid auction is a flag
+ * (auctioneer.cpp:283-292). Here: argument errors return acl_status_t != 0,
+ * per-swarm outcomes are flags in acl_swarm_status_t.
+ *
+ * Concurrency. All device entry points are stream-ordered on the hipStream_t
+ * passed as `void* stream` (NULL = default stream) and never synchronize.
+ */
+#ifndef ACLSWARM_AMD_H
+#define ACLSWARM_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACL_ABI_VERSION 1
+
+typedef enum {
+  ACL_OK = 0,
+  ACL_ERR_INVALID_ARG = 1,
+  ACL_ERR_UNSUPPORTED = 2, /* e.g. N above the kernel's supported maximum */
+  ACL_ERR_HIP = 3,         /* a HIP runtime call failed */
+  ACL_ERR_NO_DEVICE = 4
+} acl_status_t;
+
+/* DistCntrl::Gains (aclswarm/include/aclswarm/distcntrl.h:36-45). */
+typedef struct {
+  double K1_xy, K2_xy, K1_z, K2_z, e_xy_thr, e_z_thr, kp, kd;
+} acl_cntrl_gains_t;
+
+/* Safety parameters used by cmdinCb + collisionAvoidance
+ * (aclswarm/src/safety.cpp:49-52). */
+typedef struct {
+  double max_vel_xy, max_vel_z, d_avoid_thresh, r_keep_out;
+} acl_safety_params_t;
+
+/* admm::Params (aclswarm/lib/admm/include/admm/solver.h:18-31). */
+typedef struct {
+  int32_t verbose;
+  double thrSparseZero;
+  double thrPlanar;
+  double epsEig;
+  double mu;
+  double thresh;
+  double threshTr;
+  int32_t maxItr;
+} acl_admm_params_t;
+
+/* Defaults: control gains from aclswarm/launch/coordination.launch:32-39,
+ * safety from safety.cpp:49-52, ADMM from solver.h:18-31. */
+void acl_default_cntrl_gains(acl_cntrl_gains_t* g);
+void acl_default_safety_params(acl_safety_params_t* s);
+void acl_default_admm_params(acl_admm_params_t* a);
+
+/* ---- per-swarm outcome ------------------------------------------------- */
+#define ACL_SWARM_VALID     0x01u /* every vehicle's final table is a permutation
+                                     (isValidAssignment, auctioneer.cpp:325-343) */
+#define ACL_SWARM_AGREE     0x02u /* all vehicles hold identical final tables */
+#define ACL_SWARM_CHANGED   0x04u /* some vehicle adopted an assignment != P_in */
+#define ACL_SWARM_NONFINITE 0x08u /* a bid price was NaN: exact ordered-scan path */
+#define ACL_SWARM_BAD_INPUT 0x10u /* P_in not a permutation: swarm skipped */
+#define ACL_SWARM_CA_ACTIVE 0x20u /* collision avoidance modified >= 1 command */
+
+typedef struct {
+  uint32_t flags;
+  uint16_t eff_rounds; /* last CBAA round that changed any table (0..2N); the
+                          state is a fixed point after it */
+  uint16_t rounds;     /* the reference's round count, n * diameter = 2N
+                          (auctioneer.cpp:50-51, 441-444) */
+  uint16_t n_invalid;  /* vehicles whose final table is not a permutation */
+  uint16_t n_ca;       /* vehicles whose command collision avoidance modified */
+  uint32_t reserved;
+} acl_swarm_status_t; /* 16 bytes */
+
+/* ---- formation table (device memory) ------------------------------------
+ * Replaces DistCntrl::Formation (distcntrl.h:26-34) + Auctioneer::p_/adjmat_.
+ * One table holds F formations of n vehicles; swarms index it by fidx.
+ *   p        [F][n][3] f64   desired points (Formation::qdes), xyz per point
+ *   adj      [F][n][W] u64   W = (n+63)/64; bit (j%64) of word (j/64) of row i
+ *                            is adjmat(i,j). The diagonal is ignored.
+ *   gains    f64 edge planes. Formation f has E_f directed edges (i,j) with
+ *            adjmat(i,j)=1, i != j, enumerated row-major (i, then j
+ *            ascending). Block A_ij = GainMat.block<3,3>(3i,3j)
+ *            (distcntrl.cpp:66) is stored as 9 planes: element (r,c) of edge e
+ *            at gains[9*gain_off[f] + (3r+c)*E_f + e].
+ *   gain_off [F] i64         edge offset of formation f (prefix sum of E_f).
+ */
+typedef struct {
+  int32_t n;
+  int32_t n_formations;
+  const double* p;
+  const uint64_t* adj;
+  const double* gains;
+  const int64_t* gain_off;
+} acl_formations_t;
+
+/* ---- the batched solve --------------------------------------------------
+ * One "solve" = for one swarm of n vehicles:
+ *   (1) each vehicle's local 2-D Umeyama alignment of the formation to its
+ *       neighbours (Auctioneer::alignFormation, auctioneer.cpp:347-415),
+ *   (2) CBAA to consensus in lockstep-equivalent rounds
+ *       (start/processBid/updateTaskAssignment/selectTaskAssignment,
+ *       auctioneer.cpp:78-306,469-549), exact early exit at the fixed point,
+ *   (3) adoption (isValidAssignment, auctioneer.cpp:250-295),
+ *   (4) one DistCntrl::compute per vehicle with its adopted assignment
+ *       (distcntrl.cpp:46-102),
+ *   (5) Safety::cmdinCb saturation and Safety::collisionAvoidance
+ *       (safety.cpp:172-197, 412-541).
+ * All pointers are device pointers.
+ *   fidx    [B]        formation of swarm b (0 <= fidx < F)
+ *   q       [B][n][3]  vehicle positions, vehicle space (PtsMat q, one row
+ *                      per vehicle)
+ *   vel     [B][n][3]  vehicle velocities (the controller's damping input)
+ *   P_in    [B][n]     assignment before the auction: vehicle -> formation
+ *                      point (AssignmentPerm::indices())
+ *   P_out   [B][n]     per-vehicle adopted formation point: the assignment
+ *                      vehicle v adopts (its own table if valid, else P_in),
+ *                      evaluated at v. Equals the consensus P when AGREE.
+ *   status  [B]
+ *   u       [B][n][3]  DistCntrl::compute (NULL to skip storing)
+ *   u_safe  [B][n][3]  after saturation and collision avoidance (NULL ok)
+ *   ca_flag [B][n]     VelocityGoal::modified (NULL ok)
+ *   who     [B][n][n]  optional final CBAA tables, vehicle rows (NULL ok);
+ *                      0xFFFF = unassigned (who == -1)
+ */
+typedef struct {
+  int32_t B;
+  const int32_t* fidx;
+  const double* q;
+  const double* vel;
+  const uint16_t* P_in;
+  uint16_t* P_out;
+  acl_swarm_status_t* status;
+  double* u;
+  double* u_safe;
+  uint8_t* ca_flag;
+  uint16_t* who;
+  acl_cntrl_gains_t cntrl;
+  acl_safety_params_t safety;
+  int32_t early_exit; /* 1: stop at the first fixed point (bit-exact), 0: run
+                         all 2N rounds like the reference */
+  int32_t do_control; /* 0: auction only */
+} acl_solve_args_t;
+
+/* Largest n the batched solve kernel accepts. */
+int32_t acl_max_vehicles(void);
+
+acl_status_t acl_solve_batch(const acl_formations_t* formations,
+                             const acl_solve_args_t* args, void* stream);
+
+/* ---- host-side packing helpers (reference layouts -> device layout) ----- */
+/* Number of directed edges (i != j, adjmat(i,j) != 0); adj is the
+ * reference's column-major AdjMat (n x n u8). */
+int64_t acl_count_edges(int32_t n, const uint8_t* adj_colmajor);
+/* AdjMat (column-major n x n u8) -> [n][W] u64 bit rows. */
+acl_status_t acl_pack_adjacency(int32_t n, const uint8_t* adj_colmajor,
+                                uint64_t* out_bits);
+/* GainMat (column-major 3n x 3n f64) -> 9 edge planes of E doubles
+ * (E = acl_count_edges). */
+acl_status_t acl_pack_gains(int32_t n, const uint8_t* adj_colmajor,
+                            const double* gains_colmajor, double* out_planes);
+
+/* ---- ADMM formation-gain design (admm::Solver::solve, solver.cpp:28-79) -
+ * F formations of n points: pts [F][3][n] column-major 3 x n per formation
+ * (Eigen::Matrix<double,3,Dynamic>), adj [F][n][n] f64 (symmetric 0/1),
+ * gains out [F][3n][3n] column-major. Device pointers. iters [F][2]
+ * (2-D and 1-D ADMM iteration counts, may be NULL). */
+acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double* pts,
+                                  const double* adj, double* gains,
+                                  int32_t* iters,
+                                  const acl_admm_params_t* params,
+                                  void* stream);
+
+/* ---- minimal device-memory helpers (for callers without a framework) ---- */
+int32_t acl_device_count(void);
+acl_status_t acl_set_device(int32_t device);
+acl_status_t acl_malloc(void** ptr, size_t bytes);
+acl_status_t acl_free(void* ptr);
+acl_status_t acl_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+acl_status_t acl_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+acl_status_t acl_memset(void* dst, int value, size_t bytes, void* stream);
+acl_status_t acl_stream_synchronize(void* stream);
+const char* acl_last_error(void);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* ACLSWARM_AMD_H */
