@@ -64,14 +64,16 @@ class FormationTable:
         n = ps[0].shape[0]
         p = torch.from_numpy(np.stack(ps)).to(device)
         bits = torch.from_numpy(np.stack(bs).view(np.int64)).to(device)
-        g = torch.from_numpy(np.concatenate(gs) if gs else np.zeros(0)).to(device)
+        g = np.concatenate(gs) if gs else np.zeros(0)
+        if g.size == 0:  # the ABI wants a valid pointer even with no edges
+            g = np.zeros(9)
+        g = torch.from_numpy(g).to(device)
         goff = torch.tensor(offs, dtype=torch.int64, device=device)
         return cls(n, p, bits, g, goff)
 
     def struct(self):
         return L.Formations(self.n, self.F, self.p.data_ptr(), self.adj.data_ptr(),
-                            self.gains.data_ptr() if self.gains.numel() else 0,
-                            self.gain_off.data_ptr())
+                            self.gains.data_ptr(), self.gain_off.data_ptr())
 
 
 def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,

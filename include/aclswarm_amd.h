@@ -114,10 +114,12 @@ typedef struct {
  * One table holds F formations of n vehicles; swarms index it by fidx.
  *   p        [F][n][3] f64   desired points (Formation::qdes), xyz per point
  *   adj      [F][n][W] u64   W = (n+63)/64; bit (j%64) of word (j/64) of row i
- *                            is adjmat(i,j). The diagonal is ignored.
+ *                            is adjmat(i,j). The auction uses the closed
+ *                            neighbourhood (the diagonal does not matter).
  *   gains    f64 edge planes. Formation f has E_f directed edges (i,j) with
- *            adjmat(i,j)=1, i != j, enumerated row-major (i, then j
- *            ascending). Block A_ij = GainMat.block<3,3>(3i,3j)
+ *            adjmat(i,j) != 0, enumerated row-major (i, then j ascending);
+ *            a diagonal entry is an edge of the control law too
+ *            (distcntrl.cpp:62 does not skip j == i). Block A_ij = GainMat.block<3,3>(3i,3j)
  *            (distcntrl.cpp:66) is stored as 9 planes: element (r,c) of edge e
  *            at gains[9*gain_off[f] + (3r+c)*E_f + e].
  *   gain_off [F] i64         edge offset of formation f (prefix sum of E_f).
@@ -186,7 +188,7 @@ acl_status_t acl_solve_batch(const acl_formations_t* formations,
                              const acl_solve_args_t* args, void* stream);
 
 /* ---- host-side packing helpers (reference layouts -> device layout) ----- */
-/* Number of directed edges (i != j, adjmat(i,j) != 0); adj is the
+/* Number of directed edges (adjmat(i,j) != 0, diagonal included); adj is the
  * reference's column-major AdjMat (n x n u8). */
 int64_t acl_count_edges(int32_t n, const uint8_t* adj_colmajor);
 /* AdjMat (column-major n x n u8) -> [n][W] u64 bit rows. */

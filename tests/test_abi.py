@@ -1,0 +1,96 @@
+"""CPU suite: the C-ABI library loads, exports every declared symbol, its host
+helpers are correct, and argument errors are reported without a GPU."""
+import ctypes as ct
+import os
+import re
+
+import numpy as np
+
+import helpers as H
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    with open(os.path.join(ROOT, "include", "aclswarm_amd.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(acl_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from aclswarm_amd import _lib as L
+    lib = L.lib()
+    syms = _declared_symbols()
+    assert len(syms) >= 17
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(syms) == set(L.EXPORTS)
+
+
+def test_defaults_match_reference_values():
+    from aclswarm_amd import _lib as L
+    g = L.default_gains()  # coordination.launch:32-39
+    assert (g.K1_xy, g.K2_xy, g.K1_z, g.K2_z, g.e_xy_thr, g.e_z_thr, g.kp, g.kd) == \
+        (0.1, 0.1, 0.5, 0.3, 0.3, 0.1, 1.5, 0.5)
+    s = L.default_safety()  # safety.cpp:49-52
+    assert (s.max_vel_xy, s.max_vel_z, s.d_avoid_thresh, s.r_keep_out) == (0.5, 0.3, 1.5, 1.2)
+    a = L.default_admm_params()  # solver.h:18-31
+    assert (a.thrSparseZero, a.thrPlanar, a.epsEig, a.mu, a.thresh, a.threshTr, a.maxItr) == \
+        (1e-8, 1e-2, 1e-5, 1.0, 1e-4, 0.10, 10)
+    assert L.lib().acl_max_vehicles() == 128
+
+
+def test_pack_adjacency_and_gains():
+    from aclswarm_amd import engine
+    pts, adj, gains, _ = H.swarm6()
+    for f in range(3):
+        A = adj[f].copy()
+        A[2, 2] = 1  # a diagonal entry is an edge of the control law
+        p, bits, planes, E = engine.pack_formation_host(pts[f], A, gains[f])
+        n = 6
+        assert E == int(A.sum())
+        for i in range(n):
+            for j in range(n):
+                assert bool((int(bits[i, 0]) >> j) & 1) == bool(A[i, j])
+        e = 0
+        for i in range(n):
+            for j in range(n):
+                if A[i, j]:
+                    blk = gains[f][3 * i:3 * i + 3, 3 * j:3 * j + 3]
+                    np.testing.assert_array_equal(planes.reshape(9, E)[:, e], blk.reshape(9))
+                    e += 1
+    # n > 64: two words per row
+    rng = np.random.RandomState(0)
+    n = 100
+    A = (rng.uniform(size=(n, n)) < 0.9).astype(np.uint8)
+    _, bits, _, E = engine.pack_formation_host(np.zeros((n, 3)), A, None)
+    assert bits.shape == (n, 2) and E == int(A.sum())
+    for i in range(0, n, 7):
+        row = [(int(bits[i, j // 64]) >> (j % 64)) & 1 for j in range(n)]
+        assert row == list(A[i])
+
+
+def test_solve_batch_argument_errors_without_gpu():
+    from aclswarm_amd import _lib as L
+    lib = L.lib()
+    F = L.Formations(0, 1, None, None, None, None)
+    a = L.SolveArgs()
+    a.B = 1
+    rc = lib.acl_solve_batch(ct.byref(F), ct.byref(a), None)
+    assert rc == 1 and b"n out of range" in lib.acl_last_error()
+    F.n = 129
+    assert lib.acl_solve_batch(ct.byref(F), ct.byref(a), None) == 1
+    F.n = 10
+    assert lib.acl_solve_batch(ct.byref(F), ct.byref(a), None) == 1  # NULL pointers
+    assert b"NULL" in lib.acl_last_error()
+    a.B = 0
+    assert lib.acl_solve_batch(ct.byref(F), ct.byref(a), None) == 0  # empty batch
+    a.B = -1
+    assert lib.acl_solve_batch(ct.byref(F), ct.byref(a), None) == 1
+    assert lib.acl_solve_batch(None, ct.byref(a), None) == 1
+
+
+def test_status_record_is_16_bytes():
+    from aclswarm_amd import _lib as L
+    assert L.STATUS_DTYPE.itemsize == 16
