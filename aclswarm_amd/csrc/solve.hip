@@ -47,21 +47,24 @@ constexpr double kPi = 3.14159265358979323846;
 
 struct Layout {
   // byte offsets into the dynamic LDS block (all 16-byte aligned)
-  int q, p, out, adjF, vadj, H, C, T0, T1, Pin, Ptin, wst, tie, myi, valid, rowptr, misc;
+  int q, p, qf, out, adjF, vadj, H, C, T0, T1, Pin, Ptin, cao, myi, valid, rowptr, misc;
   int total;
 };
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+
+constexpr int kLevels = 3;  // price levels tracked per dirty column
 
 __host__ __device__ inline Layout make_layout(int n) {
   Layout L;
   int o = 0;
   L.q = o;      o = align16(o + n * 3 * 8);
   L.p = o;      o = align16(o + n * 3 * 8);
+  L.qf = o;     o = align16(o + n * 2 * 8);   // q_xy in formation space
   L.out = o;    o = align16(o + n * 6 * 8);   // R,t per vehicle; later u, u_safe
   L.adjF = o;   o = align16(o + n * 2 * 8);
   L.vadj = o;   o = align16(o + n * 2 * 8);
-  L.H = o;      o = align16(o + n * 2 * 8);
+  L.H = o;      o = align16(o + 64 + n);      // CBAA masks + per-column buffer index
   L.C = o;
   {
     const int csz = (n + 1) * n * 4;
@@ -72,8 +75,7 @@ __host__ __device__ inline Layout make_layout(int n) {
   L.T1 = o;     o = align16(o + n * n);
   L.Pin = o;    o = align16(o + n);
   L.Ptin = o;   o = align16(o + n);
-  L.wst = o;    o = align16(o + n);
-  L.tie = o;    o = align16(o + n);
+  L.cao = o;    o = align16(o + n);
   L.myi = o;    o = align16(o + n);
   L.valid = o;  o = align16(o + n);
   L.rowptr = o; o = align16(o + (n + 1) * 4);
@@ -102,24 +104,76 @@ struct SolveParams {
   acl_safety_params_t s;
   int early_exit;
   int do_control;
+  unsigned long long* stamps;  // diagnostic: [B][16] s_memtime at phase ends (NULL = off)
 };
 
 // misc int slots
 enum { M_BAD = 0, M_NONFIN = 1, M_CHG0 = 2, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 8 };
 
-__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long y = __shfl_xor(x, o, 64);
-    x = y > x ? y : x;
-  }
-  return x;
+// Wave64 reductions on DPP (VALU lane shuffles, no LDS round trip):
+// quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, 8 give every lane its row's
+// result; row_bcast15 / row_bcast31 fold rows 0-3 into lane 63.
+// Callers must have all 64 lanes active.
+#define ACL_DPP_STEP(x, op, ctrl, rmask)                                                   \
+  x = op(x, __builtin_amdgcn_update_dpp(x, x, ctrl, rmask, 0xF, false))
+
+__device__ __forceinline__ unsigned umax32(unsigned a, int b) { return a > (unsigned)b ? a : (unsigned)b; }
+
+__device__ __forceinline__ unsigned wave_max_u32(unsigned ux) {
+  int x = (int)ux;
+#define ACL_UMAX(a, b) (int)umax32((unsigned)(a), (b))
+  ACL_DPP_STEP(x, ACL_UMAX, 0xB1, 0xF);
+  ACL_DPP_STEP(x, ACL_UMAX, 0x4E, 0xF);
+  ACL_DPP_STEP(x, ACL_UMAX, 0x124, 0xF);
+  ACL_DPP_STEP(x, ACL_UMAX, 0x128, 0xF);
+  ACL_DPP_STEP(x, ACL_UMAX, 0x142, 0xA);
+  ACL_DPP_STEP(x, ACL_UMAX, 0x143, 0xC);
+#undef ACL_UMAX
+  return (unsigned)__builtin_amdgcn_readlane(x, 63);
 }
 
+__device__ __forceinline__ float wave_max_f32(float fx) {
+  int x = __float_as_int(fx);
+#define ACL_FMAX(a, b) __float_as_int(fmaxf(__int_as_float(a), __int_as_float(b)))
+  ACL_DPP_STEP(x, ACL_FMAX, 0xB1, 0xF);
+  ACL_DPP_STEP(x, ACL_FMAX, 0x4E, 0xF);
+  ACL_DPP_STEP(x, ACL_FMAX, 0x124, 0xF);
+  ACL_DPP_STEP(x, ACL_FMAX, 0x128, 0xF);
+  ACL_DPP_STEP(x, ACL_FMAX, 0x142, 0xA);
+  ACL_DPP_STEP(x, ACL_FMAX, 0x143, 0xC);
+#undef ACL_FMAX
+  return __int_as_float(__builtin_amdgcn_readlane(x, 63));
+}
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x) {
+  const unsigned hi = (unsigned)(x >> 32), lo = (unsigned)x;
+  const unsigned mh = wave_max_u32(hi);
+  const unsigned ml = wave_max_u32(hi == mh ? lo : 0u);
+  return ((unsigned long long)mh << 32) | ml;
+}
+
+// DPP move of a double; lanes outside RMASK read 0 (the sum's identity).
+template <int CTRL, int RMASK>
+__device__ __forceinline__ double dpp_f64_z(double x) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)u, CTRL, RMASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, RMASK, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// Sum over the wave, result in every lane (tree order: the control law's
+// parity is tolerance-based, 1e-5 relative).
 __device__ __forceinline__ double wave_sum(double x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
+  x += dpp_f64_z<0xB1, 0xF>(x);
+  x += dpp_f64_z<0x4E, 0xF>(x);
+  x += dpp_f64_z<0x124, 0xF>(x);
+  x += dpp_f64_z<0x128, 0xF>(x);
+  x += dpp_f64_z<0x142, 0xA>(x);
+  x += dpp_f64_z<0x143, 0xC>(x);
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)u, 63);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(u >> 32), 63);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 __device__ __forceinline__ double wrap_to_pi(double a) {  // utils.h:275-280
@@ -128,12 +182,16 @@ __device__ __forceinline__ double wrap_to_pi(double a) {  // utils.h:275-280
   return a;
 }
 
+__device__ __forceinline__ void stamp(const SolveParams& P, int b, int tid, int k) {
+  if (P.stamps && tid == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
+}
+
 // selectTaskAssignment (auctioneer.cpp:517-542) for vehicle v as a wave
 // argmax: the first task j maximizing C[v][j] among tasks with
-// C[v][j] > price_j (price_j = C[who_j][j]); `nw[c]` is this lane's table
-// entry for task lane+64c (updated in registers and LDS).
-__device__ __forceinline__ void wave_select(int n, int v, int lane, const float* C,
-                                            unsigned char* row, int (&nw)[2]) {
+// C[v][j] > price_j (price_j = C[who_j][j]); nw[c] is this lane's entry for
+// task lane+64c. Returns the selected task (wave-uniform) or -1.
+__device__ __forceinline__ int wave_select(int n, int v, int lane, const float* C,
+                                           const int (&nw)[2]) {
   unsigned long long key = 0;
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
@@ -147,13 +205,8 @@ __device__ __forceinline__ void wave_select(int n, int v, int lane, const float*
     }
   }
   key = wave_max_u64(key);
-  if (key != 0) {
-    const int task = (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
-    if ((task & 63) == lane) {
-      nw[task >> 6] = v;
-      row[task] = (unsigned char)v;
-    }
-  }
+  if (key == 0) return -1;
+  return (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
 }
 
 __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
@@ -167,16 +220,19 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
 
   double* q = reinterpret_cast<double*>(smem + L.q);
   double* p = reinterpret_cast<double*>(smem + L.p);
+  double* qf = reinterpret_cast<double*>(smem + L.qf);
   double* out = reinterpret_cast<double*>(smem + L.out);
   unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
   unsigned long long* vadj = reinterpret_cast<unsigned long long*>(smem + L.vadj);
   unsigned long long* H = reinterpret_cast<unsigned long long*>(smem + L.H);
   float* C = reinterpret_cast<float*>(smem + L.C);
-  unsigned char* T[2] = {smem + L.T0, smem + L.T1};
+  // the two table buffers; indexed by offset so every access stays an LDS
+  // (addrspace 3) access -- a runtime-selected pointer would become flat
+  unsigned char* const T0 = smem + L.T0;
+  const int Tstr = L.T1 - L.T0;
   unsigned char* Pin = smem + L.Pin;
   unsigned char* Ptin = smem + L.Ptin;
-  unsigned char* wst = smem + L.wst;
-  unsigned char* tie = smem + L.tie;
+  unsigned char* cao = smem + L.cao;
   unsigned char* myi = smem + L.myi;
   unsigned char* validv = smem + L.valid;
   int* rowptr = reinterpret_cast<int*>(smem + L.rowptr);
@@ -187,6 +243,7 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
   const int gw = (n + 63) >> 6;  // words per row in the global table
   const unsigned long long lastmask =
       (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+  stamp(P, b, tid, 0);
 
   // ---------------- phase 0: load -----------------------------------------
   {
@@ -256,42 +313,50 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
     return;
   }
 
-  // vehicle-space closed neighbourhoods: u ~ v iff u == v or adj(P[v], P[u])
-  // (bidIterComplete, auctioneer.cpp:419-437)
-  for (int k = tid; k < n * W; k += kBlock) {
-    const int v = k >> 1, w = k & 1;
-    const int i = Pin[v];
-    unsigned long long m = 0;
-    for (int t = 0; t < 64; ++t) {
-      const int u = 64 * w + t;
-      if (u < n) {
-        const int pu = Pin[u];
-        const bool e = (u == v) || ((adjF[2 * i + (pu >> 6)] >> (pu & 63)) & 1ull);
-        m |= (unsigned long long)e << t;
-      }
-    }
-    vadj[k] = m;
+  // q in formation space: qf[j] = q[Pt[j]] (xy only; the alignment is 2-D)
+  for (int j = tid; j < n; j += kBlock) {
+    const int vj = Ptin[j];
+    qf[2 * j] = q[3 * vj];
+    qf[2 * j + 1] = q[3 * vj + 1];
   }
+  // vehicle-space closed neighbourhoods: u ~ v iff u == v or adj(P[v], P[u])
+  // (bidIterComplete, auctioneer.cpp:419-437). Lane = v, uniform loop over u.
+  for (int v = tid; v < ((n + 63) & ~63); v += kBlock) {
+    const int i = (v < n) ? Pin[v] : 0;
+    const unsigned long long a0 = adjF[2 * i], a1 = adjF[2 * i + 1];
+    unsigned long long m0 = 0, m1 = 0;
+    for (int u = 0; u < n; ++u) {
+      const int pu = Pin[u];
+      const bool e = (u == v) || (((pu < 64 ? a0 : a1) >> (pu & 63)) & 1ull);
+      if (u < 64) m0 |= (unsigned long long)e << u;
+      else m1 |= (unsigned long long)e << (u - 64);
+    }
+    if (v < n) {
+      vadj[2 * v] = m0;
+      vadj[2 * v + 1] = m1;
+    }
+  }
+  __syncthreads();
+  stamp(P, b, tid, 1);
 
   // ---------------- phase 1: alignment (one thread per vehicle) ----------
-  for (int v = tid; v < n; v += kBlock) {
-    const int i = Pin[v];
+  // Uniform loop over formation points j (broadcast LDS reads), predicated
+  // on "j in my closed neighbourhood": the sums stay sequential in
+  // ascending j, exactly as Eigen's rowwise().sum() / GEMM accumulate.
+  for (int v = tid; v < ((n + 63) & ~63); v += kBlock) {
+    const bool act = v < n;
+    const int i = act ? Pin[v] : 0;
     unsigned long long r0 = adjF[2 * i], r1 = adjF[2 * i + 1];
     if (i < 64) r0 |= 1ull << i; else r1 |= 1ull << (i - 64);
-    // means: rowwise().sum() * one_over_n, sequential in k
-    int k = 0;
+    const int k = __popcll(r0) + __popcll(r1);
     double ssx = 0, ssy = 0, sdx = 0, sdy = 0;
-    for (int w = 0; w < 2; ++w) {
-      unsigned long long m = w ? r1 : r0;
-      while (m) {
-        const int j = 64 * w + __ffsll((long long)m) - 1;
-        m &= m - 1;
-        const int vj = Ptin[j];
-        const double px = p[3 * j], py = p[3 * j + 1];
-        const double qx = q[3 * vj], qy = q[3 * vj + 1];
-        if (k == 0) { ssx = px; ssy = py; sdx = qx; sdy = qy; }
+    bool first = true;
+    for (int j = 0; j < n; ++j) {
+      const bool in = ((j < 64 ? r0 : r1) >> (j & 63)) & 1ull;
+      const double px = p[3 * j], py = p[3 * j + 1], qx = qf[2 * j], qy = qf[2 * j + 1];
+      if (in) {
+        if (first) { ssx = px; ssy = py; sdx = qx; sdy = qy; first = false; }
         else { ssx = ssx + px; ssy = ssy + py; sdx = sdx + qx; sdy = sdy + qy; }
-        ++k;
       }
     }
     const double oon = 1.0 / (double)k;
@@ -301,26 +366,23 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
     // lhs) when k + 4 < 20, GEMM (alpha after the sum) otherwise
     const bool lazy = (k + 4) < 20;
     double a00 = 0, a01 = 0, a10 = 0, a11 = 0;  // a_ij = sum dst_i * src_j
-    int kk = 0;
-    for (int w = 0; w < 2; ++w) {
-      unsigned long long m = w ? r1 : r0;
-      while (m) {
-        const int j = 64 * w + __ffsll((long long)m) - 1;
-        m &= m - 1;
-        const int vj = Ptin[j];
-        const double s0 = p[3 * j] - sm[0], s1 = p[3 * j + 1] - sm[1];
-        double d0 = q[3 * vj] - dm[0], d1 = q[3 * vj + 1] - dm[1];
-        if (lazy) {
-          d0 = oon * d0;
-          d1 = oon * d1;
-        }
-        if (lazy && kk == 0) {
+    first = true;
+    for (int j = 0; j < n; ++j) {
+      const bool in = ((j < 64 ? r0 : r1) >> (j & 63)) & 1ull;
+      const double s0 = p[3 * j] - sm[0], s1 = p[3 * j + 1] - sm[1];
+      double d0 = qf[2 * j] - dm[0], d1 = qf[2 * j + 1] - dm[1];
+      if (lazy) {
+        d0 = oon * d0;
+        d1 = oon * d1;
+      }
+      if (in) {
+        if (lazy && first) {
           a00 = d0 * s0; a01 = d0 * s1; a10 = d1 * s0; a11 = d1 * s1;
         } else {
           a00 = a00 + d0 * s0; a01 = a01 + d0 * s1;
           a10 = a10 + d1 * s0; a11 = a11 + d1 * s1;
         }
-        ++kk;
+        first = false;
       }
     }
     double S[4];  // column-major sigma
@@ -328,10 +390,13 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
     else { S[0] = a00 * oon; S[1] = a10 * oon; S[2] = a01 * oon; S[3] = a11 * oon; }
     double R[4], t[2];
     umeyama_finish(S, sm, dm, R, t);
-    double* o = out + 6 * v;
-    o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
+    if (act) {
+      double* o = out + 6 * v;
+      o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
+    }
   }
   __syncthreads();
+  stamp(P, b, tid, 2);
 
   // ---------------- phase 2: prices ---------------------------------------
   {
@@ -351,142 +416,206 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
     }
     for (int j = tid; j < n; j += kBlock) C[n * n + j] = 0.0f;  // row `none`
     // initial tables: every entry unassigned (reset, auctioneer.cpp:448-465)
-    for (int k = tid; k < n * n; k += kBlock) T[0][k] = (unsigned char)n;
+    for (int k = tid; k < n * n; k += kBlock) T0[k] = (unsigned char)n;
     if (__any(nonfin) && lane == 0) misc[M_NONFIN] = 1;
   }
   __syncthreads();
   const bool nonfinite = misc[M_NONFIN] != 0;
+  stamp(P, b, tid, 3);
 
   // ---------------- phase 3: CBAA ------------------------------------------
-  // round 0: START bid = select from the zero table (start, auctioneer.cpp:105)
+  // CBAA state in the (now free) level region: dirty-column masks by round
+  // parity, outbid-vehicle masks by round parity, per-column buffer index.
+  unsigned long long* dmask = H;      // [2][2]
+  unsigned long long* obm = H + 4;    // [2][2]
+  unsigned char* colbuf = reinterpret_cast<unsigned char*>(H + 8);  // [n]
+  if (tid < 8) H[tid] = 0ull;
+  for (int jj = tid; jj < n; jj += kBlock) colbuf[jj] = 0;
+  __syncthreads();
+  // round 0: START bid = select from the zero table (start, auctioneer.cpp:105);
+  // every column that received a bid is dirty for round 1
   for (int v = wave; v < n; v += kWaves) {
     int nw[2] = {n, n};
-    wave_select(n, v, lane, C, T[0] + v * n, nw);
+    const int task = wave_select(n, v, lane, C, nw);
+    if (task >= 0 && lane == 0) {
+      T0[v * n + task] = (unsigned char)v;
+      atomicOr(&dmask[2 * 1 + (task >> 6)], 1ull << (task & 63));
+    }
   }
   __syncthreads();
 
-  int cur = 0;
   int eff = 0;
   const int max_rounds = 2 * n;  // cbaa_max_iter_ = n * diameter (:50-51)
-  const int hn = (n + 1) >> 1;
-  unsigned long long* Hpart = reinterpret_cast<unsigned long long*>(out);  // scratch
-  for (int r = 1; r <= max_rounds; ++r) {
-    const unsigned char* Tc = T[cur];
-    unsigned char* Tn = T[cur ^ 1];
-    if (tid == 0) misc[M_CHG0 + ((r + 1) % 3)] = 0;
-    // A) per task: max price over all vehicles, its `who`, tie, holders
-    {
-      const int j = tid & 127;
-      const int half = tid >> 7;
-      float Pm = -1.0f;
-      int wm = n, tm = 0;
-      unsigned long long h0 = 0, h1 = 0;
-      if (j < n) {
-        const int u0 = half * hn;
-        const int u1 = min(n, u0 + hn);
-        for (int u = u0; u < u1; ++u) {
-          const int wu = Tc[u * n + j];
-          const float pu = C[wu * n + j];
-          const unsigned long long bit0 = (u < 64) ? (1ull << u) : 0ull;
-          const unsigned long long bit1 = (u >= 64) ? (1ull << (u - 64)) : 0ull;
-          if (pu > Pm) {
-            Pm = pu; wm = wu; tm = 0; h0 = bit0; h1 = bit1;
-          } else if (pu == Pm) {
-            h0 |= bit0; h1 |= bit1; tm |= (wu != wm);
-          }
-        }
-        if (half == 1) {
-          Hpart[4 * j + 0] = h0;
-          Hpart[4 * j + 1] = h1;
-          Hpart[4 * j + 2] = (unsigned long long)__float_as_uint(Pm);
-          Hpart[4 * j + 3] = (unsigned long long)(wm | (tm << 16));
-        }
-      }
-      __syncthreads();
-      if (half == 0 && j < n) {
-        const float Pb = __uint_as_float((unsigned)Hpart[4 * j + 2]);
-        const int wb = (int)(Hpart[4 * j + 3] & 0xFFFF);
-        const int tb = (int)(Hpart[4 * j + 3] >> 16);
-        if (Pb > Pm) {
-          Pm = Pb; wm = wb; tm = tb; h0 = Hpart[4 * j]; h1 = Hpart[4 * j + 1];
-        } else if (Pb == Pm) {
-          h0 |= Hpart[4 * j]; h1 |= Hpart[4 * j + 1]; tm |= tb | (wb != wm);
-        }
-        H[2 * j] = h0;
-        H[2 * j + 1] = h1;
-        wst[j] = (unsigned char)wm;
-        tie[j] = (unsigned char)(tm | nonfinite);
-      }
+  unsigned long long sub[4] = {0, 0, 0, 0};
+  unsigned long long tprev = P.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  auto substamp = [&](int k) {
+    if (P.stamps) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      sub[k] += t - tprev;
+      tprev = t;
     }
-    __syncthreads();
-    // B) per vehicle (one wave), lanes over tasks
-    for (int v = wave; v < n; v += kWaves) {
-      const unsigned long long vm0 = vadj[2 * v], vm1 = vadj[2 * v + 1];
-      int old[2], nw[2];
-      bool need[2];
+  };
+  for (int r = 1; r <= max_rounds; ++r) {
+    const int par = r & 1, npar = par ^ 1;
+    const unsigned long long D0 = dmask[2 * par], D1 = dmask[2 * par + 1];
+    if (P.stamps) sub[2] += __popcll(D0) + __popcll(D1);
+    // A+B) One wave per dirty column j. A column none of whose entries changed
+    // last round is a fixed point of updateTaskAssignment (it reads only
+    // that column, and a select always changes the entry it writes), so only
+    // dirty columns are recomputed. Lanes = vehicles.
+    {
+      int idx = 0;
+      for (int w = 0; w < 2; ++w) {
+        unsigned long long m = w ? D1 : D0;
+        while (m) {
+          const int j = 64 * w + __ffsll((long long)m) - 1;
+          m &= m - 1;
+          if ((idx++ & (kWaves - 1)) != wave) continue;
+          const int cb = colbuf[j];
+          const unsigned char* Tc = T0 + cb * Tstr;
+          unsigned char* Tn = T0 + (cb ^ 1) * Tstr;
+          int wu[2];
+          float pu[2];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int j = lane + 64 * c;
-        old[c] = nw[c] = n;
-        need[c] = false;
-        if (j < n) {
-          old[c] = Tc[v * n + j];
-          const bool fast = !tie[j] && (((H[2 * j] & vm0) | (H[2 * j + 1] & vm1)) != 0ull);
-          if (fast) nw[c] = wst[j];
-          else need[c] = true;
-        }
-      }
-      // exact ordered scan (ascending vehid, strict >) where the shortcut
-      // does not apply: ties or no holder of the maximum among neighbours
-      if (__any(need[0] || need[1])) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          if (!__any(need[c])) continue;
-          const int j = lane + 64 * c;
-          float bp = 0.0f;
-          int bw = n;
-          bool first = true;
-          for (int w = 0; w < 2; ++w) {
-            unsigned long long m = w ? vm1 : vm0;
-            while (m) {
-              const int u = 64 * w + __ffsll((long long)m) - 1;
-              m &= m - 1;
-              if (need[c]) {
-                const int wu = Tc[u * n + j];
-                const float pu = C[wu * n + j];
-                if (first) { bp = pu; bw = wu; first = false; }
-                else if (pu > bp) { bp = pu; bw = wu; }
-              }
+          for (int c = 0; c < 2; ++c) {
+            const int u = lane + 64 * c;
+            wu[c] = n;
+            pu[c] = -1.0f;
+            if (u < n) {
+              wu[c] = Tc[u * n + j];
+              pu[c] = C[wu[c] * n + j];
             }
           }
-          if (need[c]) nw[c] = bw;
-        }
-      }
-      bool outbid = false;
+          // A) the top kLevels distinct prices of the column, their holder
+          //    masks, `who` and tie flag (wave max + ballots)
+          float cap = __builtin_inff();
+          unsigned long long Lh0[kLevels], Lh1[kLevels];
+          int Lw[kLevels];
+          bool Lt[kLevels];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int j = lane + 64 * c;
-        if (j < n) {
-          outbid |= (old[c] == v) && (nw[c] != v);
-          Tn[v * n + j] = (unsigned char)nw[c];
+          for (int k = 0; k < kLevels; ++k) {
+            const float x0 = pu[0] < cap ? pu[0] : -1.0f;
+            const float x1 = pu[1] < cap ? pu[1] : -1.0f;
+            const float Pk = wave_max_f32(fmaxf(x0, x1));
+            const bool e0 = pu[0] == Pk, e1 = pu[1] == Pk;
+            const unsigned long long m0 = __ballot(e0), m1 = __ballot(e1);
+            const int wk = m0 ? __builtin_amdgcn_readlane(wu[0], __ffsll((long long)m0) - 1)
+                              : __builtin_amdgcn_readlane(wu[1], m1 ? __ffsll((long long)m1) - 1 : 0);
+            const bool tk = (__ballot(e0 && wu[0] != wk) | __ballot(e1 && wu[1] != wk)) != 0ull;
+            const bool empty = !(Pk >= 0.0f);
+            Lh0[k] = empty ? 0ull : m0;
+            Lh1[k] = empty ? 0ull : m1;
+            Lw[k] = wk;
+            Lt[k] = tk || nonfinite;
+            cap = Pk;
+          }
+          // B) per vehicle v: the `who` of the highest level one of v's
+          //    closed neighbours holds, unless that level is tied;
+          //    otherwise the exact ordered scan (ascending vehid, strict >)
+          bool ob[2], ch[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int v = lane + 64 * c;
+            ob[c] = ch[c] = false;
+            if (v < n) {
+              const unsigned long long vm0 = vadj[2 * v], vm1 = vadj[2 * v + 1];
+              const int old = wu[c];
+              int nw = n;
+              bool decided = false, need = false;
+#pragma unroll
+              for (int k = 0; k < kLevels; ++k) {
+                if (!decided && (((Lh0[k] & vm0) | (Lh1[k] & vm1)) != 0ull)) {
+                  decided = true;
+                  if (Lt[k]) need = true;
+                  else nw = Lw[k];
+                }
+              }
+              if (!decided) need = true;
+              if (need) {
+                float bp = 0.0f;
+                int bw = n;
+                bool first = true;
+#pragma unroll
+                for (int w2 = 0; w2 < 2; ++w2) {
+                  unsigned long long mm = w2 ? vm1 : vm0;
+                  while (mm) {
+                    const int u = 64 * w2 + __ffsll((long long)mm) - 1;
+                    mm &= mm - 1;
+                    const int wx = Tc[u * n + j];
+                    const float px = C[wx * n + j];
+                    if (first) { bp = px; bw = wx; first = false; }
+                    else if (px > bp) { bp = px; bw = wx; }
+                  }
+                }
+                nw = bw;
+              }
+              Tn[v * n + j] = (unsigned char)nw;
+              ob[c] = (old == v) && (nw != v);  // outbid (auctioneer.cpp:502)
+              ch[c] = nw != old;
+            }
+          }
+          const unsigned long long ob0 = __ballot(ob[0]), ob1 = __ballot(ob[1]);
+          const bool anych = __any(ch[0] || ch[1]);
+          if (lane == 0) {
+            if (ob0) atomicOr(&obm[2 * par], ob0);
+            if (ob1) atomicOr(&obm[2 * par + 1], ob1);
+            if (anych) atomicOr(&dmask[2 * npar + (j >> 6)], 1ull << (j & 63));
+            colbuf[j] = (unsigned char)(cb ^ 1);
+          }
         }
       }
-      if (__any(outbid)) wave_select(n, v, lane, C, Tn + v * n, nw);
-      const bool chg = (nw[0] != old[0]) || (nw[1] != old[1]);
-      if (__any(chg) && lane == 0) misc[M_CHG0 + (r % 3)] = 1;
     }
     __syncthreads();
-    const bool changed = misc[M_CHG0 + (r % 3)] != 0;
-    if (changed) {
-      eff = r;
-      cur ^= 1;
-    } else if (P.early_exit) {
-      break;  // fixed point
+    substamp(0);
+    // outbid vehicles re-select on their updated rows (auctioneer.cpp:224)
+    {
+      if (tid == 0) {
+        dmask[2 * par] = 0ull;        // consumed; becomes round r+2's mask
+        dmask[2 * par + 1] = 0ull;
+        obm[2 * npar] = 0ull;         // round r+1's outbid mask
+        obm[2 * npar + 1] = 0ull;
+      }
+      const unsigned long long O0 = obm[2 * par], O1 = obm[2 * par + 1];
+      if (P.stamps) sub[3] += __popcll(O0) + __popcll(O1);
+      int idx = 0;
+      for (int w = 0; w < 2; ++w) {
+        unsigned long long m = w ? O1 : O0;
+        while (m) {
+          const int v = 64 * w + __ffsll((long long)m) - 1;
+          m &= m - 1;
+          if ((idx++ & (kWaves - 1)) != wave) continue;
+          int nw[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int jj = lane + 64 * c;
+            nw[c] = (jj < n) ? T0[colbuf[jj] * Tstr + v * n + jj] : n;
+          }
+          const int task = wave_select(n, v, lane, C, nw);
+          if (task >= 0 && lane == 0) {
+            T0[colbuf[task] * Tstr + v * n + task] = (unsigned char)v;
+            atomicOr(&dmask[2 * npar + (task >> 6)], 1ull << (task & 63));
+          }
+        }
+      }
     }
+    __syncthreads();
+    substamp(1);
+    const bool changed = (dmask[2 * npar] | dmask[2 * npar + 1]) != 0ull;
+    if (changed) eff = r;
+    else if (P.early_exit) break;  // fixed point
   }
+  // consolidate the per-column buffers into T[0]
+  for (int k = tid; k < n * n; k += kBlock) {
+    const int jj = k % n;
+    if (colbuf[jj]) T0[k] = T0[Tstr + k];
+  }
+  __syncthreads();
+  stamp(P, b, tid, 4);
+  if (P.stamps && tid == 0)
+    for (int k = 0; k < 4; ++k) P.stamps[(size_t)b * 16 + 8 + k] = sub[k];
 
   // ---------------- phase 4: adoption --------------------------------------
-  const unsigned char* Tf = T[cur];
+  const unsigned char* Tf = T0;
   for (int v = tid; v < n; v += kBlock) {
     const unsigned char* row = Tf + v * n;
     unsigned long long s0 = 0, s1 = 0;
@@ -520,19 +649,40 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
     }
   }
   __syncthreads();
+  stamp(P, b, tid, 5);
 
   // ---------------- phase 5: control + safety -----------------------------
   if (P.do_control) {
     double* uo = out;           // [n][3] u
     double* uso = out + 3 * n;  // [n][3] u_safe
-    unsigned char* cao = wst;   // reuse: [n] ca flags
     const int E = rowptr[n];
     const double* G = P.gains + 9 * P.gain_off[f];
     const acl_cntrl_gains_t g = P.g;
     const acl_safety_params_t sp = P.s;
     double* caA = reinterpret_cast<double*>(C) + wave * (4 * n);               // angles
     signed char* caS = reinterpret_cast<signed char*>(C) + kWaves * 4 * n * 8 + wave * 4 * n;
+    // the 3x3 blocks of the vehicle's formation row: lane = column j (two
+    // chunks of 64), coalesced across lanes in each of the 9 planes
+    auto load_row = [&](int v, double (&A)[2][9], bool (&has)[2]) {
+      const int i = myi[v];
+      int ebase = rowptr[i];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const unsigned long long rowbits = adjF[2 * i + c];
+        has[c] = (rowbits >> lane) & 1ull;
+        const int e = ebase + __popcll(rowbits & ((1ull << lane) - 1ull));
+        ebase += __popcll(rowbits);
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+          A[c][k] = has[c] ? __builtin_nontemporal_load(G + (size_t)k * E + e) : 0.0;
+      }
+    };
+    double Acur[2][9], Anx[2][9];
+    bool hcur[2], hnx[2];
+    if (wave < n) load_row(wave, Acur, hcur);
     for (int v = wave; v < n; v += kWaves) {
+      // prefetch the next vehicle's gain blocks while this one computes
+      if (v + kWaves < n) load_row(v + kWaves, Anx, hnx);
       const int i = myi[v];
       const unsigned char* Ptv = validv[v] ? (Tf + v * n) : Ptin;
       const double* gv = P.vel + ((size_t)b * n + v) * 3;
@@ -541,18 +691,11 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
       const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
       const double Ni = pix * pix + piy * piy, Nzi = piz * piz;
       double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-      int ebase = rowptr[i];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int j = lane + 64 * c;
-        const unsigned long long rowbits = adjF[2 * i + c];
-        const bool has = (rowbits >> lane) & 1ull;
-        const int e = ebase + __popcll(rowbits & ((1ull << lane) - 1ull));
-        ebase += __popcll(rowbits);
-        if (has) {
-          double A[9];
-#pragma unroll
-          for (int k = 0; k < 9; ++k) A[k] = G[(size_t)k * E + e];
+        if (hcur[c]) {
+          const double* A = Acur[c];
           const int u = Ptv[j];
           const double q0 = q[3 * u] - qv0, q1 = q[3 * u + 1] - qv1, q2 = q[3 * u + 2] - qv2;
           const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
@@ -571,6 +714,12 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
           acc1 += g.kp * up1 + g.kd * (-vel1);
           acc2 += g.kp * up2 + g.kd * (-vel2);
         }
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        hcur[c] = hnx[c];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Acur[c][k] = Anx[c][k];
       }
       double cmd0 = wave_sum(acc0), cmd1 = wave_sum(acc1), cmd2 = wave_sum(acc2);
       if (lane == 0) {
@@ -720,6 +869,7 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
       for (int v = tid; v < n; v += kBlock) P.ca_flag[(size_t)b * n + v] = cao[v];
   }
 
+  stamp(P, b, tid, 6);
   if (tid == 0) {
     acl_swarm_status_t st = {};
     uint32_t fl = 0;
@@ -746,6 +896,11 @@ extern "C" acl_status_t acl__set_error(const char* msg);
 
 extern "C" int32_t acl_max_vehicles(void) { return acl_amd::kMaxN; }
 
+// Diagnostic hook (not part of the public ABI): when set, the next solves
+// record s_memtime at the end of each phase into stamps[B][8].
+static unsigned long long* g_stamps = nullptr;
+extern "C" void acl_internal_set_stamps(unsigned long long* stamps) { g_stamps = stamps; }
+
 extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_solve_args_t* a,
                                         void* stream) {
   using namespace acl_amd;
@@ -765,6 +920,7 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   P.status = a->status; P.u = a->u; P.u_safe = a->u_safe; P.ca_flag = a->ca_flag;
   P.who = a->who; P.g = a->cntrl; P.s = a->safety;
   P.early_exit = a->early_exit; P.do_control = a->do_control;
+  P.stamps = g_stamps;
   const Layout L = make_layout(n);
   static int configured = 0;
   if (!configured) {

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase cycle shares of solve_kernel (s_memtime stamps
+written by thread 0 of each workgroup at the end of every phase), on the
+bench workload. Uses the library's internal hook acl_internal_set_stamps."""
+import argparse
+import ctypes as ct
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from aclswarm_amd import _lib as L  # noqa: E402
+from aclswarm_amd import engine, workload  # noqa: E402
+
+NAMES = ["load+nbhd", "align", "prices", "cbaa", "adopt", "control+safety"]
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--B", type=int, default=8192)
+ap.add_argument("--n", type=int, default=100)
+ap.add_argument("--formations", type=int, default=0)
+args = ap.parse_args()
+dev = torch.device("cuda:0")
+gen = torch.Generator(device=dev)
+gen.manual_seed(1)
+w = workload.simform_workload(args.B, args.n, gen, dev, F=(args.formations or None))
+T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"])
+lib = L.lib()
+lib.acl_internal_set_stamps.argtypes = [ct.c_void_p]
+st = torch.zeros((args.B, 16), dtype=torch.int64, device=dev)
+engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"])  # warm
+torch.cuda.synchronize()
+lib.acl_internal_set_stamps(ct.c_void_p(st.data_ptr()))
+engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"])
+torch.cuda.synchronize()
+lib.acl_internal_set_stamps(ct.c_void_p(0))
+s = st.cpu().numpy().astype(np.float64)
+d = np.diff(s[:, :7], axis=1)
+tot = d.sum(1)
+print(f"per-swarm cycles: mean {tot.mean():.0f}  median {np.median(tot):.0f}")
+for k, nm in enumerate(NAMES):
+    print(f"  {nm:16s} mean {d[:, k].mean():10.0f}  share {d[:, k].sum() / tot.sum() * 100:5.1f}%")
+sub = s[:, 8:12]
+for k, nm in enumerate(["  dirty cols A+B", "  select", "  #dirty cols", "  #selects"]):
+    print(f"  {nm:16s} mean {sub[:, k].mean():10.0f}")
+print("eff rounds mean", float(np.mean(np.frombuffer(b"", dtype=np.uint8))) if False else "")
