@@ -28,7 +28,7 @@ STATUS_DTYPE = np.dtype([("flags", "<u4"), ("eff_rounds", "<u2"),
 # every symbol include/aclswarm_amd.h declares
 EXPORTS = (
     "acl_default_cntrl_gains", "acl_default_safety_params", "acl_default_admm_params",
-    "acl_max_vehicles", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
+    "acl_max_vehicles", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
     "acl_pack_gains", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
     "acl_malloc", "acl_free", "acl_memcpy_h2d", "acl_memcpy_d2h", "acl_memset",
     "acl_stream_synchronize", "acl_last_error",
@@ -65,7 +65,7 @@ class SolveArgs(ct.Structure):
     _fields_ = [("B", ct.c_int32), ("fidx", ct.c_void_p), ("q", ct.c_void_p),
                 ("vel", ct.c_void_p), ("P_in", ct.c_void_p), ("P_out", ct.c_void_p),
                 ("status", ct.c_void_p), ("u", ct.c_void_p), ("u_safe", ct.c_void_p),
-                ("ca_flag", ct.c_void_p), ("who", ct.c_void_p),
+                ("ca_flag", ct.c_void_p), ("who", ct.c_void_p), ("workspace", ct.c_void_p),
                 ("cntrl", CntrlGains), ("safety", SafetyParams),
                 ("early_exit", ct.c_int32), ("do_control", ct.c_int32)]
 
@@ -88,6 +88,8 @@ def lib():
     L.acl_default_safety_params.argtypes = [ct.POINTER(SafetyParams)]
     L.acl_default_admm_params.argtypes = [ct.POINTER(AdmmParams)]
     L.acl_max_vehicles.restype = I32
+    L.acl_solve_workspace_bytes.argtypes = [I32, I32]
+    L.acl_solve_workspace_bytes.restype = ct.c_size_t
     L.acl_solve_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(SolveArgs), VP]
     L.acl_solve_batch.restype = ct.c_int
     L.acl_count_edges.argtypes = [I32, VP]

@@ -36,14 +36,14 @@
 #include <stdint.h>
 
 #include "../../include/aclswarm_amd.h"
+#include "common.h"
 #include "umeyama_dev.h"
 
 namespace acl_amd {
 
-constexpr int kBlock = 256;
+constexpr int kBlock = 512;  // 8 waves per swarm, 2 swarms per CU
 constexpr int kWaves = kBlock / 64;
 constexpr int kMaxN = 128;  // two 64-bit words per bitmask row, u8 indices
-constexpr double kPi = 3.14159265358979323846;
 
 struct Layout {
   // byte offsets into the dynamic LDS block (all 16-byte aligned)
@@ -64,7 +64,7 @@ __host__ __device__ inline Layout make_layout(int n) {
   L.out = o;    o = align16(o + n * 6 * 8);   // R,t per vehicle; later u, u_safe
   L.adjF = o;   o = align16(o + n * 2 * 8);
   L.vadj = o;   o = align16(o + n * 2 * 8);
-  L.H = o;      o = align16(o + 64 + n);      // CBAA masks + per-column buffer index
+  L.H = o;      o = align16(o + 96);          // CBAA masks + per-column buffer bits
   L.C = o;
   {
     const int csz = (n + 1) * n * 4;
@@ -85,7 +85,7 @@ __host__ __device__ inline Layout make_layout(int n) {
 }
 
 struct SolveParams {
-  int n, B, F;
+  int n, B, F, b0;
   const double* p;
   const uint64_t* adj;
   const double* gains;
@@ -104,83 +104,12 @@ struct SolveParams {
   acl_safety_params_t s;
   int early_exit;
   int do_control;
+  unsigned char* ws;           // workspace: [B][n] shared rows, [B] mode, [B][n][n] rows
   unsigned long long* stamps;  // diagnostic: [B][16] s_memtime at phase ends (NULL = off)
 };
 
 // misc int slots
 enum { M_BAD = 0, M_NONFIN = 1, M_CHG0 = 2, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 8 };
-
-// Wave64 reductions on DPP (VALU lane shuffles, no LDS round trip):
-// quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, 8 give every lane its row's
-// result; row_bcast15 / row_bcast31 fold rows 0-3 into lane 63.
-// Callers must have all 64 lanes active.
-#define ACL_DPP_STEP(x, op, ctrl, rmask)                                                   \
-  x = op(x, __builtin_amdgcn_update_dpp(x, x, ctrl, rmask, 0xF, false))
-
-__device__ __forceinline__ unsigned umax32(unsigned a, int b) { return a > (unsigned)b ? a : (unsigned)b; }
-
-__device__ __forceinline__ unsigned wave_max_u32(unsigned ux) {
-  int x = (int)ux;
-#define ACL_UMAX(a, b) (int)umax32((unsigned)(a), (b))
-  ACL_DPP_STEP(x, ACL_UMAX, 0xB1, 0xF);
-  ACL_DPP_STEP(x, ACL_UMAX, 0x4E, 0xF);
-  ACL_DPP_STEP(x, ACL_UMAX, 0x124, 0xF);
-  ACL_DPP_STEP(x, ACL_UMAX, 0x128, 0xF);
-  ACL_DPP_STEP(x, ACL_UMAX, 0x142, 0xA);
-  ACL_DPP_STEP(x, ACL_UMAX, 0x143, 0xC);
-#undef ACL_UMAX
-  return (unsigned)__builtin_amdgcn_readlane(x, 63);
-}
-
-__device__ __forceinline__ float wave_max_f32(float fx) {
-  int x = __float_as_int(fx);
-#define ACL_FMAX(a, b) __float_as_int(fmaxf(__int_as_float(a), __int_as_float(b)))
-  ACL_DPP_STEP(x, ACL_FMAX, 0xB1, 0xF);
-  ACL_DPP_STEP(x, ACL_FMAX, 0x4E, 0xF);
-  ACL_DPP_STEP(x, ACL_FMAX, 0x124, 0xF);
-  ACL_DPP_STEP(x, ACL_FMAX, 0x128, 0xF);
-  ACL_DPP_STEP(x, ACL_FMAX, 0x142, 0xA);
-  ACL_DPP_STEP(x, ACL_FMAX, 0x143, 0xC);
-#undef ACL_FMAX
-  return __int_as_float(__builtin_amdgcn_readlane(x, 63));
-}
-
-__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x) {
-  const unsigned hi = (unsigned)(x >> 32), lo = (unsigned)x;
-  const unsigned mh = wave_max_u32(hi);
-  const unsigned ml = wave_max_u32(hi == mh ? lo : 0u);
-  return ((unsigned long long)mh << 32) | ml;
-}
-
-// DPP move of a double; lanes outside RMASK read 0 (the sum's identity).
-template <int CTRL, int RMASK>
-__device__ __forceinline__ double dpp_f64_z(double x) {
-  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)u, CTRL, RMASK, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, RMASK, 0xF, false);
-  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-}
-
-// Sum over the wave, result in every lane (tree order: the control law's
-// parity is tolerance-based, 1e-5 relative).
-__device__ __forceinline__ double wave_sum(double x) {
-  x += dpp_f64_z<0xB1, 0xF>(x);
-  x += dpp_f64_z<0x4E, 0xF>(x);
-  x += dpp_f64_z<0x124, 0xF>(x);
-  x += dpp_f64_z<0x128, 0xF>(x);
-  x += dpp_f64_z<0x142, 0xA>(x);
-  x += dpp_f64_z<0x143, 0xC>(x);
-  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)u, 63);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(u >> 32), 63);
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-__device__ __forceinline__ double wrap_to_pi(double a) {  // utils.h:275-280
-  if (a > kPi) return a - 2 * kPi;
-  if (a < -kPi) return a + 2 * kPi;
-  return a;
-}
 
 __device__ __forceinline__ void stamp(const SolveParams& P, int b, int tid, int k) {
   if (P.stamps && tid == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
@@ -209,11 +138,11 @@ __device__ __forceinline__ int wave_select(int n, int v, int lane, const float* 
   return (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
 }
 
-__global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
+__global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const Layout L = make_layout(n);
-  const int b = blockIdx.x;
+  const int b = P.b0 + blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -232,7 +161,6 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
   const int Tstr = L.T1 - L.T0;
   unsigned char* Pin = smem + L.Pin;
   unsigned char* Ptin = smem + L.Ptin;
-  unsigned char* cao = smem + L.cao;
   unsigned char* myi = smem + L.myi;
   unsigned char* validv = smem + L.valid;
   int* rowptr = reinterpret_cast<int*>(smem + L.rowptr);
@@ -428,9 +356,8 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
   // parity, outbid-vehicle masks by round parity, per-column buffer index.
   unsigned long long* dmask = H;      // [2][2]
   unsigned long long* obm = H + 4;    // [2][2]
-  unsigned char* colbuf = reinterpret_cast<unsigned char*>(H + 8);  // [n]
-  if (tid < 8) H[tid] = 0ull;
-  for (int jj = tid; jj < n; jj += kBlock) colbuf[jj] = 0;
+  unsigned long long* cbm = H + 8;    // [2] bit j: column j's current buffer
+  if (tid < 10) H[tid] = 0ull;
   __syncthreads();
   // round 0: START bid = select from the zero table (start, auctioneer.cpp:105);
   // every column that received a bid is dirty for round 1
@@ -447,6 +374,7 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
   int eff = 0;
   const int max_rounds = 2 * n;  // cbaa_max_iter_ = n * diameter (:50-51)
   unsigned long long sub[4] = {0, 0, 0, 0};
+  unsigned long long dbg_needcols = 0, dbg_colcyc = 0;
   unsigned long long tprev = P.stamps ? __builtin_amdgcn_s_memtime() : 0;
   auto substamp = [&](int k) {
     if (P.stamps) {
@@ -459,11 +387,13 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
     const int par = r & 1, npar = par ^ 1;
     const unsigned long long D0 = dmask[2 * par], D1 = dmask[2 * par + 1];
     if (P.stamps) sub[2] += __popcll(D0) + __popcll(D1);
+    unsigned long long t_col = 0;
     // A+B) One wave per dirty column j. A column none of whose entries changed
     // last round is a fixed point of updateTaskAssignment (it reads only
     // that column, and a select always changes the entry it writes), so only
-    // dirty columns are recomputed. Lanes = vehicles.
+    // dirty columns are recomputed. Lanes = vehicles (two chunks of 64).
     {
+      const unsigned long long CB0 = cbm[0], CB1 = cbm[1];  // buffer of each column
       int idx = 0;
       for (int w = 0; w < 2; ++w) {
         unsigned long long m = w ? D1 : D0;
@@ -471,73 +401,78 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
           const int j = 64 * w + __ffsll((long long)m) - 1;
           m &= m - 1;
           if ((idx++ & (kWaves - 1)) != wave) continue;
-          const int cb = colbuf[j];
+          if (P.stamps) t_col = __builtin_amdgcn_s_memtime();
+          const int cb = (int)(((w ? CB1 : CB0) >> (j & 63)) & 1ull);
           const unsigned char* Tc = T0 + cb * Tstr;
           unsigned char* Tn = T0 + (cb ^ 1) * Tstr;
           int wu[2];
-          float pu[2];
+          unsigned key[2];  // price bits + 1 (prices are >= 0); 0 = no vehicle
+          unsigned long long vm0[2], vm1[2];
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
             const int u = lane + 64 * c;
             wu[c] = n;
-            pu[c] = -1.0f;
+            key[c] = 0u;
+            vm0[c] = vm1[c] = 0ull;
             if (u < n) {
               wu[c] = Tc[u * n + j];
-              pu[c] = C[wu[c] * n + j];
+              key[c] = __float_as_uint(C[wu[c] * n + j]) + 1u;
+              vm0[c] = vadj[2 * u];
+              vm1[c] = vadj[2 * u + 1];
             }
           }
-          // A) the top kLevels distinct prices of the column, their holder
-          //    masks, `who` and tie flag (wave max + ballots)
-          float cap = __builtin_inff();
-          unsigned long long Lh0[kLevels], Lh1[kLevels];
-          int Lw[kLevels];
-          bool Lt[kLevels];
-#pragma unroll
-          for (int k = 0; k < kLevels; ++k) {
-            const float x0 = pu[0] < cap ? pu[0] : -1.0f;
-            const float x1 = pu[1] < cap ? pu[1] : -1.0f;
-            const float Pk = wave_max_f32(fmaxf(x0, x1));
-            const bool e0 = pu[0] == Pk, e1 = pu[1] == Pk;
-            const unsigned long long m0 = __ballot(e0), m1 = __ballot(e1);
-            const int wk = m0 ? __builtin_amdgcn_readlane(wu[0], __ffsll((long long)m0) - 1)
-                              : __builtin_amdgcn_readlane(wu[1], m1 ? __ffsll((long long)m1) - 1 : 0);
-            const bool tk = (__ballot(e0 && wu[0] != wk) | __ballot(e1 && wu[1] != wk)) != 0ull;
-            const bool empty = !(Pk >= 0.0f);
-            Lh0[k] = empty ? 0ull : m0;
-            Lh1[k] = empty ? 0ull : m1;
-            Lw[k] = wk;
-            Lt[k] = tk || nonfinite;
-            cap = Pk;
-          }
-          // B) per vehicle v: the `who` of the highest level one of v's
-          //    closed neighbours holds, unless that level is tied;
-          //    otherwise the exact ordered scan (ascending vehid, strict >)
-          bool ob[2], ch[2];
+          // A) price levels of the column, highest first, computed lazily:
+          //    level k = (max key below level k-1, holder mask, `who`, tie).
+          // B) vehicle v takes the `who` of the highest level one of its
+          //    closed neighbours holds, unless that level is tied; vehicles
+          //    no tracked level decides fall back to the exact ordered scan
+          //    (ascending vehid, strict >).
+          int nw[2] = {n, n};
+          bool dec[2], need[2];
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
-            const int v = lane + 64 * c;
-            ob[c] = ch[c] = false;
-            if (v < n) {
-              const unsigned long long vm0 = vadj[2 * v], vm1 = vadj[2 * v + 1];
-              const int old = wu[c];
-              int nw = n;
-              bool decided = false, need = false;
+            dec[c] = (lane + 64 * c) >= n;
+            need[c] = false;
+          }
+          unsigned cap = 0xFFFFFFFFu;
 #pragma unroll
-              for (int k = 0; k < kLevels; ++k) {
-                if (!decided && (((Lh0[k] & vm0) | (Lh1[k] & vm1)) != 0ull)) {
-                  decided = true;
-                  if (Lt[k]) need = true;
-                  else nw = Lw[k];
-                }
+          for (int k = 0; k < kLevels; ++k) {
+            if (!__any(!dec[0] || !dec[1])) break;
+            const unsigned Mk = wave_max_u32(max(key[0] < cap ? key[0] : 0u,
+                                                 key[1] < cap ? key[1] : 0u));
+            if (Mk == 0u) break;  // no further level
+            const bool e0 = key[0] == Mk, e1 = key[1] == Mk;
+            const unsigned long long h0 = __ballot(e0), h1 = __ballot(e1);
+            const int wk = h0 ? __builtin_amdgcn_readlane(wu[0], __ffsll((long long)h0) - 1)
+                              : __builtin_amdgcn_readlane(wu[1], __ffsll((long long)h1) - 1);
+            const bool tk = nonfinite ||
+                            ((__ballot(e0 && wu[0] != wk) | __ballot(e1 && wu[1] != wk)) != 0ull);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              if (!dec[c] && (((h0 & vm0[c]) | (h1 & vm1[c])) != 0ull)) {
+                dec[c] = true;
+                if (tk) need[c] = true;
+                else nw[c] = wk;
               }
-              if (!decided) need = true;
-              if (need) {
+            }
+            cap = Mk;
+          }
+          bool dbg_need = false;
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            if (!dec[c]) need[c] = true;
+            dbg_need |= need[c];
+          }
+          if (__any(need[0] || need[1])) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              if (need[c]) {
                 float bp = 0.0f;
                 int bw = n;
                 bool first = true;
 #pragma unroll
                 for (int w2 = 0; w2 < 2; ++w2) {
-                  unsigned long long mm = w2 ? vm1 : vm0;
+                  unsigned long long mm = w2 ? vm1[c] : vm0[c];
                   while (mm) {
                     const int u = 64 * w2 + __ffsll((long long)mm) - 1;
                     mm &= mm - 1;
@@ -547,20 +482,33 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
                     else if (px > bp) { bp = px; bw = wx; }
                   }
                 }
-                nw = bw;
+                nw[c] = bw;
               }
-              Tn[v * n + j] = (unsigned char)nw;
-              ob[c] = (old == v) && (nw != v);  // outbid (auctioneer.cpp:502)
-              ch[c] = nw != old;
+            }
+          }
+          bool ob[2], ch[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int v = lane + 64 * c;
+            ob[c] = ch[c] = false;
+            if (v < n) {
+              Tn[v * n + j] = (unsigned char)nw[c];
+              ob[c] = (wu[c] == v) && (nw[c] != v);  // outbid (auctioneer.cpp:502)
+              ch[c] = nw[c] != wu[c];
             }
           }
           const unsigned long long ob0 = __ballot(ob[0]), ob1 = __ballot(ob[1]);
           const bool anych = __any(ch[0] || ch[1]);
+          if (P.stamps) {
+            sub[3] += 1;  // columns seen by this wave (wave 0 -> tid 0's counters)
+            dbg_needcols += __any(dbg_need) ? 1 : 0;
+            dbg_colcyc += __builtin_amdgcn_s_memtime() - t_col;
+          }
           if (lane == 0) {
             if (ob0) atomicOr(&obm[2 * par], ob0);
             if (ob1) atomicOr(&obm[2 * par + 1], ob1);
             if (anych) atomicOr(&dmask[2 * npar + (j >> 6)], 1ull << (j & 63));
-            colbuf[j] = (unsigned char)(cb ^ 1);
+            atomicXor(&cbm[j >> 6], 1ull << (j & 63));
           }
         }
       }
@@ -576,7 +524,8 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
         obm[2 * npar + 1] = 0ull;
       }
       const unsigned long long O0 = obm[2 * par], O1 = obm[2 * par + 1];
-      if (P.stamps) sub[3] += __popcll(O0) + __popcll(O1);
+      const unsigned long long SB0 = cbm[0], SB1 = cbm[1];
+
       int idx = 0;
       for (int w = 0; w < 2; ++w) {
         unsigned long long m = w ? O1 : O0;
@@ -588,11 +537,13 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
             const int jj = lane + 64 * c;
-            nw[c] = (jj < n) ? T0[colbuf[jj] * Tstr + v * n + jj] : n;
+            const int cbj = (int)(((c ? SB1 : SB0) >> lane) & 1ull);
+            nw[c] = (jj < n) ? T0[cbj * Tstr + v * n + jj] : n;
           }
           const int task = wave_select(n, v, lane, C, nw);
           if (task >= 0 && lane == 0) {
-            T0[colbuf[task] * Tstr + v * n + task] = (unsigned char)v;
+            const int cbt = (int)(((task < 64 ? SB0 : SB1) >> (task & 63)) & 1ull);
+            T0[cbt * Tstr + v * n + task] = (unsigned char)v;
             atomicOr(&dmask[2 * npar + (task >> 6)], 1ull << (task & 63));
           }
         }
@@ -605,14 +556,21 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
     else if (P.early_exit) break;  // fixed point
   }
   // consolidate the per-column buffers into T[0]
-  for (int k = tid; k < n * n; k += kBlock) {
-    const int jj = k % n;
-    if (colbuf[jj]) T0[k] = T0[Tstr + k];
+  {
+    const unsigned long long SB0 = cbm[0], SB1 = cbm[1];
+    for (int k = tid; k < n * n; k += kBlock) {
+      const int jj = k % n;
+      if (((jj < 64 ? SB0 : SB1) >> (jj & 63)) & 1ull) T0[k] = T0[Tstr + k];
+    }
   }
   __syncthreads();
   stamp(P, b, tid, 4);
   if (P.stamps && tid == 0)
     for (int k = 0; k < 4; ++k) P.stamps[(size_t)b * 16 + 8 + k] = sub[k];
+  if (P.stamps && tid == 0) {
+    P.stamps[(size_t)b * 16 + 12] = dbg_needcols;
+    P.stamps[(size_t)b * 16 + 13] = dbg_colcyc;
+  }
 
   // ---------------- phase 4: adoption --------------------------------------
   const unsigned char* Tf = T0;
@@ -651,224 +609,25 @@ __global__ void __launch_bounds__(kBlock) solve_kernel(const SolveParams P) {
   __syncthreads();
   stamp(P, b, tid, 5);
 
-  // ---------------- phase 5: control + safety -----------------------------
-  if (P.do_control) {
-    double* uo = out;           // [n][3] u
-    double* uso = out + 3 * n;  // [n][3] u_safe
-    const int E = rowptr[n];
-    const double* G = P.gains + 9 * P.gain_off[f];
-    const acl_cntrl_gains_t g = P.g;
-    const acl_safety_params_t sp = P.s;
-    double* caA = reinterpret_cast<double*>(C) + wave * (4 * n);               // angles
-    signed char* caS = reinterpret_cast<signed char*>(C) + kWaves * 4 * n * 8 + wave * 4 * n;
-    // the 3x3 blocks of the vehicle's formation row: lane = column j (two
-    // chunks of 64), coalesced across lanes in each of the 9 planes
-    auto load_row = [&](int v, double (&A)[2][9], bool (&has)[2]) {
-      const int i = myi[v];
-      int ebase = rowptr[i];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const unsigned long long rowbits = adjF[2 * i + c];
-        has[c] = (rowbits >> lane) & 1ull;
-        const int e = ebase + __popcll(rowbits & ((1ull << lane) - 1ull));
-        ebase += __popcll(rowbits);
-#pragma unroll
-        for (int k = 0; k < 9; ++k)
-          A[c][k] = has[c] ? __builtin_nontemporal_load(G + (size_t)k * E + e) : 0.0;
-      }
-    };
-    double Acur[2][9], Anx[2][9];
-    bool hcur[2], hnx[2];
-    if (wave < n) load_row(wave, Acur, hcur);
-    for (int v = wave; v < n; v += kWaves) {
-      // prefetch the next vehicle's gain blocks while this one computes
-      if (v + kWaves < n) load_row(v + kWaves, Anx, hnx);
-      const int i = myi[v];
-      const unsigned char* Ptv = validv[v] ? (Tf + v * n) : Ptin;
-      const double* gv = P.vel + ((size_t)b * n + v) * 3;
-      const double vel0 = gv[0], vel1 = gv[1], vel2 = gv[2];
-      const double qv0 = q[3 * v], qv1 = q[3 * v + 1], qv2 = q[3 * v + 2];
-      const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
-      const double Ni = pix * pix + piy * piy, Nzi = piz * piz;
-      double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int j = lane + 64 * c;
-        if (hcur[c]) {
-          const double* A = Acur[c];
-          const int u = Ptv[j];
-          const double q0 = q[3 * u] - qv0, q1 = q[3 * u + 1] - qv1, q2 = q[3 * u + 2] - qv2;
-          const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
-          const double Nj = pjx * pjx + pjy * pjy, Nzj = pjz * pjz;
-          const double dxy = sqrt((Ni + Nj) - 2.0 * (pix * pjx + piy * pjy));
-          const double dz = sqrt((Nzi + Nzj) - 2.0 * (piz * pjz));
-          const double e_xy = sqrt(q0 * q0 + q1 * q1) - dxy;
-          const double e_z = sqrt(q2 * q2) - dz;
-          double Fxy = 0.0, Fz = 0.0;
-          if (fabs(e_xy) > g.e_xy_thr) Fxy = g.K1_xy * atan(g.K2_xy * e_xy);
-          if (fabs(e_z) > g.e_z_thr) Fz = g.K1_z * atan(g.K2_z * e_z);
-          const double up0 = ((A[0] * q0 + A[1] * q1) + A[2] * q2) + Fxy * q0;
-          const double up1 = ((A[3] * q0 + A[4] * q1) + A[5] * q2) + Fxy * q1;
-          const double up2 = ((A[6] * q0 + A[7] * q1) + A[8] * q2) + Fz * q2;
-          acc0 += g.kp * up0 + g.kd * (-vel0);
-          acc1 += g.kp * up1 + g.kd * (-vel1);
-          acc2 += g.kp * up2 + g.kd * (-vel2);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        hcur[c] = hnx[c];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) Acur[c][k] = Anx[c][k];
-      }
-      double cmd0 = wave_sum(acc0), cmd1 = wave_sum(acc1), cmd2 = wave_sum(acc2);
-      if (lane == 0) {
-        uo[3 * v] = cmd0; uo[3 * v + 1] = cmd1; uo[3 * v + 2] = cmd2;
-      }
-      // Safety::cmdinCb saturation (safety.cpp:185-196)
-      {
-        const double velxy = sqrt(cmd0 * cmd0 + cmd1 * cmd1);
-        if (velxy > sp.max_vel_xy) {
-          cmd0 = cmd0 / velxy * sp.max_vel_xy;
-          cmd1 = cmd1 / velxy * sp.max_vel_xy;
-        }
-        const double velz = fabs(cmd2);
-        if (velz > sp.max_vel_z) cmd2 = cmd2 / velz * sp.max_vel_z;
-      }
-      // Safety::collisionAvoidance (safety.cpp:412-541)
-      bool modified = false;
-      {
-        bool cand[2];
-        double dxv[2], dyv[2], dv[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const int j = lane + 64 * c;
-          cand[c] = false;
-          if (j < n && j != v) {
-            dxv[c] = q[3 * j] - qv0;
-            dyv[c] = q[3 * j + 1] - qv1;
-            dv[c] = sqrt(dxv[c] * dxv[c] + dyv[c] * dyv[c]);
-            cand[c] = !(dv[c] > sp.d_avoid_thresh);
-          }
-        }
-        const unsigned long long m0 = __ballot(cand[0]), m1 = __ballot(cand[1]);
-        if (m0 | m1) {
-          bool wrapped = false;
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            if (cand[c]) {
-              const int slot = 4 * (__popcll((c ? m1 : m0) & ((1ull << lane) - 1ull)) +
-                                    (c ? __popcll(m0) : 0));
-              const double theta = atan2(dyv[c], dxv[c]);
-              const double x = sp.r_keep_out / dv[c];
-              const double alpha = fabs(asin(x < 1.0 ? x : 1.0));
-              const double beg = wrap_to_pi(theta - alpha);
-              const double end = wrap_to_pi(theta + alpha);
-              caA[slot] = beg;     caS[slot] = +1;
-              caA[slot + 1] = end; caS[slot + 1] = -1;
-              if (beg > end) {
-                wrapped = true;
-                caA[slot + 2] = -kPi; caS[slot + 2] = +1;
-                caA[slot + 3] = kPi;  caS[slot + 3] = -1;
-              } else {
-                caS[slot + 2] = 0;
-                caS[slot + 3] = 0;
-              }
-            }
-          }
-          const bool didWrap = __any(wrapped);
-          const int nslot = 4 * (__popcll(m0) + __popcll(m1));
-          __builtin_amdgcn_wave_barrier();
-          asm volatile("" ::: "memory");
-          if (lane == 0) {
-            // compact + insertion sort by (angle, sign) = std::sort on pairs
-            int ne = 0;
-            for (int k = 0; k < nslot; ++k) {
-              const signed char sg = caS[k];
-              if (sg == 0) continue;
-              const double a = caA[k];
-              int pos = ne;
-              while (pos > 0 && (a < caA[pos - 1] || (!(caA[pos - 1] < a) && sg < caS[pos - 1]))) {
-                caA[pos] = caA[pos - 1];
-                caS[pos] = caS[pos - 1];
-                --pos;
-              }
-              caA[pos] = a;
-              caS[pos] = sg;
-              ++ne;
-            }
-            // parenthesis-count union into zones, stored in place (nz <= ne/2)
-            int nz = 0, count = 0;
-            double start = 0.0;
-            for (int k = 0; k < ne; ++k) {
-              const double a = caA[k];
-              if (count == 0) start = a;
-              count += caS[k];
-              if (count == 0) {
-                caA[2 * nz] = start;
-                caA[2 * nz + 1] = a;
-                ++nz;
-              }
-            }
-            const double psi = atan2(cmd1, cmd0);
-            bool safe = true;
-            for (int k = 0; k < nz; ++k)
-              if (psi > caA[2 * k] && psi < caA[2 * k + 1]) { safe = false; break; }
-            if (!safe) {
-              modified = true;
-              // flatten zone edges (drop +-pi ones when wrapped), sort
-              int m = 0;
-              for (int k = 0; k < 2 * nz; ++k) {
-                const double a = caA[k];
-                if (!didWrap || fabs(a) != kPi) caA[m++] = a;
-              }
-              if (m == 0) {
-                cmd0 = cmd1 = 0.0;
-                cmd2 = 0.0;
-              } else {
-                for (int k = 1; k < m; ++k) {
-                  const double a = caA[k];
-                  int pos = k;
-                  while (pos > 0 && a < caA[pos - 1]) { caA[pos] = caA[pos - 1]; --pos; }
-                  caA[pos] = a;
-                }
-                int it = 0;  // std::lower_bound
-                while (it < m && caA[it] < psi) ++it;
-                int idx;
-                if (it == 0) idx = 0;
-                else if (it == m || fabs(caA[it - 1] - psi) < fabs(caA[it] - psi)) idx = it - 1;
-                else idx = it;
-                const double edge = caA[idx];
-                if (fabs(wrap_to_pi(edge - psi)) <= kPi / 2) {
-                  const double umag = sqrt(cmd0 * cmd0 + cmd1 * cmd1);
-                  cmd0 = umag * cos(edge);
-                  cmd1 = umag * sin(edge);
-                } else {
-                  cmd0 = cmd1 = 0.0;
-                  cmd2 = 0.0;
-                }
-              }
-            }
-          }
-          __builtin_amdgcn_wave_barrier();
-          asm volatile("" ::: "memory");
-        }
-      }
-      if (lane == 0) {
-        uso[3 * v] = cmd0; uso[3 * v + 1] = cmd1; uso[3 * v + 2] = cmd2;
-        cao[v] = modified;
-        if (modified) atomicAdd(&misc[M_NCA], 1);
+  // ---------------- hand-off to the control kernel ------------------------
+  // Each vehicle's adopted inverse assignment (formation point -> vehicle):
+  // one shared row when every vehicle adopts the same one (all tables valid
+  // and identical, or none valid), else one row per vehicle.
+  {
+    const bool allvalid = misc[M_NINV] == 0;
+    const bool uniform = (allvalid && misc[M_AGREE]) || misc[M_NINV] == n;
+    unsigned char* wsPt = P.ws + (size_t)b * n;
+    if (tid == 0) P.ws[(size_t)P.B * n + b] = uniform ? 0 : 1;
+    if (uniform) {
+      for (int jj = tid; jj < n; jj += kBlock) wsPt[jj] = allvalid ? Tf[jj] : Ptin[jj];
+    } else {
+      unsigned char* rows = P.ws + (size_t)P.B * (n + 1) + (size_t)b * n * n;
+      for (int k = tid; k < n * n; k += kBlock) {
+        const int v = k / n, jj = k - v * n;
+        rows[k] = validv[v] ? Tf[k] : Ptin[jj];
       }
     }
-    __syncthreads();
-    for (int k = tid; k < 3 * n; k += kBlock) {
-      if (P.u) P.u[(size_t)b * n * 3 + k] = uo[k];
-      if (P.u_safe) P.u_safe[(size_t)b * n * 3 + k] = uso[k];
-    }
-    if (P.ca_flag)
-      for (int v = tid; v < n; v += kBlock) P.ca_flag[(size_t)b * n + v] = cao[v];
   }
-
   stamp(P, b, tid, 6);
   if (tid == 0) {
     acl_swarm_status_t st = {};
@@ -901,6 +660,25 @@ extern "C" int32_t acl_max_vehicles(void) { return acl_amd::kMaxN; }
 static unsigned long long* g_stamps = nullptr;
 extern "C" void acl_internal_set_stamps(unsigned long long* stamps) { g_stamps = stamps; }
 
+#include "control_params.h"
+
+extern "C" size_t acl_solve_workspace_bytes(int32_t n, int32_t B) {
+  if (n < 1 || B < 0) return 0;
+  return (size_t)B * ((size_t)n + 1 + (size_t)n * n);
+}
+
+namespace {
+// Second stream + events for the auction -> control pipeline (one set per
+// device, created on first use).
+struct Pipe {
+  hipStream_t ctl = nullptr;
+  hipEvent_t ev[16] = {};
+  hipEvent_t done = nullptr;
+  bool ok = false;
+};
+Pipe g_pipe[16];
+}  // namespace
+
 extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_solve_args_t* a,
                                         void* stream) {
   using namespace acl_amd;
@@ -911,15 +689,16 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   if (a->B == 0) return ACL_OK;
   if (!F->p || !F->adj || !a->fidx || !a->q || !a->P_in || !a->P_out || !a->status)
     return acl__set_error("acl_solve_batch: required pointer is NULL");
-  if (a->do_control && (!F->gains || !F->gain_off || !a->vel))
-    return acl__set_error("acl_solve_batch: do_control needs gains, gain_off and vel");
+  if (a->do_control && (!F->gains || !F->gain_off || !a->vel || !a->workspace))
+    return acl__set_error("acl_solve_batch: do_control needs gains, gain_off, vel and workspace");
   SolveParams P;
-  P.n = n; P.B = a->B; P.F = F->n_formations;
+  P.n = n; P.B = a->B; P.F = F->n_formations; P.b0 = 0;
   P.p = F->p; P.adj = F->adj; P.gains = F->gains; P.gain_off = F->gain_off;
   P.fidx = a->fidx; P.q = a->q; P.vel = a->vel; P.P_in = a->P_in; P.P_out = a->P_out;
   P.status = a->status; P.u = a->u; P.u_safe = a->u_safe; P.ca_flag = a->ca_flag;
   P.who = a->who; P.g = a->cntrl; P.s = a->safety;
   P.early_exit = a->early_exit; P.do_control = a->do_control;
+  P.ws = (unsigned char*)a->workspace;
   P.stamps = g_stamps;
   const Layout L = make_layout(n);
   static int configured = 0;
@@ -929,8 +708,48 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
       return acl__set_error("hipFuncSetAttribute failed");
     configured = 1;
   }
-  hipLaunchKernelGGL(solve_kernel, dim3(a->B), dim3(kBlock), L.total, (hipStream_t)stream, P);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+  hipStream_t s = (hipStream_t)stream;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  Pipe& pp = g_pipe[dev & 15];
+  if (a->do_control && !pp.ok) {
+    if (hipStreamCreateWithFlags(&pp.ctl, hipStreamNonBlocking) != hipSuccess)
+      return acl__set_error("hipStreamCreateWithFlags failed");
+    for (auto& e : pp.ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&pp.done, hipEventDisableTiming);
+    pp.ok = true;
+  }
+  // the control stream may not run ahead of work already queued on `s`
+  if (a->do_control) {
+    (void)hipEventRecord(pp.done, s);
+    (void)hipStreamWaitEvent(pp.ctl, pp.done, 0);
+  }
+  // chunks: the control kernel of chunk k overlaps the auction of chunk k+1
+  const int chunk = a->B <= 4096 ? a->B : ((a->B + 7) / 8 + 255) / 256 * 256;
+  int k = 0;
+  for (int b0 = 0; b0 < a->B; b0 += chunk, ++k) {
+    const int nb = (a->B - b0) < chunk ? (a->B - b0) : chunk;
+    P.b0 = b0;
+    hipLaunchKernelGGL(solve_kernel, dim3(nb), dim3(kBlock), L.total, s, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+    if (a->do_control) {
+      hipEvent_t ev = pp.ev[k & 15];
+      (void)hipEventRecord(ev, s);
+      (void)hipStreamWaitEvent(pp.ctl, ev, 0);
+      CtlParams C;
+      C.n = n; C.B = a->B; C.b0 = b0;
+      C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
+      C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P_out;
+      C.status = a->status; C.u = a->u; C.u_safe = a->u_safe; C.ca_flag = a->ca_flag;
+      C.ws = (const unsigned char*)a->workspace; C.g = a->cntrl; C.s = a->safety;
+      e = launch_control(C, nb, pp.ctl);
+      if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+    }
+  }
+  if (a->do_control) {
+    (void)hipEventRecord(pp.done, pp.ctl);
+    (void)hipStreamWaitEvent(s, pp.done, 0);
+  }
   return ACL_OK;
 }

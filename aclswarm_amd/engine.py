@@ -76,6 +76,20 @@ class FormationTable:
                             self.gains.data_ptr(), self.gain_off.data_ptr())
 
 
+_WS = {}
+
+
+def workspace(n, B, device):
+    """Device workspace for acl_solve_batch (cached per device, grown on demand)."""
+    need = int(L.lib().acl_solve_workspace_bytes(n, B))
+    key = str(device)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(max(need, 1), dtype=torch.uint8, device=device)
+        _WS[key] = ws
+    return ws
+
+
 def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
           do_control=True, want_who=False, out=None, stream=None):
     """Run acl_solve_batch for B = q.shape[0] swarms. All tensors on device.
@@ -106,6 +120,7 @@ def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
     a.u_safe = out["u_safe"].data_ptr() if out.get("u_safe") is not None else None
     a.ca_flag = out["ca_flag"].data_ptr() if out.get("ca_flag") is not None else None
     a.who = out["who"].data_ptr() if out.get("who") is not None else None
+    a.workspace = workspace(n, B, dev).data_ptr()
     a.cntrl = cntrl or L.default_gains()
     a.safety = safety or L.default_safety()
     a.early_exit = int(bool(early_exit))

@@ -161,6 +161,14 @@ typedef struct {
  *   ca_flag [B][n]     VelocityGoal::modified (NULL ok)
  *   who     [B][n][n]  optional final CBAA tables, vehicle rows (NULL ok);
  *                      0xFFFF = unassigned (who == -1)
+ *   workspace          device scratch of acl_solve_workspace_bytes(n, B)
+ *                      bytes (required when do_control): the auction kernel
+ *                      hands each vehicle's adopted assignment to the
+ *                      control kernel through it.
+ * The call enqueues, per chunk of swarms, the auction kernel on `stream` and
+ * the control kernel on an internal second stream (fork/join with events),
+ * so one chunk's gain stream overlaps the next chunk's auction. Completion
+ * is ordered on `stream`.
  */
 typedef struct {
   int32_t B;
@@ -174,6 +182,7 @@ typedef struct {
   double* u_safe;
   uint8_t* ca_flag;
   uint16_t* who;
+  void* workspace;
   acl_cntrl_gains_t cntrl;
   acl_safety_params_t safety;
   int32_t early_exit; /* 1: stop at the first fixed point (bit-exact), 0: run
@@ -183,6 +192,9 @@ typedef struct {
 
 /* Largest n the batched solve kernel accepts. */
 int32_t acl_max_vehicles(void);
+
+/* Bytes of device workspace acl_solve_batch needs for B swarms of n. */
+size_t acl_solve_workspace_bytes(int32_t n, int32_t B);
 
 acl_status_t acl_solve_batch(const acl_formations_t* formations,
                              const acl_solve_args_t* args, void* stream);

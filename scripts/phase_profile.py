@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from aclswarm_amd import _lib as L  # noqa: E402
 from aclswarm_amd import engine, workload  # noqa: E402
 
-NAMES = ["load+nbhd", "align", "prices", "cbaa", "adopt", "control+safety"]
+NAMES = ["load+nbhd", "align", "prices", "cbaa", "adopt", "handoff"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--B", type=int, default=8192)
@@ -42,6 +42,6 @@ print(f"per-swarm cycles: mean {tot.mean():.0f}  median {np.median(tot):.0f}")
 for k, nm in enumerate(NAMES):
     print(f"  {nm:16s} mean {d[:, k].mean():10.0f}  share {d[:, k].sum() / tot.sum() * 100:5.1f}%")
 sub = s[:, 8:12]
-for k, nm in enumerate(["  dirty cols A+B", "  select", "  #dirty cols", "  #selects"]):
+for k, nm in enumerate(["  dirty cols A+B", "  select", "  #dirty cols", "  #cols wave0"]):
     print(f"  {nm:16s} mean {sub[:, k].mean():10.0f}")
-print("eff rounds mean", float(np.mean(np.frombuffer(b"", dtype=np.uint8))) if False else "")
+print("  wave0 cols needing scan", s[:, 12].mean(), " wave0 in-column cycles", s[:, 13].mean())
