@@ -30,6 +30,19 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned ux) {
   return (unsigned)__builtin_amdgcn_readlane(x, 63);
 }
 
+__device__ __forceinline__ unsigned wave_or_u32(unsigned ux) {
+  int x = (int)ux;
+#define ACL_UOR(a, b) ((a) | (b))
+  ACL_DPP_STEP(x, ACL_UOR, 0xB1, 0xF);
+  ACL_DPP_STEP(x, ACL_UOR, 0x4E, 0xF);
+  ACL_DPP_STEP(x, ACL_UOR, 0x124, 0xF);
+  ACL_DPP_STEP(x, ACL_UOR, 0x128, 0xF);
+  ACL_DPP_STEP(x, ACL_UOR, 0x142, 0xA);
+  ACL_DPP_STEP(x, ACL_UOR, 0x143, 0xC);
+#undef ACL_UOR
+  return (unsigned)__builtin_amdgcn_readlane(x, 63);
+}
+
 __device__ __forceinline__ float wave_max_f32(float fx) {
   int x = __float_as_int(fx);
 #define ACL_FMAX(a, b) __float_as_int(fmaxf(__int_as_float(a), __int_as_float(b)))

@@ -68,8 +68,8 @@ __host__ __device__ inline Layout make_layout(int n) {
   L.C = o;
   {
     const int csz = (n + 1) * n * 4;
-    const int ca = kWaves * 4 * n * 9;         // collision-avoidance scratch
-    o = align16(o + (csz > ca ? csz : ca));
+    const int sc = 64 * n;                     // alignment-sum scratch
+    o = align16(o + (csz > sc ? csz : sc));
   }
   L.T0 = o;     o = align16(o + n * n);
   L.T1 = o;     o = align16(o + n * n);
@@ -209,16 +209,6 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
       Ptin[pv] = (unsigned char)v;
     }
   }
-  // rows of the formation CSR (edge e of row i in row-major order); the
-  // diagonal is an edge of the control law if adjmat(i,i) != 0 (distcntrl.cpp:62)
-  if (tid == 0) {
-    int acc = 0;
-    for (int i = 0; i < n; ++i) {
-      rowptr[i] = acc;
-      acc += __popcll(adjF[2 * i]) + __popcll(adjF[2 * i + 1]);
-    }
-    rowptr[n] = acc;
-  }
   __syncthreads();
   if (misc[M_BAD]) {
     // P_in is not a permutation: the reference never holds such a P.
@@ -248,80 +238,115 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
     qf[2 * j + 1] = q[3 * vj + 1];
   }
   // vehicle-space closed neighbourhoods: u ~ v iff u == v or adj(P[v], P[u])
-  // (bidIterComplete, auctioneer.cpp:419-437). Lane = v, uniform loop over u.
-  for (int v = tid; v < ((n + 63) & ~63); v += kBlock) {
-    const int i = (v < n) ? Pin[v] : 0;
-    const unsigned long long a0 = adjF[2 * i], a1 = adjF[2 * i + 1];
-    unsigned long long m0 = 0, m1 = 0;
-    for (int u = 0; u < n; ++u) {
-      const int pu = Pin[u];
-      const bool e = (u == v) || (((pu < 64 ? a0 : a1) >> (pu & 63)) & 1ull);
-      if (u < 64) m0 |= (unsigned long long)e << u;
-      else m1 |= (unsigned long long)e << (u - 64);
-    }
-    if (v < n) {
-      vadj[2 * v] = m0;
-      vadj[2 * v + 1] = m1;
+  // (bidIterComplete, auctioneer.cpp:419-437); one wave per vehicle, lanes
+  // over u, one ballot per 64-bit word
+  {
+    const int pu0 = (lane < n) ? Pin[lane] : 0;
+    const int pu1 = (64 + lane < n) ? Pin[64 + lane] : 0;
+    for (int v = wave; v < n; v += kWaves) {
+      const int i = Pin[v];
+      const unsigned long long a0 = adjF[2 * i], a1 = adjF[2 * i + 1];
+      const bool e0 = (lane < n) && ((lane == v) || (((pu0 < 64 ? a0 : a1) >> (pu0 & 63)) & 1ull));
+      const bool e1 = (64 + lane < n) &&
+                      ((64 + lane == v) || (((pu1 < 64 ? a0 : a1) >> (pu1 & 63)) & 1ull));
+      const unsigned long long m0 = __ballot(e0), m1 = __ballot(e1);
+      if (lane == 0) {
+        vadj[2 * v] = m0;
+        vadj[2 * v + 1] = m1;
+      }
     }
   }
   __syncthreads();
   stamp(P, b, tid, 1);
 
-  // ---------------- phase 1: alignment (one thread per vehicle) ----------
-  // Uniform loop over formation points j (broadcast LDS reads), predicated
-  // on "j in my closed neighbourhood": the sums stay sequential in
-  // ascending j, exactly as Eigen's rowwise().sum() / GEMM accumulate.
-  for (int v = tid; v < ((n + 63) & ~63); v += kBlock) {
+  // ---------------- phase 1: alignment -------------------------------------
+  // Eigen::umeyama's sums run sequentially in ascending neighbour order; each
+  // of the 4 sums of a pass is one thread's sequential loop (4 threads per
+  // vehicle), so the order -- and every rounding -- is the reference's.
+  double* sums = reinterpret_cast<double*>(C);  // [n][8] scratch (C is filled later)
+  {
+    const int v = tid >> 2, c = tid & 3;
+    const bool act = v < n;
+    const int i = act ? Pin[v] : 0;
+    unsigned long long r0 = adjF[2 * i], r1 = adjF[2 * i + 1];
+    if (i < 64) r0 |= 1ull << i; else r1 |= 1ull << (i - 64);
+    // pass 1: rowwise().sum() of src (p) and dst (q in formation space)
+    const double* src = (c < 2) ? (p + c) : (qf + (c - 2));
+    const int stride = (c < 2) ? 3 : 2;
+    double acc = 0.0;
+    bool first = true;
+    for (int j0 = 0; j0 < n; j0 += 4) {
+      double val[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) val[x] = (j0 + x < n) ? src[(j0 + x) * stride] : 0.0;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int j = j0 + x;
+        const bool in = (j < n) && (((j < 64 ? r0 : r1) >> (j & 63)) & 1ull);
+        if (in) {
+          acc = first ? val[x] : acc + val[x];
+          first = false;
+        }
+      }
+    }
+    if (act) sums[8 * v + c] = acc;
+  }
+  __syncthreads();
+  {
+    const int v = tid >> 2, c = tid & 3;
     const bool act = v < n;
     const int i = act ? Pin[v] : 0;
     unsigned long long r0 = adjF[2 * i], r1 = adjF[2 * i + 1];
     if (i < 64) r0 |= 1ull << i; else r1 |= 1ull << (i - 64);
     const int k = __popcll(r0) + __popcll(r1);
-    double ssx = 0, ssy = 0, sdx = 0, sdy = 0;
-    bool first = true;
-    for (int j = 0; j < n; ++j) {
-      const bool in = ((j < 64 ? r0 : r1) >> (j & 63)) & 1ull;
-      const double px = p[3 * j], py = p[3 * j + 1], qx = qf[2 * j], qy = qf[2 * j + 1];
-      if (in) {
-        if (first) { ssx = px; ssy = py; sdx = qx; sdy = qy; first = false; }
-        else { ssx = ssx + px; ssy = ssy + py; sdx = sdx + qx; sdy = sdy + qy; }
-      }
-    }
     const double oon = 1.0 / (double)k;
-    const double sm[2] = {ssx * oon, ssy * oon};
-    const double dm[2] = {sdx * oon, sdy * oon};
+    // pass 2: a_(di,sj) = sum_j dst_demean[di] * src_demean[sj]; c = 2*di + sj
+    const int di = c >> 1, sj = c & 1;
+    const double smj = act ? sums[8 * v + sj] * oon : 0.0;
+    const double dmi = act ? sums[8 * v + 2 + di] * oon : 0.0;
     // sigma = one_over_n * dst_demean * src_demean^T: lazy product (scaled
     // lhs) when k + 4 < 20, GEMM (alpha after the sum) otherwise
     const bool lazy = (k + 4) < 20;
-    double a00 = 0, a01 = 0, a10 = 0, a11 = 0;  // a_ij = sum dst_i * src_j
-    first = true;
-    for (int j = 0; j < n; ++j) {
-      const bool in = ((j < 64 ? r0 : r1) >> (j & 63)) & 1ull;
-      const double s0 = p[3 * j] - sm[0], s1 = p[3 * j + 1] - sm[1];
-      double d0 = qf[2 * j] - dm[0], d1 = qf[2 * j + 1] - dm[1];
-      if (lazy) {
-        d0 = oon * d0;
-        d1 = oon * d1;
+    double acc = 0.0;
+    bool first = true;
+    for (int j0 = 0; j0 < n; j0 += 4) {
+      double sv[4], dv[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int j = (j0 + x < n) ? j0 + x : 0;
+        sv[x] = p[3 * j + sj];
+        dv[x] = qf[2 * j + di];
       }
-      if (in) {
-        if (lazy && first) {
-          a00 = d0 * s0; a01 = d0 * s1; a10 = d1 * s0; a11 = d1 * s1;
-        } else {
-          a00 = a00 + d0 * s0; a01 = a01 + d0 * s1;
-          a10 = a10 + d1 * s0; a11 = a11 + d1 * s1;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int j = j0 + x;
+        const bool in = (j < n) && (((j < 64 ? r0 : r1) >> (j & 63)) & 1ull);
+        const double s0 = sv[x] - smj;
+        double d0 = dv[x] - dmi;
+        if (lazy) d0 = oon * d0;
+        if (in) {
+          acc = (lazy && first) ? d0 * s0 : acc + d0 * s0;
+          first = false;
         }
-        first = false;
       }
     }
-    double S[4];  // column-major sigma
-    if (lazy) { S[0] = a00; S[1] = a10; S[2] = a01; S[3] = a11; }
-    else { S[0] = a00 * oon; S[1] = a10 * oon; S[2] = a01 * oon; S[3] = a11 * oon; }
+    if (act) sums[8 * v + 4 + c] = lazy ? acc : acc * oon;
+  }
+  __syncthreads();
+  for (int v = tid; v < n; v += kBlock) {
+    const int i = Pin[v];
+    unsigned long long r0 = adjF[2 * i], r1 = adjF[2 * i + 1];
+    if (i < 64) r0 |= 1ull << i; else r1 |= 1ull << (i - 64);
+    const int k = __popcll(r0) + __popcll(r1);
+    const double oon = 1.0 / (double)k;
+    const double sm[2] = {sums[8 * v] * oon, sums[8 * v + 1] * oon};
+    const double dm[2] = {sums[8 * v + 2] * oon, sums[8 * v + 3] * oon};
+    // column-major sigma: S(di, sj) = a_(di, sj)
+    const double S[4] = {sums[8 * v + 4], sums[8 * v + 6], sums[8 * v + 5], sums[8 * v + 7]};
     double R[4], t[2];
     umeyama_finish(S, sm, dm, R, t);
-    if (act) {
-      double* o = out + 6 * v;
-      o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
-    }
+    double* o = out + 6 * v;
+    o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
   }
   __syncthreads();
   stamp(P, b, tid, 2);
@@ -373,6 +398,14 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
 
   int eff = 0;
   const int max_rounds = 2 * n;  // cbaa_max_iter_ = n * diameter (:50-51)
+  // closed neighbourhood masks of this lane's vehicles (lane, lane + 64)
+  unsigned long long vmy0[2], vmy1[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int v = lane + 64 * c;
+    vmy0[c] = (v < n) ? vadj[2 * v] : 0ull;
+    vmy1[c] = (v < n) ? vadj[2 * v + 1] : 0ull;
+  }
   unsigned long long sub[4] = {0, 0, 0, 0};
   unsigned long long dbg_needcols = 0, dbg_colcyc = 0;
   unsigned long long tprev = P.stamps ? __builtin_amdgcn_s_memtime() : 0;
@@ -417,8 +450,8 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
             if (u < n) {
               wu[c] = Tc[u * n + j];
               key[c] = __float_as_uint(C[wu[c] * n + j]) + 1u;
-              vm0[c] = vadj[2 * u];
-              vm1[c] = vadj[2 * u + 1];
+              vm0[c] = vmy0[c];
+              vm1[c] = vmy1[c];
             }
           }
           // A) price levels of the column, highest first, computed lazily:
@@ -573,32 +606,42 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
   }
 
   // ---------------- phase 4: adoption --------------------------------------
+  // isValidAssignment (auctioneer.cpp:325-343) on each vehicle's table: one
+  // wave per vehicle, lanes over tasks; a permutation <=> every entry < n and
+  // the OR of the one-hot entries has n bits.
   const unsigned char* Tf = T0;
-  for (int v = tid; v < n; v += kBlock) {
+  for (int v = wave; v < n; v += kWaves) {
     const unsigned char* row = Tf + v * n;
-    unsigned long long s0 = 0, s1 = 0;
-    bool valid = true, agree = true;
-    int mine = -1;
-    for (int j = 0; j < n; ++j) {
-      const int w = row[j];
-      if (w >= n) { valid = false; continue; }
-      const unsigned long long bit = 1ull << (w & 63);
-      unsigned long long& s = (w < 64) ? s0 : s1;
-      if (s & bit) valid = false;
-      s |= bit;
-      if (w == v && mine < 0) mine = j;
+    int w[2];
+    unsigned lo[4] = {0u, 0u, 0u, 0u};
+    bool bad = false, diff = false, ismine[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int jj = lane + 64 * c;
+      w[c] = (jj < n) ? row[jj] : -1;
+      ismine[c] = (jj < n) && (w[c] == v);
+      if (jj < n) {
+        if (w[c] >= n) bad = true;
+        else lo[w[c] >> 5] |= 1u << (w[c] & 31);
+        diff |= (w[c] != Tf[jj]);
+      }
     }
-    for (int j = 0; j < n && agree; ++j) agree = (row[j] == Tf[j]);
-    if (!valid || mine < 0) {
-      valid = false;
-      mine = Pin[v];
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cnt += __popc(wave_or_u32(lo[k]));
+    const unsigned long long mm0 = __ballot(ismine[0]), mm1 = __ballot(ismine[1]);
+    const bool valid = !__any(bad) && cnt == n && (mm0 | mm1) != 0ull;
+    const bool agree = !__any(diff);
+    const int mine = valid ? (mm0 ? __ffsll((long long)mm0) - 1 : 64 + __ffsll((long long)mm1) - 1)
+                           : Pin[v];
+    if (lane == 0) {
+      validv[v] = valid;
+      myi[v] = (unsigned char)mine;
+      if (!valid) atomicAdd(&misc[M_NINV], 1);
+      if (!agree) misc[M_AGREE] = 0;
+      if (mine != Pin[v]) misc[M_CHANGED] = 1;
+      P.P_out[(size_t)b * n + v] = (uint16_t)mine;
     }
-    validv[v] = valid;
-    myi[v] = (unsigned char)mine;
-    if (!valid) atomicAdd(&misc[M_NINV], 1);
-    if (!agree) misc[M_AGREE] = 0;
-    if (mine != Pin[v]) misc[M_CHANGED] = 1;
-    P.P_out[(size_t)b * n + v] = (uint16_t)mine;
   }
   if (P.who) {
     for (int k = tid; k < n * n; k += kBlock) {
