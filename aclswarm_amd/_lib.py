@@ -115,6 +115,11 @@ def lib():
     L.acl_stream_synchronize.argtypes = [VP]
     L.acl_stream_synchronize.restype = ct.c_int
     L.acl_last_error.restype = ct.c_char_p
+    # diagnostics (not in the public header)
+    L.acl_internal_kernel_timing.argtypes = [ct.c_int]
+    L.acl_internal_kernel_timing.restype = None
+    L.acl_internal_kernel_times.argtypes = [ct.POINTER(ct.c_double), ct.POINTER(ct.c_int)]
+    L.acl_internal_kernel_times.restype = ct.c_int
     _lib = L
     return L
 

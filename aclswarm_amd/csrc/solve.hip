@@ -720,7 +720,51 @@ struct Pipe {
   bool ok = false;
 };
 Pipe g_pipe[16];
+
+// Diagnostic per-launch kernel timing (not part of the public ABI): events on
+// the stream each kernel runs on, so bench.py can time the auction and the
+// control kernel separately while they overlap.
+struct KTiming {
+  bool on = false;
+  int n[2] = {0, 0};
+  hipEvent_t ev[2][64][2] = {};
+};
+KTiming g_kt;
+
+void kt_record(int kind, int which, hipStream_t s) {
+  if (!g_kt.on) return;
+  const int i = g_kt.n[kind];
+  if (i >= 64) return;
+  hipEvent_t& e = g_kt.ev[kind][i][which];
+  if (!e) (void)hipEventCreate(&e);
+  (void)hipEventRecord(e, s);
+  if (which == 1) g_kt.n[kind] = i + 1;
+}
 }  // namespace
+
+// enable != 0 starts a fresh timing window; 0 stops recording.
+extern "C" void acl_internal_kernel_timing(int enable) {
+  g_kt.on = enable != 0;
+  if (enable) g_kt.n[0] = g_kt.n[1] = 0;
+}
+
+// Sums the recorded launches: ms[0]/count[0] auction kernel, ms[1]/count[1]
+// control kernel. Synchronises on the recorded events.
+extern "C" int acl_internal_kernel_times(double* ms, int* count) {
+  for (int k = 0; k < 2; ++k) {
+    double t = 0.0;
+    for (int i = 0; i < g_kt.n[k]; ++i) {
+      float x = 0.f;
+      if (hipEventSynchronize(g_kt.ev[k][i][1]) != hipSuccess ||
+          hipEventElapsedTime(&x, g_kt.ev[k][i][0], g_kt.ev[k][i][1]) != hipSuccess)
+        return -1;
+      t += x;
+    }
+    ms[k] = t;
+    count[k] = g_kt.n[k];
+  }
+  return 0;
+}
 
 extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_solve_args_t* a,
                                         void* stream) {
@@ -773,7 +817,9 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   for (int b0 = 0; b0 < a->B; b0 += chunk, ++k) {
     const int nb = (a->B - b0) < chunk ? (a->B - b0) : chunk;
     P.b0 = b0;
+    kt_record(0, 0, s);
     hipLaunchKernelGGL(solve_kernel, dim3(nb), dim3(kBlock), L.total, s, P);
+    kt_record(0, 1, s);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
     if (a->do_control) {
@@ -786,7 +832,9 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
       C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P_out;
       C.status = a->status; C.u = a->u; C.u_safe = a->u_safe; C.ca_flag = a->ca_flag;
       C.ws = (const unsigned char*)a->workspace; C.g = a->cntrl; C.s = a->safety;
+      kt_record(1, 0, pp.ctl);
       e = launch_control(C, nb, pp.ctl);
+      kt_record(1, 1, pp.ctl);
       if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
     }
   }

@@ -14,6 +14,7 @@ RCCL gather of assignments + statistics to rank 0.
 Prints ONE JSON line on rank 0 (the driver's contract).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -34,18 +35,40 @@ METRIC = "swarm assignment+control solves/sec (N=100) at 1/2/4/8 MI355X; % HBM r
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def algorithmic_bytes(w, B):
-    """Bytes the solve must move per launch (each input read once, each
-    output written once). Per swarm: fidx 4, q 24n, vel 24n, P_in 2n,
-    P_out 2n, status 16, u 24n, u_safe 24n, ca n. Per formation used: p 24n,
-    adjacency bits 8nW, gain_off 8, gains 72 E_f."""
+def algorithmic_bytes(w, lo, hi):
+    """Bytes the solve of swarms [lo, hi) must move (each input read once,
+    each output written once), split by the kernel that owns
+    them. Auction kernel, per swarm: fidx 4, q 24n, P_in 2n, P_out 2n,
+    status 16; per formation used: p 24n, adjacency bits 8nW. Control
+    kernel, per swarm: vel 24n, u 24n, u_safe 24n, ca n; per formation used:
+    gain_off 8, gains 72 E_f. Re-reads (the control kernel's q, p, adjacency,
+    P_out, the workspace hand-off) are implementation traffic, not counted."""
     n = w["n"]
     W = (n + 63) // 64
-    per_swarm = 4 + n * (24 + 24 + 2 + 2 + 24 + 24 + 1) + 16
-    used = torch.unique(w["fidx"][:B])
+    Bc = hi - lo
+    used = torch.unique(w["fidx"][lo:hi])
     E = w["E"][used].sum().item()
-    per_form = used.numel() * (24 * n + 8 * n * W + 8) + 72 * E
-    return B * per_swarm + per_form, E / used.numel()
+    auction = Bc * (4 + n * (24 + 2 + 2) + 16) + used.numel() * (24 * n + 8 * n * W)
+    control = Bc * n * (24 + 24 + 24 + 1) + used.numel() * 8 + 72 * E
+    return auction, control, E / used.numel()
+
+
+def pmc_traffic(n, B, kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/r*_pmc_traffic.json, scripts/gpu_pmc.sh + pmc_summary.py) when
+    it was measured on this same configuration; else None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    for f in reversed(files):
+        d = json.load(open(f))
+        if d["config"]["n"] == n and d["config"]["B_per_gpu"] == B and kernel in d["kernels"]:
+            return d["kernels"][kernel]["hbm_bytes"], os.path.relpath(f, ROOT)
+    return None, None
+
+
+def chunk_size(B):
+    """acl_solve_batch's chunking (solve.hip): one launch per chunk."""
+    return B if B <= 4096 else ((B + 7) // 8 + 255) // 256 * 256
 
 
 def cpu_baseline(w, out, budget_s, nthreads):
@@ -153,6 +176,8 @@ def main():
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
+    lib = L.lib()
+    lib.acl_internal_kernel_timing(1)   # HIP events around each launch, on its stream
     t0 = time.perf_counter()
     res = None
     for k in range(args.steps):
@@ -166,15 +191,34 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    call_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kms = (ctypes.c_double * 2)()
+    kcnt = (ctypes.c_int * 2)()
+    if lib.acl_internal_kernel_times(kms, kcnt) != 0:
+        raise RuntimeError("kernel timing failed")
+    lib.acl_internal_kernel_timing(0)
     dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt_max = float(dt_t.item())
     stats = D.stats_dict(res[1], res[2])
 
-    nbytes, e_avg = algorithmic_bytes(w, B)
-    achieved = nbytes / (kern_ms * 1e-3) / 1e9
+    # algorithmic bytes per launch (the chunk every launch but the last covers)
+    ch = chunk_size(B)
+    nlaunch = (B + ch - 1) // ch
+    a_all, c_all, e_avg = algorithmic_bytes(w, 0, B)
+    per_launch = {"auction": a_all / nlaunch, "control": c_all / nlaunch}
+    kern = {}
+    for k, (name, sym) in enumerate((("auction", "acl_amd::solve_kernel"),
+                                     ("control", "acl_amd::control_kernel"))):
+        avg = kms[k] / max(kcnt[k], 1)
+        ach = per_launch[name] / (avg * 1e-3) / 1e9
+        traffic, tsrc = pmc_traffic(n, B, sym) if args.formations == 0 else (None, None)
+        kern[name] = {"kernel": sym, "launches_per_step": nlaunch, "avg_launch_ms": avg,
+                      "bytes_per_launch": per_launch[name], "achieved_GBs": ach,
+                      "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc}
+    dom = max(kern, key=lambda k: kern[k]["avg_launch_ms"])
+    pipe_ach = (a_all + c_all) / (call_ms * 1e-3) / 1e9
     line = {
         "metric": METRIC,
         "value": world * B / dt_max,
@@ -199,10 +243,17 @@ def main():
             "gains": "synthetic random 3x3 blocks (values do not affect throughput)",
         },
         "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": "acl_amd::solve_kernel", "kernel_ms": kern_ms,
-            "bytes_per_launch": nbytes,
+            "bound": "hbm", "achieved": kern[dom]["achieved_GBs"], "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": kern[dom]["frac"], "traffic": kern[dom]["traffic"],
+            "traffic_source": kern[dom]["traffic_source"],
+            "kernel": kern[dom]["kernel"], "avg_launch_ms": kern[dom]["avg_launch_ms"],
+            "bytes_per_launch": kern[dom]["bytes_per_launch"],
+            "note": "dominant kernel by time; the auction kernel is LDS/VALU-bound "
+                    "(CBAA tables live in LDS), see DESIGN.md",
+            "kernels": kern,
+            "pipeline": {"what": "whole acl_solve_batch call (both kernels overlapped)",
+                         "call_ms": call_ms, "bytes": a_all + c_all,
+                         "achieved_GBs": pipe_ach, "frac": pipe_ach / HBM_PEAK_GBS},
         },
         "stats": stats,
         "gen_s": t_gen,
