@@ -120,6 +120,8 @@ def lib():
     L.acl_internal_kernel_timing.restype = None
     L.acl_internal_kernel_times.argtypes = [ct.POINTER(ct.c_double), ct.POINTER(ct.c_int)]
     L.acl_internal_kernel_times.restype = ct.c_int
+    L.acl_internal_admm_flop_counter.argtypes = [VP]
+    L.acl_internal_admm_flop_counter.restype = None
     _lib = L
     return L
 

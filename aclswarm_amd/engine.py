@@ -136,3 +136,29 @@ def status_to_numpy(status_u8):
     """[B][16] uint8 device/host tensor -> structured numpy array."""
     arr = status_u8.detach().cpu().numpy()
     return np.ascontiguousarray(arr).view(L.STATUS_DTYPE).reshape(-1)
+
+
+def admm_design(pts, adj, params=None, stream=None):
+    """Batched ADMM formation-gain design (acl_admm_solve_batch; the
+    reference's admm::Solver::solve / ADMM::calculateFormationGains,
+    aclswarm/lib/admm/src/solver.cpp:28-79, aclswarm/src/admm.cpp:32-51).
+
+    pts [F][n][3] f64 and adj [F][n][n] f64 (0/1, symmetric) on the device.
+    Returns (gains [F][3n][3n] f64 with gains[f][r][c] = GainMat(r, c),
+    iters [F][2] int32: ADMM iterations of the xy and z designs, negative if
+    that part's sign iteration did not converge).
+    """
+    lib = L.lib()
+    F, n = int(pts.shape[0]), int(pts.shape[1])
+    dev = pts.device
+    pts = pts.contiguous()          # [n][3] row-major == Eigen 3 x n column-major
+    adj = adj.contiguous()          # symmetric: either layout
+    out = torch.empty((F, 3 * n, 3 * n), dtype=torch.float64, device=dev)
+    iters = torch.empty((F, 2), dtype=torch.int32, device=dev)
+    prm = params or L.default_admm_params()
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    L.check(lib.acl_admm_solve_batch(F, n, pts.data_ptr(), adj.data_ptr(), out.data_ptr(),
+                                     iters.data_ptr(), ct.byref(prm), ct.c_void_p(stream)),
+            "acl_admm_solve_batch")
+    return out.transpose(1, 2), iters
