@@ -12,48 +12,38 @@ constexpr double kPi = 3.14159265358979323846;
 // quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, 8 give every lane its row's
 // result; row_bcast15 / row_bcast31 fold rows 0-3 into lane 63.
 // Callers must have all 64 lanes active.
-#define ACL_DPP_STEP(x, op, ctrl, rmask)                                                   \
-  x = op(x, __builtin_amdgcn_update_dpp(x, x, ctrl, rmask, 0xF, false))
-
-__device__ __forceinline__ unsigned umax32(unsigned a, int b) { return a > (unsigned)b ? a : (unsigned)b; }
-
-__device__ __forceinline__ unsigned wave_max_u32(unsigned ux) {
-  int x = (int)ux;
-#define ACL_UMAX(a, b) (int)umax32((unsigned)(a), (b))
-  ACL_DPP_STEP(x, ACL_UMAX, 0xB1, 0xF);
-  ACL_DPP_STEP(x, ACL_UMAX, 0x4E, 0xF);
-  ACL_DPP_STEP(x, ACL_UMAX, 0x124, 0xF);
-  ACL_DPP_STEP(x, ACL_UMAX, 0x128, 0xF);
-  ACL_DPP_STEP(x, ACL_UMAX, 0x142, 0xA);
-  ACL_DPP_STEP(x, ACL_UMAX, 0x143, 0xC);
-#undef ACL_UMAX
-  return (unsigned)__builtin_amdgcn_readlane(x, 63);
+// DPP lane move with the reduction identity 0 in lanes the pattern leaves
+// out (bound_ctrl): `op(x, dppz<..>(x))` folds into one `v_op_dpp`.
+template <int CTRL, int RMASK>
+__device__ __forceinline__ unsigned dppz(unsigned x) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, RMASK, 0xF, true);
 }
 
-__device__ __forceinline__ unsigned wave_or_u32(unsigned ux) {
-  int x = (int)ux;
-#define ACL_UOR(a, b) ((a) | (b))
-  ACL_DPP_STEP(x, ACL_UOR, 0xB1, 0xF);
-  ACL_DPP_STEP(x, ACL_UOR, 0x4E, 0xF);
-  ACL_DPP_STEP(x, ACL_UOR, 0x124, 0xF);
-  ACL_DPP_STEP(x, ACL_UOR, 0x128, 0xF);
-  ACL_DPP_STEP(x, ACL_UOR, 0x142, 0xA);
-  ACL_DPP_STEP(x, ACL_UOR, 0x143, 0xC);
-#undef ACL_UOR
-  return (unsigned)__builtin_amdgcn_readlane(x, 63);
+// Result of a 6-step wave reduction sits in lane 63.
+#define ACL_WAVE_REDUCE(x, OP)          \
+  x = OP(x, dppz<0xB1, 0xF>(x));        \
+  x = OP(x, dppz<0x4E, 0xF>(x));        \
+  x = OP(x, dppz<0x124, 0xF>(x));       \
+  x = OP(x, dppz<0x128, 0xF>(x));       \
+  x = OP(x, dppz<0x142, 0xA>(x));       \
+  x = OP(x, dppz<0x143, 0xC>(x))
+
+__device__ __forceinline__ unsigned op_umax(unsigned a, unsigned b) { return a > b ? a : b; }
+__device__ __forceinline__ unsigned op_or(unsigned a, unsigned b) { return a | b; }
+
+__device__ __forceinline__ unsigned wave_max_u32(unsigned x) {
+  ACL_WAVE_REDUCE(x, op_umax);
+  return (unsigned)__builtin_amdgcn_readlane((int)x, 63);
 }
 
-__device__ __forceinline__ float wave_max_f32(float fx) {
-  int x = __float_as_int(fx);
-#define ACL_FMAX(a, b) __float_as_int(fmaxf(__int_as_float(a), __int_as_float(b)))
-  ACL_DPP_STEP(x, ACL_FMAX, 0xB1, 0xF);
-  ACL_DPP_STEP(x, ACL_FMAX, 0x4E, 0xF);
-  ACL_DPP_STEP(x, ACL_FMAX, 0x124, 0xF);
-  ACL_DPP_STEP(x, ACL_FMAX, 0x128, 0xF);
-  ACL_DPP_STEP(x, ACL_FMAX, 0x142, 0xA);
-  ACL_DPP_STEP(x, ACL_FMAX, 0x143, 0xC);
-#undef ACL_FMAX
-  return __int_as_float(__builtin_amdgcn_readlane(x, 63));
+__device__ __forceinline__ unsigned wave_or_u32(unsigned x) {
+  ACL_WAVE_REDUCE(x, op_or);
+  return (unsigned)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// non-negative floats order like their bit patterns
+__device__ __forceinline__ float wave_max_f32_nonneg(float fx) {
+  return __uint_as_float(wave_max_u32(__float_as_uint(fx)));
 }
 
 __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x) {
@@ -85,6 +75,31 @@ __device__ __forceinline__ double wave_sum(double x) {
   const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)u, 63);
   const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(u >> 32), 63);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// atan in fp64, branch-free (selects): the classic fdlibm reduction to
+// |t| < 7/16 around atan(0.5), atan(1), atan(1.5), atan(inf) and its odd
+// degree-23 polynomial; max error 1 ulp (checked against libm on 3e5 points).
+// Leaner in registers than the library call, which matters in the gain
+// kernel's occupancy.
+__device__ __forceinline__ double acl_atan(double x) {
+  const double ax = fabs(x);
+  const bool r0 = ax >= 0.4375, r1 = ax >= 0.6875, r2 = ax >= 1.1875, r3 = ax >= 2.4375;
+  double num = ax, den = 1.0, hi = 0.0, lo = 0.0;
+  if (r0) { num = 2.0 * ax - 1.0; den = 2.0 + ax; hi = 4.63647609000806093515e-01; lo = 2.26987774529616870924e-17; }
+  if (r1) { num = ax - 1.0; den = ax + 1.0; hi = 7.85398163397448278999e-01; lo = 3.06161699786838301793e-17; }
+  if (r2) { num = ax - 1.5; den = 1.0 + 1.5 * ax; hi = 9.82793723247329054082e-01; lo = 1.39033110312309984516e-17; }
+  if (r3) { num = -1.0; den = ax; hi = 1.57079632679489655800e+00; lo = 6.12323399573676603587e-17; }
+  const double t = num / den;
+  const double z = t * t, w = z * z;
+  const double s1 = z * (3.33333333333329318027e-01 + w * (1.42857142725034663711e-01 +
+                    w * (9.09088713343650656196e-02 + w * (6.66107313738753120669e-02 +
+                    w * (4.97687799461593236017e-02 + w * 1.62858201153657823623e-02)))));
+  const double s2 = w * (-1.99999999998764832476e-01 + w * (-1.11111104054623557880e-01 +
+                    w * (-7.69187620504482999495e-02 + w * (-5.83357013379057348645e-02 +
+                    w * -3.65315727442169155270e-02))));
+  const double r = r0 ? hi - ((t * (s1 + s2) - lo) - t) : t - t * (s1 + s2);
+  return copysign(r, x);
 }
 
 __device__ __forceinline__ double wrap_to_pi(double a) {  // utils.h:275-280

@@ -1,21 +1,24 @@
 // control.hip -- batched DistCntrl::compute + Safety for gfx950.
 //
-// Runs after the auction kernel (solve.hip) on the same swarms, usually on a
-// second stream so that it streams one chunk's gain blocks from HBM while
-// the auction kernel works on the next chunk out of LDS.
+// Runs after the auction kernel (solve.hip) on the same swarms, on a second
+// stream so that one chunk's gain stream overlaps the next chunk's auction.
+// Two kernels:
 //
-// One workgroup (4 wave64) per swarm, small LDS footprint so that many
-// swarms are resident per CU and the 9-plane gain stream keeps enough bytes
-// in flight. One wave per vehicle v:
-//   DistCntrl::compute (aclswarm/src/distcntrl.cpp:46-102): lanes = formation
-//   neighbours j of v's adopted point i (two chunks of 64), 3x3 block A_ij
-//   loaded from the 9 coalesced planes, pdistmat's Gram-formula distances
-//   (utils.h:137-147), atan scale terms gated on |e| > thr, per-neighbour
-//   damping; the wave sum gives u (tree order: parity within 1e-5 relative).
-//   Safety::cmdinCb saturation (safety.cpp:185-196) and
-//   Safety::collisionAvoidance (safety.cpp:412-541): lanes find the vehicles
-//   inside d_avoid_thresh, lane 0 sorts the sector edges, unions them and
-//   picks the closest safe edge exactly as the reference.
+//   gain_kernel    DistCntrl::compute (aclswarm/src/distcntrl.cpp:46-102):
+//                  the HBM stream (72 B of gain block per directed edge).
+//                  One wave per vehicle v, lanes = formation neighbours j of
+//                  v's adopted point i (two chunks of 64), the 3x3 block A_ij
+//                  read from the 9 coalesced planes, pdistmat's Gram-formula
+//                  distances (utils.h:137-147), atan scale terms gated on
+//                  |e| > thr, per-neighbour damping; a wave sum gives u (tree
+//                  order: parity within 1e-5 relative). Lean on registers and
+//                  LDS (~7 KB per swarm) so 8 swarms are resident per CU and
+//                  enough gain bytes are in flight.
+//   safety_kernel  Safety::cmdinCb saturation (safety.cpp:185-196) and
+//                  Safety::collisionAvoidance (safety.cpp:412-541): lanes find
+//                  the vehicles inside d_avoid_thresh, lane 0 sorts the sector
+//                  edges, unions them and picks the closest safe edge exactly
+//                  as the reference.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,14 +31,14 @@ namespace acl_amd {
 constexpr int kCtlBlock = 256;
 constexpr int kCtlWaves = kCtlBlock / 64;
 
-struct CtlLayout {
-  int q, p, adjF, rowptr, Pt, myi, out, caA, caS, misc, total;
-};
-
 __host__ __device__ inline int cal16(int x) { return (x + 15) & ~15; }
 
-__host__ __device__ inline CtlLayout make_ctl_layout(int n) {
-  CtlLayout L;
+struct GainLayout {
+  int q, p, adjF, rowptr, Pt, myi, out, total;
+};
+
+__host__ __device__ inline GainLayout make_gain_layout(int n) {
+  GainLayout L;
   int o = 0;
   L.q = o;      o = cal16(o + n * 3 * 8);
   L.p = o;      o = cal16(o + n * 3 * 8);
@@ -43,18 +46,15 @@ __host__ __device__ inline CtlLayout make_ctl_layout(int n) {
   L.rowptr = o; o = cal16(o + (n + 1) * 4);
   L.Pt = o;     o = cal16(o + n);
   L.myi = o;    o = cal16(o + n);
-  L.out = o;    o = cal16(o + n * 6 * 8);
-  L.caA = o;    o = cal16(o + kCtlWaves * 4 * n * 8);
-  L.caS = o;    o = cal16(o + kCtlWaves * 4 * n);
-  L.misc = o;   o = cal16(o + 16);
+  L.out = o;    o = cal16(o + n * 3 * 8);
   L.total = o;
   return L;
 }
 
-__global__ void __launch_bounds__(kCtlBlock, 2) control_kernel(const CtlParams P) {
+__global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
-  const CtlLayout L = make_ctl_layout(n);
+  const GainLayout L = make_gain_layout(n);
   const int b = P.b0 + blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -68,8 +68,6 @@ __global__ void __launch_bounds__(kCtlBlock, 2) control_kernel(const CtlParams P
   unsigned char* Pt = smem + L.Pt;
   unsigned char* myi = smem + L.myi;
   double* uo = reinterpret_cast<double*>(smem + L.out);
-  double* uso = uo + 3 * n;
-  int* misc = reinterpret_cast<int*>(smem + L.misc);
 
   const int f = P.fidx[b];
   const int gw = (n + 63) >> 6;
@@ -97,7 +95,6 @@ __global__ void __launch_bounds__(kCtlBlock, 2) control_kernel(const CtlParams P
       myi[v] = (unsigned char)P.P_out[(size_t)b * n + v];
       if (uniform) Pt[v] = P.ws[(size_t)b * n + v];
     }
-    if (tid == 0) misc[0] = 0;
   }
   __syncthreads();
   // formation CSR row starts (edges enumerated row-major, diagonal included)
@@ -106,8 +103,7 @@ __global__ void __launch_bounds__(kCtlBlock, 2) control_kernel(const CtlParams P
     for (int c = 0; c < 2; ++c) {
       const int i = lane + 64 * c;
       const int cnt = (i < n) ? __popcll(adjF[2 * i]) + __popcll(adjF[2 * i + 1]) : 0;
-      // inclusive wave scan of cnt
-      int x = cnt;
+      int x = cnt;  // inclusive wave scan
       for (int o = 1; o < 64; o <<= 1) {
         const int y = __shfl_up(x, o, 64);
         if (lane >= o) x += y;
@@ -122,10 +118,6 @@ __global__ void __launch_bounds__(kCtlBlock, 2) control_kernel(const CtlParams P
   const int E = rowptr[n];
   const double* G = P.gains + 9 * P.gain_off[f];
   const acl_cntrl_gains_t g = P.g;
-  const acl_safety_params_t sp = P.s;
-  double* caA = reinterpret_cast<double*>(smem + L.caA) + wave * (4 * n);
-  signed char* caS = reinterpret_cast<signed char*>(smem + L.caS) + wave * (4 * n);
-  int nca = 0;
   for (int v = wave; v < n; v += kCtlWaves) {
     const int i = myi[v];
     const double* gv = P.vel + ((size_t)b * n + v) * 3;
@@ -135,24 +127,17 @@ __global__ void __launch_bounds__(kCtlBlock, 2) control_kernel(const CtlParams P
     const double Ni = pix * pix + piy * piy, Nzi = piz * piz;
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
     int ebase = rowptr[i];
-    // 3x3 blocks of row i: lane = column j, coalesced in each of the 9 planes;
-    // both chunks' loads are issued before any use
-    double A[2][9];
-    bool has[2];
-#pragma unroll
+#pragma unroll 1
     for (int c = 0; c < 2; ++c) {
       const unsigned long long rowbits = adjF[2 * i + c];
-      has[c] = (rowbits >> lane) & 1ull;
+      const bool has = (rowbits >> lane) & 1ull;
       const int e = ebase + __popcll(rowbits & ((1ull << lane) - 1ull));
       ebase += __popcll(rowbits);
+      if (has) {
+        double A[9];
 #pragma unroll
-      for (int k = 0; k < 9; ++k)
-        A[c][k] = has[c] ? __builtin_nontemporal_load(G + (size_t)k * E + e) : 0.0;
-    }
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int j = lane + 64 * c;
-      if (has[c]) {
+        for (int k = 0; k < 9; ++k) A[k] = __builtin_nontemporal_load(G + (size_t)k * E + e);
+        const int j = lane + 64 * c;
         const int uu = uniform ? Pt[j] : rows[(size_t)v * n + j];
         const double q0 = q[3 * uu] - qv0, q1 = q[3 * uu + 1] - qv1, q2 = q[3 * uu + 2] - qv2;
         const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
@@ -162,21 +147,71 @@ __global__ void __launch_bounds__(kCtlBlock, 2) control_kernel(const CtlParams P
         const double e_xy = sqrt(q0 * q0 + q1 * q1) - dxy;
         const double e_z = sqrt(q2 * q2) - dz;
         double Fxy = 0.0, Fz = 0.0;
-        if (fabs(e_xy) > g.e_xy_thr) Fxy = g.K1_xy * atan(g.K2_xy * e_xy);
-        if (fabs(e_z) > g.e_z_thr) Fz = g.K1_z * atan(g.K2_z * e_z);
-        const double* Ac = A[c];
-        const double up0 = ((Ac[0] * q0 + Ac[1] * q1) + Ac[2] * q2) + Fxy * q0;
-        const double up1 = ((Ac[3] * q0 + Ac[4] * q1) + Ac[5] * q2) + Fxy * q1;
-        const double up2 = ((Ac[6] * q0 + Ac[7] * q1) + Ac[8] * q2) + Fz * q2;
+        if (fabs(e_xy) > g.e_xy_thr) Fxy = g.K1_xy * acl_atan(g.K2_xy * e_xy);
+        if (fabs(e_z) > g.e_z_thr) Fz = g.K1_z * acl_atan(g.K2_z * e_z);
+        const double up0 = ((A[0] * q0 + A[1] * q1) + A[2] * q2) + Fxy * q0;
+        const double up1 = ((A[3] * q0 + A[4] * q1) + A[5] * q2) + Fxy * q1;
+        const double up2 = ((A[6] * q0 + A[7] * q1) + A[8] * q2) + Fz * q2;
         acc0 += g.kp * up0 + g.kd * (-vel0);
         acc1 += g.kp * up1 + g.kd * (-vel1);
         acc2 += g.kp * up2 + g.kd * (-vel2);
       }
     }
-    double cmd0 = wave_sum(acc0), cmd1 = wave_sum(acc1), cmd2 = wave_sum(acc2);
+    const double cmd0 = wave_sum(acc0), cmd1 = wave_sum(acc1), cmd2 = wave_sum(acc2);
     if (lane == 0) {
       uo[3 * v] = cmd0; uo[3 * v + 1] = cmd1; uo[3 * v + 2] = cmd2;
     }
+  }
+  __syncthreads();
+  for (int k = tid; k < 3 * n; k += kCtlBlock) P.u[(size_t)b * n * 3 + k] = uo[k];
+}
+
+struct SafeLayout {
+  int q, u, caA, caS, misc, total;
+};
+
+__host__ __device__ inline SafeLayout make_safe_layout(int n) {
+  SafeLayout L;
+  int o = 0;
+  L.q = o;    o = cal16(o + n * 3 * 8);
+  L.u = o;    o = cal16(o + n * 3 * 8);
+  L.caA = o;  o = cal16(o + kCtlWaves * 4 * n * 8);
+  L.caS = o;  o = cal16(o + kCtlWaves * 4 * n);
+  L.misc = o; o = cal16(o + 16);
+  L.total = o;
+  return L;
+}
+
+__global__ void __launch_bounds__(kCtlBlock) safety_kernel(const CtlParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = P.n;
+  const SafeLayout L = make_safe_layout(n);
+  const int b = P.b0 + blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  if (P.status[b].flags & ACL_SWARM_BAD_INPUT) return;
+
+  double* q = reinterpret_cast<double*>(smem + L.q);
+  double* uo = reinterpret_cast<double*>(smem + L.u);
+  int* misc = reinterpret_cast<int*>(smem + L.misc);
+  {
+    const double* gq = P.q + (size_t)b * n * 3;
+    const double* gu = P.u + (size_t)b * n * 3;
+    for (int k = tid; k < 3 * n; k += kCtlBlock) {
+      q[k] = gq[k];
+      uo[k] = gu[k];
+    }
+    if (tid == 0) misc[0] = 0;
+  }
+  __syncthreads();
+  const acl_safety_params_t sp = P.s;
+  double* caA = reinterpret_cast<double*>(smem + L.caA) + wave * (4 * n);
+  signed char* caS = reinterpret_cast<signed char*>(smem + L.caS) + wave * (4 * n);
+  int nca = 0;
+  for (int v = wave; v < n; v += kCtlWaves) {
+    double cmd0 = uo[3 * v], cmd1 = uo[3 * v + 1], cmd2 = uo[3 * v + 2];
+    const double qv0 = q[3 * v], qv1 = q[3 * v + 1];
     // Safety::cmdinCb saturation (safety.cpp:185-196)
     {
       const double velxy = sqrt(cmd0 * cmd0 + cmd1 * cmd1);
@@ -308,33 +343,29 @@ __global__ void __launch_bounds__(kCtlBlock, 2) control_kernel(const CtlParams P
       }
     }
     if (lane == 0) {
-      uso[3 * v] = cmd0; uso[3 * v + 1] = cmd1; uso[3 * v + 2] = cmd2;
+      uo[3 * v] = cmd0; uo[3 * v + 1] = cmd1; uo[3 * v + 2] = cmd2;
       if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = modified;
       nca += modified;
     }
   }
   if (lane == 0 && nca) atomicAdd(&misc[0], nca);
   __syncthreads();
-  for (int k = tid; k < 3 * n; k += kCtlBlock) {
-    if (P.u) P.u[(size_t)b * n * 3 + k] = uo[k];
-    if (P.u_safe) P.u_safe[(size_t)b * n * 3 + k] = uso[k];
-  }
+  if (P.u_safe)
+    for (int k = tid; k < 3 * n; k += kCtlBlock) P.u_safe[(size_t)b * n * 3 + k] = uo[k];
   if (tid == 0 && misc[0]) {
     P.status[b].n_ca = (uint16_t)misc[0];
     P.status[b].flags |= ACL_SWARM_CA_ACTIVE;
   }
 }
 
-// Launches control_kernel for swarms [P.b0, P.b0 + nb) of the batch.
-hipError_t launch_control(const CtlParams& P, int nb, hipStream_t stream) {
-  static bool configured = false;
-  if (!configured) {
-    (void)hipFuncSetAttribute((const void*)control_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    configured = true;
+hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream) {
+  if (which == 0) {
+    const GainLayout L = make_gain_layout(P.n);
+    hipLaunchKernelGGL(gain_kernel, dim3(nb), dim3(kCtlBlock), L.total, stream, P);
+  } else {
+    const SafeLayout L = make_safe_layout(P.n);
+    hipLaunchKernelGGL(safety_kernel, dim3(nb), dim3(kCtlBlock), L.total, stream, P);
   }
-  const CtlLayout L = make_ctl_layout(P.n);
-  hipLaunchKernelGGL(control_kernel, dim3(nb), dim3(kCtlBlock), L.total, stream, P);
   return hipGetLastError();
 }
 

@@ -34,6 +34,7 @@
 // CPU restatement (oracle/).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "../../include/aclswarm_amd.h"
 #include "common.h"
@@ -41,44 +42,49 @@
 
 namespace acl_amd {
 
-constexpr int kBlock = 512;  // 8 waves per swarm, 2 swarms per CU
+constexpr int kBlock = 512;  // 8 waves per swarm
 constexpr int kWaves = kBlock / 64;
-constexpr int kMaxN = 128;  // two 64-bit words per bitmask row, u8 indices
+constexpr int kMinWavesPerEU = 6;  // 3 swarms x 8 waves per CU (LDS <= 160 KiB / 3)
+constexpr int kMaxN = 128;     // two 64-bit words per bitmask row, u8 indices
 
+// LDS layout (byte offsets, 16-byte aligned). The CBAA table T (n x n u8,
+// who per vehicle row) is written after the prices are known and overlays
+// the arrays only phases 0-2 read (formation-ordered q, p, the alignments,
+// the formation adjacency), so one swarm needs ~53 KB at n = 100 and three
+// swarms fit a CU.
 struct Layout {
-  // byte offsets into the dynamic LDS block (all 16-byte aligned)
-  int q, p, qf, out, adjF, vadj, H, C, T0, T1, Pin, Ptin, cao, myi, valid, rowptr, misc;
+  int C;                                  // n x n f32 prices; alignment-sum scratch first
+  int A, qf, p, out, adjF;                // region A (phases 0-2) ...
+  int T;                                  // ... reused by the CBAA table (phase 3-4)
+  int vadj, Pin, Ptin, myi, valid, H, misc;
   int total;
 };
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
-constexpr int kLevels = 3;  // price levels tracked per dirty column
+constexpr int kLevels = 3;  // price levels resolved per dirty column before the exact scan
 
 __host__ __device__ inline Layout make_layout(int n) {
   Layout L;
   int o = 0;
-  L.q = o;      o = align16(o + n * 3 * 8);
-  L.p = o;      o = align16(o + n * 3 * 8);
-  L.qf = o;     o = align16(o + n * 2 * 8);   // q_xy in formation space
-  L.out = o;    o = align16(o + n * 6 * 8);   // R,t per vehicle; later u, u_safe
-  L.adjF = o;   o = align16(o + n * 2 * 8);
-  L.vadj = o;   o = align16(o + n * 2 * 8);
-  L.H = o;      o = align16(o + 96);          // CBAA masks + per-column buffer bits
   L.C = o;
   {
-    const int csz = (n + 1) * n * 4;
-    const int sc = 64 * n;                     // alignment-sum scratch
+    const int csz = n * n * 4, sc = 64 * n;  // prices / alignment sums [n][8] f64
     o = align16(o + (csz > sc ? csz : sc));
   }
-  L.T0 = o;     o = align16(o + n * n);
-  L.T1 = o;     o = align16(o + n * n);
+  L.A = o;
+  L.qf = o;     o = align16(o + n * 3 * 8);   // q in formation order: qf[j] = q[Pt[j]]
+  L.p = o;      o = align16(o + n * 3 * 8);
+  L.out = o;    o = align16(o + n * 6 * 8);   // R, t per vehicle
+  L.adjF = o;   o = align16(o + n * 2 * 8);
+  L.T = L.A;
+  if (L.A + n * n > o) o = align16(L.A + n * n);
+  L.vadj = o;   o = align16(o + n * 2 * 8);
   L.Pin = o;    o = align16(o + n);
   L.Ptin = o;   o = align16(o + n);
-  L.cao = o;    o = align16(o + n);
   L.myi = o;    o = align16(o + n);
   L.valid = o;  o = align16(o + n);
-  L.rowptr = o; o = align16(o + (n + 1) * 4);
+  L.H = o;      o = align16(o + 96);
   L.misc = o;   o = align16(o + 64);
   L.total = o;
   return L;
@@ -109,36 +115,43 @@ struct SolveParams {
 };
 
 // misc int slots
-enum { M_BAD = 0, M_NONFIN = 1, M_CHG0 = 2, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 8 };
+enum { M_BAD = 0, M_NONFIN = 1, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 8 };
 
 __device__ __forceinline__ void stamp(const SolveParams& P, int b, int tid, int k) {
   if (P.stamps && tid == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
 }
 
+// Price of a table entry: C[who][j], 0 for `none` (who == n; reset,
+// auctioneer.cpp:448-465, price 0).
+__device__ __forceinline__ float entry_price(const float* C, int n, int w, int j) {
+  const float c = C[(w < n ? w : 0) * n + j];
+  return w < n ? c : 0.0f;
+}
+
 // selectTaskAssignment (auctioneer.cpp:517-542) for vehicle v as a wave
 // argmax: the first task j maximizing C[v][j] among tasks with
-// C[v][j] > price_j (price_j = C[who_j][j]); nw[c] is this lane's entry for
-// task lane+64c. Returns the selected task (wave-uniform) or -1.
+// C[v][j] > 0 and C[v][j] > price_j (price_j = C[who_j][j]); nw[c] is this
+// lane's entry for task lane+64c. Returns the selected task (wave-uniform) or -1.
 __device__ __forceinline__ int wave_select(int n, int v, int lane, const float* C,
                                            const int (&nw)[2]) {
-  unsigned long long key = 0;
+  unsigned key[2];
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const int j = lane + 64 * c;
+    key[c] = 0u;
     if (j < n) {
       const float cv = C[v * n + j];
-      const float pr = C[nw[c] * n + j];
-      if (cv > 0.0f && cv > pr)
-        key = max(key, ((unsigned long long)__float_as_uint(cv) << 32) |
-                           (unsigned long long)(0xFFFFFFFFu - (unsigned)j));
+      const float pr = entry_price(C, n, nw[c], j);
+      if (cv > 0.0f && cv > pr) key[c] = __float_as_uint(cv);
     }
   }
-  key = wave_max_u64(key);
-  if (key == 0) return -1;
-  return (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+  const unsigned M = wave_max_u32(key[0] > key[1] ? key[0] : key[1]);
+  if (M == 0u) return -1;
+  const unsigned long long e0 = __ballot(key[0] == M), e1 = __ballot(key[1] == M);
+  return e0 ? __ffsll((long long)e0) - 1 : 64 + __ffsll((long long)e1) - 1;
 }
 
-__global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
+__global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const SolveParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const Layout L = make_layout(n);
@@ -147,27 +160,21 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
 
-  double* q = reinterpret_cast<double*>(smem + L.q);
-  double* p = reinterpret_cast<double*>(smem + L.p);
+  float* C = reinterpret_cast<float*>(smem + L.C);
   double* qf = reinterpret_cast<double*>(smem + L.qf);
+  double* p = reinterpret_cast<double*>(smem + L.p);
   double* out = reinterpret_cast<double*>(smem + L.out);
   unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
   unsigned long long* vadj = reinterpret_cast<unsigned long long*>(smem + L.vadj);
   unsigned long long* H = reinterpret_cast<unsigned long long*>(smem + L.H);
-  float* C = reinterpret_cast<float*>(smem + L.C);
-  // the two table buffers; indexed by offset so every access stays an LDS
-  // (addrspace 3) access -- a runtime-selected pointer would become flat
-  unsigned char* const T0 = smem + L.T0;
-  const int Tstr = L.T1 - L.T0;
+  unsigned char* const T = smem + L.T;
   unsigned char* Pin = smem + L.Pin;
   unsigned char* Ptin = smem + L.Ptin;
   unsigned char* myi = smem + L.myi;
   unsigned char* validv = smem + L.valid;
-  int* rowptr = reinterpret_cast<int*>(smem + L.rowptr);
   int* misc = reinterpret_cast<int*>(smem + L.misc);
 
   const int f = P.fidx[b];
-  const int W = 2;
   const int gw = (n + 63) >> 6;  // words per row in the global table
   const unsigned long long lastmask =
       (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
@@ -175,14 +182,10 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
 
   // ---------------- phase 0: load -----------------------------------------
   {
-    const double* gq = P.q + (size_t)b * n * 3;
     const double* gp = P.p + (size_t)f * n * 3;
-    for (int k = tid; k < 3 * n; k += kBlock) {
-      q[k] = gq[k];
-      p[k] = gp[k];
-    }
+    for (int k = tid; k < 3 * n; k += kBlock) p[k] = gp[k];
     const uint64_t* ga = P.adj + (size_t)f * n * gw;
-    for (int k = tid; k < n * W; k += kBlock) {
+    for (int k = tid; k < n * 2; k += kBlock) {
       const int i = k >> 1, w = k & 1;
       unsigned long long x = 0;
       if (w < gw) {
@@ -231,11 +234,14 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
     return;
   }
 
-  // q in formation space: qf[j] = q[Pt[j]] (xy only; the alignment is 2-D)
-  for (int j = tid; j < n; j += kBlock) {
-    const int vj = Ptin[j];
-    qf[2 * j] = q[3 * vj];
-    qf[2 * j + 1] = q[3 * vj + 1];
+  // q in formation order: qf[j] = q[Pt[j]] (the alignment reads the
+  // formation-ordered xy, the prices read qf[P[v]] = q[v])
+  {
+    const double* gq = P.q + (size_t)b * n * 3;
+    for (int k = tid; k < 3 * n; k += kBlock) {
+      const int j = k / 3, c = k - 3 * j;
+      qf[k] = gq[3 * Ptin[j] + c];
+    }
   }
   // vehicle-space closed neighbourhoods: u ~ v iff u == v or adj(P[v], P[u])
   // (bidIterComplete, auctioneer.cpp:419-437); one wave per vehicle, lanes
@@ -272,13 +278,12 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
     if (i < 64) r0 |= 1ull << i; else r1 |= 1ull << (i - 64);
     // pass 1: rowwise().sum() of src (p) and dst (q in formation space)
     const double* src = (c < 2) ? (p + c) : (qf + (c - 2));
-    const int stride = (c < 2) ? 3 : 2;
     double acc = 0.0;
     bool first = true;
     for (int j0 = 0; j0 < n; j0 += 4) {
       double val[4];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) val[x] = (j0 + x < n) ? src[(j0 + x) * stride] : 0.0;
+      for (int x = 0; x < 4; ++x) val[x] = (j0 + x < n) ? src[(j0 + x) * 3] : 0.0;
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
         const int j = j0 + x;
@@ -315,7 +320,7 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
       for (int x = 0; x < 4; ++x) {
         const int j = (j0 + x < n) ? j0 + x : 0;
         sv[x] = p[3 * j + sj];
-        dv[x] = qf[2 * j + di];
+        dv[x] = qf[3 * j + di];
       }
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
@@ -357,47 +362,19 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
     for (int k = tid; k < n * n; k += kBlock) {
       const int v = k / n, j = k - v * n;
       const double* o = out + 6 * v;
+      const double* qv = qf + 3 * Pin[v];
       const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
       const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
       const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
       const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
-      const double dx = q[3 * v] - ax, dy = q[3 * v + 1] - ay, dz = q[3 * v + 2] - az;
+      const double dx = qv[0] - ax, dy = qv[1] - ay, dz = qv[2] - az;
       const double nrm = sqrt((dx * dx + dy * dy) + dz * dz);
       const float c = (float)(1.0 / (nrm + 1e-8));
       C[k] = c;
       nonfin |= (c != c);
     }
-    for (int j = tid; j < n; j += kBlock) C[n * n + j] = 0.0f;  // row `none`
-    // initial tables: every entry unassigned (reset, auctioneer.cpp:448-465)
-    for (int k = tid; k < n * n; k += kBlock) T0[k] = (unsigned char)n;
     if (__any(nonfin) && lane == 0) misc[M_NONFIN] = 1;
   }
-  __syncthreads();
-  const bool nonfinite = misc[M_NONFIN] != 0;
-  stamp(P, b, tid, 3);
-
-  // ---------------- phase 3: CBAA ------------------------------------------
-  // CBAA state in the (now free) level region: dirty-column masks by round
-  // parity, outbid-vehicle masks by round parity, per-column buffer index.
-  unsigned long long* dmask = H;      // [2][2]
-  unsigned long long* obm = H + 4;    // [2][2]
-  unsigned long long* cbm = H + 8;    // [2] bit j: column j's current buffer
-  if (tid < 10) H[tid] = 0ull;
-  __syncthreads();
-  // round 0: START bid = select from the zero table (start, auctioneer.cpp:105);
-  // every column that received a bid is dirty for round 1
-  for (int v = wave; v < n; v += kWaves) {
-    int nw[2] = {n, n};
-    const int task = wave_select(n, v, lane, C, nw);
-    if (task >= 0 && lane == 0) {
-      T0[v * n + task] = (unsigned char)v;
-      atomicOr(&dmask[2 * 1 + (task >> 6)], 1ull << (task & 63));
-    }
-  }
-  __syncthreads();
-
-  int eff = 0;
-  const int max_rounds = 2 * n;  // cbaa_max_iter_ = n * diameter (:50-51)
   // closed neighbourhood masks of this lane's vehicles (lane, lane + 64)
   unsigned long long vmy0[2], vmy1[2];
 #pragma unroll
@@ -406,148 +383,123 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
     vmy0[c] = (v < n) ? vadj[2 * v] : 0ull;
     vmy1[c] = (v < n) ? vadj[2 * v + 1] : 0ull;
   }
-  unsigned long long sub[4] = {0, 0, 0, 0};
-  unsigned long long dbg_needcols = 0, dbg_colcyc = 0;
-  unsigned long long tprev = P.stamps ? __builtin_amdgcn_s_memtime() : 0;
-  auto substamp = [&](int k) {
-    if (P.stamps) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      sub[k] += t - tprev;
-      tprev = t;
+  __syncthreads();  // region A (q, p, alignments) is dead from here: T overlays it
+  const bool nonfinite = misc[M_NONFIN] != 0;
+  // initial tables: every entry unassigned (reset, auctioneer.cpp:448-465)
+  for (int k = tid; k < n * n; k += kBlock) T[k] = (unsigned char)n;
+  // CBAA state: dirty-column masks and outbid-vehicle masks by round parity
+  unsigned long long* dmask = H;      // [2][2]
+  unsigned long long* obm = H + 4;    // [2][2]
+  if (tid < 8) H[tid] = 0ull;
+  __syncthreads();
+  stamp(P, b, tid, 3);
+
+  // ---------------- phase 3: CBAA ------------------------------------------
+  // round 0: START bid = select from the zero table (start, auctioneer.cpp:105);
+  // every column that received a bid is dirty for round 1
+  for (int v = wave; v < n; v += kWaves) {
+    int nw[2] = {n, n};
+    const int task = wave_select(n, v, lane, C, nw);
+    if (task >= 0 && lane == 0) {
+      T[v * n + task] = (unsigned char)v;
+      atomicOr(&dmask[2 * 1 + (task >> 6)], 1ull << (task & 63));
     }
-  };
+  }
+  __syncthreads();
+
+  int eff = 0;
+  const int max_rounds = 2 * n;  // cbaa_max_iter_ = n * diameter (:50-51)
+  const bool ok0 = lane < n, ok1 = lane + 64 < n;
   for (int r = 1; r <= max_rounds; ++r) {
     const int par = r & 1, npar = par ^ 1;
     const unsigned long long D0 = dmask[2 * par], D1 = dmask[2 * par + 1];
-    if (P.stamps) sub[2] += __popcll(D0) + __popcll(D1);
-    unsigned long long t_col = 0;
-    // A+B) One wave per dirty column j. A column none of whose entries changed
-    // last round is a fixed point of updateTaskAssignment (it reads only
-    // that column, and a select always changes the entry it writes), so only
-    // dirty columns are recomputed. Lanes = vehicles (two chunks of 64).
-    {
-      const unsigned long long CB0 = cbm[0], CB1 = cbm[1];  // buffer of each column
-      int idx = 0;
-      for (int w = 0; w < 2; ++w) {
-        unsigned long long m = w ? D1 : D0;
-        while (m) {
-          const int j = 64 * w + __ffsll((long long)m) - 1;
-          m &= m - 1;
-          if ((idx++ & (kWaves - 1)) != wave) continue;
-          if (P.stamps) t_col = __builtin_amdgcn_s_memtime();
-          const int cb = (int)(((w ? CB1 : CB0) >> (j & 63)) & 1ull);
-          const unsigned char* Tc = T0 + cb * Tstr;
-          unsigned char* Tn = T0 + (cb ^ 1) * Tstr;
-          int wu[2];
-          unsigned key[2];  // price bits + 1 (prices are >= 0); 0 = no vehicle
-          unsigned long long vm0[2], vm1[2];
+    // One wave per dirty column j, lanes = vehicles (two chunks of 64). A
+    // column none of whose entries changed last round is a fixed point of
+    // updateTaskAssignment (it reads only that column, and a select always
+    // changes the entry it writes), so only dirty columns are recomputed.
+    // Each column is read whole into registers before it is rewritten in
+    // place; no other wave touches it this round.
+    int idx = 0;
+    for (int w = 0; w < 2; ++w) {
+      unsigned long long m = w ? D1 : D0;
+      while (m) {
+        const int j = 64 * w + __ffsll((long long)m) - 1;
+        m &= m - 1;
+        if ((idx++ & (kWaves - 1)) != wave) continue;
+        const int wu0 = ok0 ? T[lane * n + j] : n;
+        const int wu1 = ok1 ? T[(lane + 64) * n + j] : n;
+        // key = price bits + 1 (prices are >= 0); 0 = no vehicle in this lane
+        const unsigned key0 = ok0 ? __float_as_uint(entry_price(C, n, wu0, j)) + 1u : 0u;
+        const unsigned key1 = ok1 ? __float_as_uint(entry_price(C, n, wu1, j)) + 1u : 0u;
+        // A) price levels of the column, highest first, computed lazily:
+        //    level k = (max key below level k-1, holder mask, `who`, tie).
+        // B) vehicle v takes the `who` of the highest level one of its
+        //    closed neighbours holds, unless that level is tied; vehicles
+        //    no tracked level decides fall back to the exact ordered scan
+        //    (ascending vehid, strict >).
+        int nw0 = n, nw1 = n;
+        bool dec0 = !ok0, dec1 = !ok1, need0 = false, need1 = false;
+        unsigned cap = 0xFFFFFFFFu;
+#pragma unroll
+        for (int k = 0; k < kLevels; ++k) {
+          const unsigned Mk = wave_max_u32(max(key0 < cap ? key0 : 0u, key1 < cap ? key1 : 0u));
+          if (Mk == 0u) break;  // no further level
+          const bool e0 = key0 == Mk, e1 = key1 == Mk;
+          const unsigned long long h0 = __ballot(e0), h1 = __ballot(e1);
+          const int wk = h0 ? __builtin_amdgcn_readlane(wu0, __ffsll((long long)h0) - 1)
+                            : __builtin_amdgcn_readlane(wu1, __ffsll((long long)h1) - 1);
+          const bool tk = nonfinite || __ballot((e0 && wu0 != wk) || (e1 && wu1 != wk)) != 0ull;
+          const bool hit0 = !dec0 && ((h0 & vmy0[0]) | (h1 & vmy1[0])) != 0ull;
+          const bool hit1 = !dec1 && ((h0 & vmy0[1]) | (h1 & vmy1[1])) != 0ull;
+          nw0 = hit0 ? wk : nw0;
+          nw1 = hit1 ? wk : nw1;
+          need0 |= hit0 && tk;
+          need1 |= hit1 && tk;
+          dec0 |= hit0;
+          dec1 |= hit1;
+          if (__ballot(!dec0 || !dec1) == 0ull) break;
+          cap = Mk;
+        }
+        need0 |= !dec0;
+        need1 |= !dec1;
+        if (__ballot(need0 || need1) != 0ull) {
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
-            const int u = lane + 64 * c;
-            wu[c] = n;
-            key[c] = 0u;
-            vm0[c] = vm1[c] = 0ull;
-            if (u < n) {
-              wu[c] = Tc[u * n + j];
-              key[c] = __float_as_uint(C[wu[c] * n + j]) + 1u;
-              vm0[c] = vmy0[c];
-              vm1[c] = vmy1[c];
-            }
-          }
-          // A) price levels of the column, highest first, computed lazily:
-          //    level k = (max key below level k-1, holder mask, `who`, tie).
-          // B) vehicle v takes the `who` of the highest level one of its
-          //    closed neighbours holds, unless that level is tied; vehicles
-          //    no tracked level decides fall back to the exact ordered scan
-          //    (ascending vehid, strict >).
-          int nw[2] = {n, n};
-          bool dec[2], need[2];
+            if (c ? need1 : need0) {
+              float bp = 0.0f;
+              int bw = n;
+              bool first = true;
 #pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            dec[c] = (lane + 64 * c) >= n;
-            need[c] = false;
-          }
-          unsigned cap = 0xFFFFFFFFu;
-#pragma unroll
-          for (int k = 0; k < kLevels; ++k) {
-            if (!__any(!dec[0] || !dec[1])) break;
-            const unsigned Mk = wave_max_u32(max(key[0] < cap ? key[0] : 0u,
-                                                 key[1] < cap ? key[1] : 0u));
-            if (Mk == 0u) break;  // no further level
-            const bool e0 = key[0] == Mk, e1 = key[1] == Mk;
-            const unsigned long long h0 = __ballot(e0), h1 = __ballot(e1);
-            const int wk = h0 ? __builtin_amdgcn_readlane(wu[0], __ffsll((long long)h0) - 1)
-                              : __builtin_amdgcn_readlane(wu[1], __ffsll((long long)h1) - 1);
-            const bool tk = nonfinite ||
-                            ((__ballot(e0 && wu[0] != wk) | __ballot(e1 && wu[1] != wk)) != 0ull);
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-              if (!dec[c] && (((h0 & vm0[c]) | (h1 & vm1[c])) != 0ull)) {
-                dec[c] = true;
-                if (tk) need[c] = true;
-                else nw[c] = wk;
-              }
-            }
-            cap = Mk;
-          }
-          bool dbg_need = false;
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            if (!dec[c]) need[c] = true;
-            dbg_need |= need[c];
-          }
-          if (__any(need[0] || need[1])) {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-              if (need[c]) {
-                float bp = 0.0f;
-                int bw = n;
-                bool first = true;
-#pragma unroll
-                for (int w2 = 0; w2 < 2; ++w2) {
-                  unsigned long long mm = w2 ? vm1[c] : vm0[c];
-                  while (mm) {
-                    const int u = 64 * w2 + __ffsll((long long)mm) - 1;
-                    mm &= mm - 1;
-                    const int wx = Tc[u * n + j];
-                    const float px = C[wx * n + j];
-                    if (first) { bp = px; bw = wx; first = false; }
-                    else if (px > bp) { bp = px; bw = wx; }
-                  }
+              for (int w2 = 0; w2 < 2; ++w2) {
+                unsigned long long mm = w2 ? vmy1[c] : vmy0[c];
+                while (mm) {
+                  const int u = 64 * w2 + __ffsll((long long)mm) - 1;
+                  mm &= mm - 1;
+                  const int wx = T[u * n + j];
+                  const float px = entry_price(C, n, wx, j);
+                  if (first) { bp = px; bw = wx; first = false; }
+                  else if (px > bp) { bp = px; bw = wx; }
                 }
-                nw[c] = bw;
               }
+              if (c) nw1 = bw; else nw0 = bw;
             }
           }
-          bool ob[2], ch[2];
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int v = lane + 64 * c;
-            ob[c] = ch[c] = false;
-            if (v < n) {
-              Tn[v * n + j] = (unsigned char)nw[c];
-              ob[c] = (wu[c] == v) && (nw[c] != v);  // outbid (auctioneer.cpp:502)
-              ch[c] = nw[c] != wu[c];
-            }
-          }
-          const unsigned long long ob0 = __ballot(ob[0]), ob1 = __ballot(ob[1]);
-          const bool anych = __any(ch[0] || ch[1]);
-          if (P.stamps) {
-            sub[3] += 1;  // columns seen by this wave (wave 0 -> tid 0's counters)
-            dbg_needcols += __any(dbg_need) ? 1 : 0;
-            dbg_colcyc += __builtin_amdgcn_s_memtime() - t_col;
-          }
-          if (lane == 0) {
-            if (ob0) atomicOr(&obm[2 * par], ob0);
-            if (ob1) atomicOr(&obm[2 * par + 1], ob1);
-            if (anych) atomicOr(&dmask[2 * npar + (j >> 6)], 1ull << (j & 63));
-            atomicXor(&cbm[j >> 6], 1ull << (j & 63));
-          }
+        }
+        // the exact scan above read the column: rewrite it only now
+        __builtin_amdgcn_wave_barrier();
+        if (ok0) T[lane * n + j] = (unsigned char)nw0;
+        if (ok1) T[(lane + 64) * n + j] = (unsigned char)nw1;
+        const unsigned long long ob0 = __ballot(ok0 && wu0 == lane && nw0 != lane);
+        const unsigned long long ob1 = __ballot(ok1 && wu1 == lane + 64 && nw1 != lane + 64);
+        const bool anych = __ballot(nw0 != wu0 || nw1 != wu1) != 0ull;
+        if (lane == 0) {
+          if (ob0) atomicOr(&obm[2 * par], ob0);  // outbid (auctioneer.cpp:502)
+          if (ob1) atomicOr(&obm[2 * par + 1], ob1);
+          if (anych) atomicOr(&dmask[2 * npar + (j >> 6)], 1ull << (j & 63));
         }
       }
     }
     __syncthreads();
-    substamp(0);
     // outbid vehicles re-select on their updated rows (auctioneer.cpp:224)
     {
       if (tid == 0) {
@@ -557,61 +509,37 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
         obm[2 * npar + 1] = 0ull;
       }
       const unsigned long long O0 = obm[2 * par], O1 = obm[2 * par + 1];
-      const unsigned long long SB0 = cbm[0], SB1 = cbm[1];
-
-      int idx = 0;
+      int idx2 = 0;
       for (int w = 0; w < 2; ++w) {
         unsigned long long m = w ? O1 : O0;
         while (m) {
           const int v = 64 * w + __ffsll((long long)m) - 1;
           m &= m - 1;
-          if ((idx++ & (kWaves - 1)) != wave) continue;
+          if ((idx2++ & (kWaves - 1)) != wave) continue;
           int nw[2];
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int jj = lane + 64 * c;
-            const int cbj = (int)(((c ? SB1 : SB0) >> lane) & 1ull);
-            nw[c] = (jj < n) ? T0[cbj * Tstr + v * n + jj] : n;
-          }
+          nw[0] = ok0 ? T[v * n + lane] : n;
+          nw[1] = ok1 ? T[v * n + lane + 64] : n;
           const int task = wave_select(n, v, lane, C, nw);
           if (task >= 0 && lane == 0) {
-            const int cbt = (int)(((task < 64 ? SB0 : SB1) >> (task & 63)) & 1ull);
-            T0[cbt * Tstr + v * n + task] = (unsigned char)v;
+            T[v * n + task] = (unsigned char)v;
             atomicOr(&dmask[2 * npar + (task >> 6)], 1ull << (task & 63));
           }
         }
       }
     }
     __syncthreads();
-    substamp(1);
     const bool changed = (dmask[2 * npar] | dmask[2 * npar + 1]) != 0ull;
     if (changed) eff = r;
     else if (P.early_exit) break;  // fixed point
   }
-  // consolidate the per-column buffers into T[0]
-  {
-    const unsigned long long SB0 = cbm[0], SB1 = cbm[1];
-    for (int k = tid; k < n * n; k += kBlock) {
-      const int jj = k % n;
-      if (((jj < 64 ? SB0 : SB1) >> (jj & 63)) & 1ull) T0[k] = T0[Tstr + k];
-    }
-  }
-  __syncthreads();
   stamp(P, b, tid, 4);
-  if (P.stamps && tid == 0)
-    for (int k = 0; k < 4; ++k) P.stamps[(size_t)b * 16 + 8 + k] = sub[k];
-  if (P.stamps && tid == 0) {
-    P.stamps[(size_t)b * 16 + 12] = dbg_needcols;
-    P.stamps[(size_t)b * 16 + 13] = dbg_colcyc;
-  }
 
   // ---------------- phase 4: adoption --------------------------------------
   // isValidAssignment (auctioneer.cpp:325-343) on each vehicle's table: one
   // wave per vehicle, lanes over tasks; a permutation <=> every entry < n and
   // the OR of the one-hot entries has n bits.
-  const unsigned char* Tf = T0;
   for (int v = wave; v < n; v += kWaves) {
-    const unsigned char* row = Tf + v * n;
+    const unsigned char* row = T + v * n;
     int w[2];
     unsigned lo[4] = {0u, 0u, 0u, 0u};
     bool bad = false, diff = false, ismine[2];
@@ -623,7 +551,7 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
       if (jj < n) {
         if (w[c] >= n) bad = true;
         else lo[w[c] >> 5] |= 1u << (w[c] & 31);
-        diff |= (w[c] != Tf[jj]);
+        diff |= (w[c] != T[jj]);
       }
     }
     int cnt = 0;
@@ -645,7 +573,7 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
   }
   if (P.who) {
     for (int k = tid; k < n * n; k += kBlock) {
-      const int w = Tf[k];
+      const int w = T[k];
       P.who[(size_t)b * n * n + k] = (w >= n) ? (uint16_t)0xFFFF : (uint16_t)w;
     }
   }
@@ -662,12 +590,12 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
     unsigned char* wsPt = P.ws + (size_t)b * n;
     if (tid == 0) P.ws[(size_t)P.B * n + b] = uniform ? 0 : 1;
     if (uniform) {
-      for (int jj = tid; jj < n; jj += kBlock) wsPt[jj] = allvalid ? Tf[jj] : Ptin[jj];
+      for (int jj = tid; jj < n; jj += kBlock) wsPt[jj] = allvalid ? T[jj] : Ptin[jj];
     } else {
       unsigned char* rows = P.ws + (size_t)P.B * (n + 1) + (size_t)b * n * n;
       for (int k = tid; k < n * n; k += kBlock) {
         const int v = k / n, jj = k - v * n;
-        rows[k] = validv[v] ? Tf[k] : Ptin[jj];
+        rows[k] = validv[v] ? T[k] : Ptin[jj];
       }
     }
   }
@@ -688,7 +616,6 @@ __global__ void __launch_bounds__(kBlock, 4) solve_kernel(const SolveParams P) {
     P.status[b] = st;
   }
 }
-
 }  // namespace acl_amd
 
 // ---------------------------------------------------------------------------
@@ -707,7 +634,7 @@ extern "C" void acl_internal_set_stamps(unsigned long long* stamps) { g_stamps =
 
 extern "C" size_t acl_solve_workspace_bytes(int32_t n, int32_t B) {
   if (n < 1 || B < 0) return 0;
-  return (size_t)B * ((size_t)n + 1 + (size_t)n * n);
+  return acl_amd::ws_u_offset(n, B) + (size_t)B * n * 3 * sizeof(double);
 }
 
 namespace {
@@ -726,8 +653,8 @@ Pipe g_pipe[16];
 // control kernel separately while they overlap.
 struct KTiming {
   bool on = false;
-  int n[2] = {0, 0};
-  hipEvent_t ev[2][64][2] = {};
+  int n[3] = {0, 0, 0};
+  hipEvent_t ev[3][64][2] = {};
 };
 KTiming g_kt;
 
@@ -745,13 +672,13 @@ void kt_record(int kind, int which, hipStream_t s) {
 // enable != 0 starts a fresh timing window; 0 stops recording.
 extern "C" void acl_internal_kernel_timing(int enable) {
   g_kt.on = enable != 0;
-  if (enable) g_kt.n[0] = g_kt.n[1] = 0;
+  if (enable) g_kt.n[0] = g_kt.n[1] = g_kt.n[2] = 0;
 }
 
-// Sums the recorded launches: ms[0]/count[0] auction kernel, ms[1]/count[1]
-// control kernel. Synchronises on the recorded events.
+// Sums the recorded launches: ms[k]/count[k] for k = 0 auction kernel,
+// 1 gain kernel, 2 safety kernel. Synchronises on the recorded events.
 extern "C" int acl_internal_kernel_times(double* ms, int* count) {
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < 3; ++k) {
     double t = 0.0;
     for (int i = 0; i < g_kt.n[k]; ++i) {
       float x = 0.f;
@@ -799,6 +726,10 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   int dev = 0;
   (void)hipGetDevice(&dev);
   Pipe& pp = g_pipe[dev & 15];
+  static const bool serial = [] {
+    const char* e = getenv("ACL_SERIAL");
+    return e && e[0] == '1';
+  }();
   if (a->do_control && !pp.ok) {
     if (hipStreamCreateWithFlags(&pp.ctl, hipStreamNonBlocking) != hipSuccess)
       return acl__set_error("hipStreamCreateWithFlags failed");
@@ -830,12 +761,20 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
       C.n = n; C.B = a->B; C.b0 = b0;
       C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
       C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P_out;
-      C.status = a->status; C.u = a->u; C.u_safe = a->u_safe; C.ca_flag = a->ca_flag;
+      C.status = a->status;
+      C.u = a->u ? a->u
+                 : (double*)((unsigned char*)a->workspace + ws_u_offset(n, a->B));
+      C.u_safe = a->u_safe; C.ca_flag = a->ca_flag;
       C.ws = (const unsigned char*)a->workspace; C.g = a->cntrl; C.s = a->safety;
-      kt_record(1, 0, pp.ctl);
-      e = launch_control(C, nb, pp.ctl);
-      kt_record(1, 1, pp.ctl);
-      if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+      for (int which = 0; which < 2; ++which) {
+        // diagnostic: ACL_SERIAL=1 runs every kernel on the caller's stream
+        // (no overlap), so each kernel's time is its own
+        hipStream_t cs = serial ? s : pp.ctl;
+        kt_record(1 + which, 0, cs);
+        e = launch_control(C, nb, which, cs);
+        kt_record(1 + which, 1, cs);
+        if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+      }
     }
   }
   if (a->do_control) {

@@ -39,18 +39,20 @@ def algorithmic_bytes(w, lo, hi):
     """Bytes the solve of swarms [lo, hi) must move (each input read once,
     each output written once), split by the kernel that owns
     them. Auction kernel, per swarm: fidx 4, q 24n, P_in 2n, P_out 2n,
-    status 16; per formation used: p 24n, adjacency bits 8nW. Control
-    kernel, per swarm: vel 24n, u 24n, u_safe 24n, ca n; per formation used:
-    gain_off 8, gains 72 E_f. Re-reads (the control kernel's q, p, adjacency,
-    P_out, the workspace hand-off) are implementation traffic, not counted."""
+    status 16; per formation used: p 24n, adjacency bits 8nW. Gain kernel
+    (DistCntrl), per swarm: vel 24n, u 24n; per formation used: gain_off 8,
+    gains 72 E_f. Safety kernel, per swarm: u_safe 24n, ca n. Re-reads (the
+    later kernels' q, p, adjacency, P_out, u, the workspace hand-off) are
+    implementation traffic, not counted."""
     n = w["n"]
     W = (n + 63) // 64
     Bc = hi - lo
     used = torch.unique(w["fidx"][lo:hi])
     E = w["E"][used].sum().item()
     auction = Bc * (4 + n * (24 + 2 + 2) + 16) + used.numel() * (24 * n + 8 * n * W)
-    control = Bc * n * (24 + 24 + 24 + 1) + used.numel() * 8 + 72 * E
-    return auction, control, E / used.numel()
+    gain = Bc * n * (24 + 24) + used.numel() * 8 + 72 * E
+    safety = Bc * n * (24 + 1)
+    return auction, gain, safety, E / used.numel()
 
 
 def pmc_traffic(n, B, kernel):
@@ -192,8 +194,8 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     call_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    kms = (ctypes.c_double * 2)()
-    kcnt = (ctypes.c_int * 2)()
+    kms = (ctypes.c_double * 3)()
+    kcnt = (ctypes.c_int * 3)()
     if lib.acl_internal_kernel_times(kms, kcnt) != 0:
         raise RuntimeError("kernel timing failed")
     lib.acl_internal_kernel_timing(0)
@@ -206,11 +208,13 @@ def main():
     # algorithmic bytes per launch (the chunk every launch but the last covers)
     ch = chunk_size(B)
     nlaunch = (B + ch - 1) // ch
-    a_all, c_all, e_avg = algorithmic_bytes(w, 0, B)
-    per_launch = {"auction": a_all / nlaunch, "control": c_all / nlaunch}
+    a_all, g_all, s_all, e_avg = algorithmic_bytes(w, 0, B)
+    c_all = g_all + s_all
+    per_launch = {"auction": a_all / nlaunch, "gain": g_all / nlaunch, "safety": s_all / nlaunch}
     kern = {}
     for k, (name, sym) in enumerate((("auction", "acl_amd::solve_kernel"),
-                                     ("control", "acl_amd::control_kernel"))):
+                                     ("gain", "acl_amd::gain_kernel"),
+                                     ("safety", "acl_amd::safety_kernel"))):
         avg = kms[k] / max(kcnt[k], 1)
         ach = per_launch[name] / (avg * 1e-3) / 1e9
         traffic, tsrc = pmc_traffic(n, B, sym) if args.formations == 0 else (None, None)
@@ -251,7 +255,7 @@ def main():
             "note": "dominant kernel by time; the auction kernel is LDS/VALU-bound "
                     "(CBAA tables live in LDS), see DESIGN.md",
             "kernels": kern,
-            "pipeline": {"what": "whole acl_solve_batch call (both kernels overlapped)",
+            "pipeline": {"what": "whole acl_solve_batch call (auction overlapped with gain+safety)",
                          "call_ms": call_ms, "bytes": a_all + c_all,
                          "achieved_GBs": pipe_ach, "frac": pipe_ach / HBM_PEAK_GBS},
         },

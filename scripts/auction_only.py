@@ -1,0 +1,35 @@
+"""Runs the auction kernel alone (do_control=0) on the bench workload, for
+PMC/ISA studies: python scripts/auction_only.py [--B 8192] [--reps 3]"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from aclswarm_amd import engine, workload  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--B", type=int, default=8192)
+ap.add_argument("--n", type=int, default=100)
+ap.add_argument("--reps", type=int, default=3)
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+gen = torch.Generator(device=dev)
+gen.manual_seed(1)
+w = workload.simform_workload(a.B, a.n, gen, dev)
+T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"])
+engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=False)  # warm
+torch.cuda.synchronize()
+ms = []
+for _ in range(a.reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    out = engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=False)
+    e1.record()
+    torch.cuda.synchronize()
+    ms.append(e0.elapsed_time(e1))
+st = engine.status_to_numpy(out["status"])
+print("auction-only B=%d n=%d: %.3f ms (min of %d), %.0f swarms/s; eff_rounds sum %d, valid %d" % (
+    a.B, a.n, min(ms), a.reps, a.B / min(ms) * 1e3, int(st["eff_rounds"].sum()),
+    int((st["flags"] & 1).sum())))
