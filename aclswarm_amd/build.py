@@ -11,7 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "lib", "libaclswarm_amd.so")
-SOURCES = ["solve.hip", "control.hip", "admm.hip", "api.cpp"]
+SOURCES = ["solve.hip", "solve_wide.hip", "control.hip", "admm.hip", "api.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
          "-fPIC", "-shared", "-Wall", "-Wno-unused-function"]

@@ -1,24 +1,27 @@
 // control.hip -- batched DistCntrl::compute + Safety for gfx950.
 //
-// Runs after the auction kernel (solve.hip) on the same swarms, on a second
-// stream so that one chunk's gain stream overlaps the next chunk's auction.
-// Two kernels:
+// Runs after the auction kernel (solve.hip / solve_wide.hip) on the same
+// swarms. Two kernels:
 //
 //   gain_kernel    DistCntrl::compute (aclswarm/src/distcntrl.cpp:46-102):
 //                  the HBM stream (72 B of gain block per directed edge).
 //                  One wave per vehicle v, lanes = formation neighbours j of
-//                  v's adopted point i (two chunks of 64), the 3x3 block A_ij
-//                  read from the 9 coalesced planes, pdistmat's Gram-formula
+//                  v's adopted point i (chunks of 64), the 3x3 block A_ij read
+//                  from the 9 coalesced planes, pdistmat's Gram-formula
 //                  distances (utils.h:137-147), atan scale terms gated on
 //                  |e| > thr, per-neighbour damping; a wave sum gives u (tree
 //                  order: parity within 1e-5 relative). Lean on registers and
-//                  LDS (~7 KB per swarm) so 8 swarms are resident per CU and
-//                  enough gain bytes are in flight.
-//   safety_kernel  Safety::cmdinCb saturation (safety.cpp:185-196) and
-//                  Safety::collisionAvoidance (safety.cpp:412-541): lanes find
-//                  the vehicles inside d_avoid_thresh, lane 0 sorts the sector
-//                  edges, unions them and picks the closest safe edge exactly
-//                  as the reference.
+//                  LDS (~12 KB per swarm at n = 100) so several swarms are
+//                  resident per CU and enough gain bytes are in flight. Its
+//                  epilogue is Safety::cmdinCb saturation (safety.cpp:185-196)
+//                  and the first test of Safety::collisionAvoidance
+//                  (safety.cpp:412-541): a vehicle with no other vehicle
+//                  inside d_avoid_thresh keeps its saturated command; the
+//                  others are appended to a list.
+//   ca_kernel      the rest of collisionAvoidance for the listed vehicles:
+//                  lanes build the sector edges of the close vehicles, lane 0
+//                  sorts them (std::sort on (angle, sign)), unions them and
+//                  picks the closest safe edge exactly as the reference.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -34,26 +37,42 @@ constexpr int kCtlWaves = kCtlBlock / 64;
 __host__ __device__ inline int cal16(int x) { return (x + 15) & ~15; }
 
 struct GainLayout {
-  int q, p, adjF, rowptr, Pt, myi, out, total;
+  int q, p, adjF, rowptr, Pt, myi, out, outs, cafl, total;
 };
 
 __host__ __device__ inline GainLayout make_gain_layout(int n) {
+  const int NW = (n + 63) >> 6;
   GainLayout L;
   int o = 0;
   L.q = o;      o = cal16(o + n * 3 * 8);
   L.p = o;      o = cal16(o + n * 3 * 8);
-  L.adjF = o;   o = cal16(o + n * 2 * 8);
+  L.adjF = o;   o = cal16(o + n * NW * 8);
   L.rowptr = o; o = cal16(o + (n + 1) * 4);
-  L.Pt = o;     o = cal16(o + n);
-  L.myi = o;    o = cal16(o + n);
-  L.out = o;    o = cal16(o + n * 3 * 8);
+  L.Pt = o;     o = cal16(o + n * 2);
+  L.myi = o;    o = cal16(o + n * 2);
+  L.out = o;    o = cal16(o + n * 3 * 8);   // u (DistCntrl)
+  L.outs = o;   o = cal16(o + n * 3 * 8);   // u_safe of the vehicles no one is close to
+  L.cafl = o;   o = cal16(o + n);
   L.total = o;
   return L;
+}
+
+// Safety::cmdinCb saturation (safety.cpp:185-196)
+__device__ __forceinline__ void saturate(const acl_safety_params_t& sp, double& c0, double& c1,
+                                         double& c2) {
+  const double velxy = sqrt(c0 * c0 + c1 * c1);
+  if (velxy > sp.max_vel_xy) {
+    c0 = c0 / velxy * sp.max_vel_xy;
+    c1 = c1 / velxy * sp.max_vel_xy;
+  }
+  const double velz = fabs(c2);
+  if (velz > sp.max_vel_z) c2 = c2 / velz * sp.max_vel_z;
 }
 
 __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
+  const int NW = (n + 63) >> 6;
   const GainLayout L = make_gain_layout(n);
   const int b = P.b0 + blockIdx.x;
   const int tid = threadIdx.x;
@@ -65,15 +84,16 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
   double* p = reinterpret_cast<double*>(smem + L.p);
   unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
   int* rowptr = reinterpret_cast<int*>(smem + L.rowptr);
-  unsigned char* Pt = smem + L.Pt;
-  unsigned char* myi = smem + L.myi;
+  uint16_t* Pt = reinterpret_cast<uint16_t*>(smem + L.Pt);
+  uint16_t* myi = reinterpret_cast<uint16_t*>(smem + L.myi);
   double* uo = reinterpret_cast<double*>(smem + L.out);
+  double* us = reinterpret_cast<double*>(smem + L.outs);
+  unsigned char* cafl = smem + L.cafl;
 
   const int f = P.fidx[b];
-  const int gw = (n + 63) >> 6;
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
-  const bool uniform = P.ws[(size_t)P.B * n + b] == 0;
-  const unsigned char* rows = P.ws + (size_t)P.B * (n + 1) + (size_t)b * n * n;
+  const bool uniform = P.wsMode[b] == 0;
+  const uint16_t* rows = P.wsRows + (size_t)b * n * n;
   {
     const double* gq = P.q + (size_t)b * n * 3;
     const double* gp = P.p + (size_t)f * n * 3;
@@ -81,28 +101,26 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
       q[k] = gq[k];
       p[k] = gp[k];
     }
-    const uint64_t* ga = P.adj + (size_t)f * n * gw;
-    for (int k = tid; k < n * 2; k += kCtlBlock) {
-      const int i = k >> 1, w = k & 1;
-      unsigned long long x = 0;
-      if (w < gw) {
-        x = ga[(size_t)i * gw + w];
-        if (w == gw - 1) x &= lastmask;
-      }
+    const uint64_t* ga = P.adj + (size_t)f * n * NW;
+    for (int k = tid; k < n * NW; k += kCtlBlock) {
+      unsigned long long x = ga[k];
+      if (k % NW == NW - 1) x &= lastmask;
       adjF[k] = x;
     }
     for (int v = tid; v < n; v += kCtlBlock) {
-      myi[v] = (unsigned char)P.P_out[(size_t)b * n + v];
-      if (uniform) Pt[v] = P.ws[(size_t)b * n + v];
+      myi[v] = P.P_out[(size_t)b * n + v];
+      if (uniform) Pt[v] = P.wsPt[(size_t)b * n + v];
     }
   }
   __syncthreads();
   // formation CSR row starts (edges enumerated row-major, diagonal included)
   if (wave == 0) {
     int base = 0;
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < NW; ++c) {
       const int i = lane + 64 * c;
-      const int cnt = (i < n) ? __popcll(adjF[2 * i]) + __popcll(adjF[2 * i + 1]) : 0;
+      int cnt = 0;
+      if (i < n)
+        for (int w = 0; w < NW; ++w) cnt += __popcll(adjF[i * NW + w]);
       int x = cnt;  // inclusive wave scan
       for (int o = 1; o < 64; o <<= 1) {
         const int y = __shfl_up(x, o, 64);
@@ -118,6 +136,9 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
   const int E = rowptr[n];
   const double* G = P.gains + 9 * P.gain_off[f];
   const acl_cntrl_gains_t g = P.g;
+  const acl_safety_params_t sp = P.s;
+  const double thr_hi = sp.d_avoid_thresh * (1.0 + 0x1p-40);
+  const double thr2hi = thr_hi * thr_hi;
   for (int v = wave; v < n; v += kCtlWaves) {
     const int i = myi[v];
     const double* gv = P.vel + ((size_t)b * n + v) * 3;
@@ -128,8 +149,8 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
     int ebase = rowptr[i];
 #pragma unroll 1
-    for (int c = 0; c < 2; ++c) {
-      const unsigned long long rowbits = adjF[2 * i + c];
+    for (int c = 0; c < NW; ++c) {
+      const unsigned long long rowbits = adjF[i * NW + c];
       const bool has = (rowbits >> lane) & 1ull;
       const int e = ebase + __popcll(rowbits & ((1ull << lane) - 1ull));
       ebase += __popcll(rowbits);
@@ -145,7 +166,7 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
         const double dxy = sqrt((Ni + Nj) - 2.0 * (pix * pjx + piy * pjy));
         const double dz = sqrt((Nzi + Nzj) - 2.0 * (piz * pjz));
         const double e_xy = sqrt(q0 * q0 + q1 * q1) - dxy;
-        const double e_z = sqrt(q2 * q2) - dz;
+        const double e_z = fabs(q2) - dz;  // |q_ij.z| = sqrt(q2^2) (no over/underflow)
         double Fxy = 0.0, Fz = 0.0;
         if (fabs(e_xy) > g.e_xy_thr) Fxy = g.K1_xy * acl_atan(g.K2_xy * e_xy);
         if (fabs(e_z) > g.e_z_thr) Fz = g.K1_z * acl_atan(g.K2_z * e_z);
@@ -157,115 +178,112 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
         acc2 += g.kp * up2 + g.kd * (-vel2);
       }
     }
-    const double cmd0 = wave_sum(acc0), cmd1 = wave_sum(acc1), cmd2 = wave_sum(acc2);
+    double cmd0 = wave_sum(acc0), cmd1 = wave_sum(acc1), cmd2 = wave_sum(acc2);
     if (lane == 0) {
       uo[3 * v] = cmd0; uo[3 * v + 1] = cmd1; uo[3 * v + 2] = cmd2;
     }
+    saturate(sp, cmd0, cmd1, cmd2);
+    // collisionAvoidance's first test: any other vehicle with
+    // !(|dq_xy| > d_avoid_thresh)? |dq_xy|^2 above (thr (1 + 2^-40))^2 is
+    // far for certain, so the sqrt is taken only near the threshold.
+    bool close = false;
+    for (int c = 0; c < NW; ++c) {
+      const int j = lane + 64 * c;
+      if (j < n && j != v) {
+        const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
+        const double s2 = dx * dx + dy * dy;
+        if (!(s2 > thr2hi)) close |= !(sqrt(s2) > sp.d_avoid_thresh);
+      }
+    }
+    const bool anyclose = __ballot(close) != 0ull;
+    if (lane == 0) {
+      us[3 * v] = cmd0; us[3 * v + 1] = cmd1; us[3 * v + 2] = cmd2;
+      cafl[v] = 0;
+      if (anyclose) {  // the rest of collisionAvoidance runs in ca_kernel
+        const unsigned slot = atomicAdd(P.ca_count, 1u);
+        P.ca_list[slot] = (unsigned)(b * n + v);
+      }
+    }
   }
   __syncthreads();
-  for (int k = tid; k < 3 * n; k += kCtlBlock) P.u[(size_t)b * n * 3 + k] = uo[k];
+  for (int k = tid; k < 3 * n; k += kCtlBlock) {
+    P.u[(size_t)b * n * 3 + k] = uo[k];
+    if (P.u_safe) P.u_safe[(size_t)b * n * 3 + k] = us[k];
+  }
+  if (P.ca_flag)
+    for (int v = tid; v < n; v += kCtlBlock) P.ca_flag[(size_t)b * n + v] = cafl[v];
 }
 
-struct SafeLayout {
-  int q, u, caA, caS, misc, total;
-};
+// collisionAvoidance (safety.cpp:412-541) for the vehicles gain_kernel
+// listed; one wave per listed vehicle, the swarm's q in the wave's LDS.
+constexpr int kCaWaves = 4;
 
-__host__ __device__ inline SafeLayout make_safe_layout(int n) {
-  SafeLayout L;
-  int o = 0;
-  L.q = o;    o = cal16(o + n * 3 * 8);
-  L.u = o;    o = cal16(o + n * 3 * 8);
-  L.caA = o;  o = cal16(o + kCtlWaves * 4 * n * 8);
-  L.caS = o;  o = cal16(o + kCtlWaves * 4 * n);
-  L.misc = o; o = cal16(o + 16);
-  L.total = o;
-  return L;
+__host__ __device__ inline int ca_wave_bytes(int n) {
+  return cal16(n * 3 * 8) + cal16(4 * n * 8) + cal16(4 * n);
 }
 
-__global__ void __launch_bounds__(kCtlBlock) safety_kernel(const CtlParams P) {
+__global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
-  const SafeLayout L = make_safe_layout(n);
-  const int b = P.b0 + blockIdx.x;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  if (P.status[b].flags & ACL_SWARM_BAD_INPUT) return;
-
-  double* q = reinterpret_cast<double*>(smem + L.q);
-  double* uo = reinterpret_cast<double*>(smem + L.u);
-  int* misc = reinterpret_cast<int*>(smem + L.misc);
-  {
-    const double* gq = P.q + (size_t)b * n * 3;
-    const double* gu = P.u + (size_t)b * n * 3;
-    for (int k = tid; k < 3 * n; k += kCtlBlock) {
-      q[k] = gq[k];
-      uo[k] = gu[k];
-    }
-    if (tid == 0) misc[0] = 0;
-  }
-  __syncthreads();
+  const int NW = (n + 63) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  unsigned char* base_ = smem + wave * ca_wave_bytes(n);
+  double* q = reinterpret_cast<double*>(base_);
+  double* caA = reinterpret_cast<double*>(base_ + cal16(n * 3 * 8));
+  signed char* caS = reinterpret_cast<signed char*>(base_ + cal16(n * 3 * 8) + cal16(4 * n * 8));
   const acl_safety_params_t sp = P.s;
-  double* caA = reinterpret_cast<double*>(smem + L.caA) + wave * (4 * n);
-  signed char* caS = reinterpret_cast<signed char*>(smem + L.caS) + wave * (4 * n);
-  int nca = 0;
-  for (int v = wave; v < n; v += kCtlWaves) {
-    double cmd0 = uo[3 * v], cmd1 = uo[3 * v + 1], cmd2 = uo[3 * v + 2];
+  const unsigned count = *P.ca_count;
+  for (unsigned it = blockIdx.x * kCaWaves + wave; it < count; it += gridDim.x * kCaWaves) {
+    const unsigned ent = P.ca_list[it];
+    const int b = (int)(ent / (unsigned)n), v = (int)(ent % (unsigned)n);
+    const double* gq = P.q + (size_t)b * n * 3;
+    for (int k = lane; k < 3 * n; k += 64) q[k] = gq[k];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const double* gu = P.u + ((size_t)b * n + v) * 3;
+    double cmd0 = gu[0], cmd1 = gu[1], cmd2 = gu[2];
+    saturate(sp, cmd0, cmd1, cmd2);
     const double qv0 = q[3 * v], qv1 = q[3 * v + 1];
-    // Safety::cmdinCb saturation (safety.cpp:185-196)
-    {
-      const double velxy = sqrt(cmd0 * cmd0 + cmd1 * cmd1);
-      if (velxy > sp.max_vel_xy) {
-        cmd0 = cmd0 / velxy * sp.max_vel_xy;
-        cmd1 = cmd1 / velxy * sp.max_vel_xy;
-      }
-      const double velz = fabs(cmd2);
-      if (velz > sp.max_vel_z) cmd2 = cmd2 / velz * sp.max_vel_z;
-    }
     // Safety::collisionAvoidance (safety.cpp:412-541)
     bool modified = false;
     {
-      bool cand[2];
-      double dxv[2], dyv[2], dv[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      int base = 0;
+      bool wrapped = false;
+      for (int c = 0; c < NW; ++c) {
         const int j = lane + 64 * c;
-        cand[c] = false;
-        dxv[c] = dyv[c] = dv[c] = 0.0;
+        bool cand = false;
+        double dx = 0.0, dy = 0.0, dd = 0.0;
         if (j < n && j != v) {
-          dxv[c] = q[3 * j] - qv0;
-          dyv[c] = q[3 * j + 1] - qv1;
-          dv[c] = sqrt(dxv[c] * dxv[c] + dyv[c] * dyv[c]);
-          cand[c] = !(dv[c] > sp.d_avoid_thresh);
+          dx = q[3 * j] - qv0;
+          dy = q[3 * j + 1] - qv1;
+          dd = sqrt(dx * dx + dy * dy);
+          cand = !(dd > sp.d_avoid_thresh);
         }
-      }
-      const unsigned long long m0 = __ballot(cand[0]), m1 = __ballot(cand[1]);
-      if (m0 | m1) {
-        bool wrapped = false;
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          if (cand[c]) {
-            const int slot = 4 * (__popcll((c ? m1 : m0) & ((1ull << lane) - 1ull)) +
-                                  (c ? __popcll(m0) : 0));
-            const double theta = atan2(dyv[c], dxv[c]);
-            const double x = sp.r_keep_out / dv[c];
-            const double alpha = fabs(asin(x < 1.0 ? x : 1.0));
-            const double beg = wrap_to_pi(theta - alpha);
-            const double end = wrap_to_pi(theta + alpha);
-            caA[slot] = beg;     caS[slot] = +1;
-            caA[slot + 1] = end; caS[slot + 1] = -1;
-            if (beg > end) {
-              wrapped = true;
-              caA[slot + 2] = -kPi; caS[slot + 2] = +1;
-              caA[slot + 3] = kPi;  caS[slot + 3] = -1;
-            } else {
-              caS[slot + 2] = 0;
-              caS[slot + 3] = 0;
-            }
+        const unsigned long long m = __ballot(cand);
+        if (cand) {
+          const int slot = 4 * (base + __popcll(m & ((1ull << lane) - 1ull)));
+          const double theta = atan2(dy, dx);
+          const double x = sp.r_keep_out / dd;
+          const double alpha = fabs(asin(x < 1.0 ? x : 1.0));
+          const double beg = wrap_to_pi(theta - alpha);
+          const double end = wrap_to_pi(theta + alpha);
+          caA[slot] = beg;     caS[slot] = +1;
+          caA[slot + 1] = end; caS[slot + 1] = -1;
+          if (beg > end) {
+            wrapped = true;
+            caA[slot + 2] = -kPi; caS[slot + 2] = +1;
+            caA[slot + 3] = kPi;  caS[slot + 3] = -1;
+          } else {
+            caS[slot + 2] = 0;
+            caS[slot + 3] = 0;
           }
         }
+        base += __popcll(m);
+      }
+      if (base > 0) {
         const bool didWrap = __any(wrapped);
-        const int nslot = 4 * (__popcll(m0) + __popcll(m1));
+        const int nslot = 4 * base;
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
         if (lane == 0) {
@@ -343,28 +361,37 @@ __global__ void __launch_bounds__(kCtlBlock) safety_kernel(const CtlParams P) {
       }
     }
     if (lane == 0) {
-      uo[3 * v] = cmd0; uo[3 * v + 1] = cmd1; uo[3 * v + 2] = cmd2;
-      if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = modified;
-      nca += modified;
+      if (P.u_safe) {
+        double* o = P.u_safe + ((size_t)b * n + v) * 3;
+        o[0] = cmd0; o[1] = cmd1; o[2] = cmd2;
+      }
+      if (modified) {
+        if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 1;
+        // n_ca is the high half of the status word at byte offset 8
+        atomicAdd(reinterpret_cast<unsigned*>(&P.status[b]) + 2, 1u << 16);
+        atomicOr(&P.status[b].flags, (uint32_t)ACL_SWARM_CA_ACTIVE);
+      }
     }
-  }
-  if (lane == 0 && nca) atomicAdd(&misc[0], nca);
-  __syncthreads();
-  if (P.u_safe)
-    for (int k = tid; k < 3 * n; k += kCtlBlock) P.u_safe[(size_t)b * n * 3 + k] = uo[k];
-  if (tid == 0 && misc[0]) {
-    P.status[b].n_ca = (uint16_t)misc[0];
-    P.status[b].flags |= ACL_SWARM_CA_ACTIVE;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
   }
 }
 
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream) {
   if (which == 0) {
     const GainLayout L = make_gain_layout(P.n);
+    if (L.total > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)gain_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, L.total);
     hipLaunchKernelGGL(gain_kernel, dim3(nb), dim3(kCtlBlock), L.total, stream, P);
   } else {
-    const SafeLayout L = make_safe_layout(P.n);
-    hipLaunchKernelGGL(safety_kernel, dim3(nb), dim3(kCtlBlock), L.total, stream, P);
+    // a fixed grid striding over the device-side count of listed vehicles
+    const int lds = kCaWaves * ca_wave_bytes(P.n);
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)ca_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(ca_kernel, dim3(nb < 1024 ? nb : 1024), dim3(64 * kCaWaves), lds, stream,
+                       P);
   }
   return hipGetLastError();
 }

@@ -1,13 +1,75 @@
-// control_params.h -- parameters of the control kernel (control.hip),
-// filled by acl_solve_batch (solve.hip).
+// control_params.h -- the solve workspace layout and the parameters of the
+// kernels acl_solve_batch launches (solve.hip, solve_wide.hip, control.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/aclswarm_amd.h"
 
 namespace acl_amd {
+
+constexpr int kMaxN = 128;      // LDS-resident auction kernel (solve.hip)
+constexpr int kMaxNWide = 512;  // tables-in-HBM auction kernel (solve_wide.hip)
+
+// Solve workspace (acl_solve_workspace_bytes), 256-byte aligned regions:
+//   pt      [B][n] u16    the adopted inverse assignment (point -> vehicle)
+//                         when every vehicle adopted the same one
+//   mode    [B]    u8     0: all vehicles use pt, 1: per-vehicle rows
+//   rows    [B][n][n] u16 per-vehicle inverse assignments (mode 1)
+//   u       [B][n][3] f64 DistCntrl output when the caller passes u = NULL
+//   calist  [B*n] u32     vehicles whose collisionAvoidance must finish
+//   cacount u32
+//   wide    [B] x (C n*n f32, CT n*n f32, T n*n u16): the CBAA tables of
+//           the n > 128 kernel, which do not fit LDS
+struct WsLayout {
+  size_t pt, mode, rows, u, calist, cacount, wide, wide_stride, total;
+};
+
+__host__ __device__ inline size_t ws_al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+__host__ __device__ inline WsLayout ws_layout(int n, int B) {
+  WsLayout W;
+  const size_t nb = (size_t)n, bb = (size_t)B;
+  size_t o = 0;
+  W.pt = o;      o = ws_al(o + bb * nb * 2);
+  W.mode = o;    o = ws_al(o + bb);
+  W.rows = o;    o = ws_al(o + bb * nb * nb * 2);
+  W.u = o;       o = ws_al(o + bb * nb * 3 * 8);
+  W.calist = o;  o = ws_al(o + bb * nb * 4);
+  W.cacount = o; o = ws_al(o + 16);
+  W.wide = o;
+  W.wide_stride = n > kMaxN ? ws_al(nb * nb * (4 + 4 + 2)) : 0;
+  o += bb * W.wide_stride;
+  W.total = o;
+  return W;
+}
+
+struct SolveParams {
+  int n, B, F, b0;
+  const double* p;
+  const uint64_t* adj;
+  const double* gains;
+  const int64_t* gain_off;
+  const int32_t* fidx;
+  const double* q;
+  const double* vel;
+  const uint16_t* P_in;
+  uint16_t* P_out;
+  acl_swarm_status_t* status;
+  double* u;
+  double* u_safe;
+  uint8_t* ca_flag;
+  uint16_t* who;
+  acl_cntrl_gains_t g;
+  acl_safety_params_t s;
+  int early_exit;
+  int do_control;
+  unsigned char* ws;  // workspace base (WsLayout)
+  WsLayout W;
+  unsigned long long* stamps;  // diagnostic: [B][16] s_memtime at phase ends (NULL = off)
+};
 
 struct CtlParams {
   int n, B, b0;
@@ -20,22 +82,27 @@ struct CtlParams {
   const double* vel;
   const uint16_t* P_out;
   acl_swarm_status_t* status;
-  double* u;        // DistCntrl output: the caller's u, or workspace scratch
+  double* u;  // DistCntrl output: the caller's u, or workspace scratch
   double* u_safe;
   uint8_t* ca_flag;
-  const unsigned char* ws;
+  const uint16_t* wsPt;
+  const uint8_t* wsMode;
+  const uint16_t* wsRows;
+  unsigned* ca_list;
+  unsigned* ca_count;
   acl_cntrl_gains_t g;
   acl_safety_params_t s;
 };
 
-// Control stage of chunk [P.b0, P.b0 + nb): which = 0 launches the gain
-// kernel (DistCntrl::compute, the HBM stream), 1 the safety kernel
-// (saturation + collision avoidance).
+// misc int slots of the auction kernels' LDS
+enum { M_BAD = 0, M_NONFIN = 1, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 8 };
+
+// Control stage: which = 0 launches the gain kernel for swarms
+// [P.b0, P.b0 + nb) (DistCntrl::compute, saturation, the collision test),
+// 1 the collisionAvoidance kernel over the listed vehicles.
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream);
 
-// Byte offset of the f64 u scratch inside the solve workspace.
-__host__ __device__ inline size_t ws_u_offset(int n, int B) {
-  return ((size_t)B * ((size_t)n + 1 + (size_t)n * n) + 255) & ~(size_t)255;
-}
+// The n > 128 auction kernel (solve_wide.hip).
+hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream);
 
 }  // namespace acl_amd

@@ -34,18 +34,17 @@
 // CPU restatement (oracle/).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <cstdlib>
 
 #include "../../include/aclswarm_amd.h"
 #include "common.h"
 #include "umeyama_dev.h"
+#include "control_params.h"
 
 namespace acl_amd {
 
 constexpr int kBlock = 512;  // 8 waves per swarm
 constexpr int kWaves = kBlock / 64;
 constexpr int kMinWavesPerEU = 6;  // 3 swarms x 8 waves per CU (LDS <= 160 KiB / 3)
-constexpr int kMaxN = 128;     // two 64-bit words per bitmask row, u8 indices
 
 // LDS layout (byte offsets, 16-byte aligned). The CBAA table T (n x n u8,
 // who per vehicle row) is written after the prices are known and overlays
@@ -89,33 +88,6 @@ __host__ __device__ inline Layout make_layout(int n) {
   L.total = o;
   return L;
 }
-
-struct SolveParams {
-  int n, B, F, b0;
-  const double* p;
-  const uint64_t* adj;
-  const double* gains;
-  const int64_t* gain_off;
-  const int32_t* fidx;
-  const double* q;
-  const double* vel;
-  const uint16_t* P_in;
-  uint16_t* P_out;
-  acl_swarm_status_t* status;
-  double* u;
-  double* u_safe;
-  uint8_t* ca_flag;
-  uint16_t* who;
-  acl_cntrl_gains_t g;
-  acl_safety_params_t s;
-  int early_exit;
-  int do_control;
-  unsigned char* ws;           // workspace: [B][n] shared rows, [B] mode, [B][n][n] rows
-  unsigned long long* stamps;  // diagnostic: [B][16] s_memtime at phase ends (NULL = off)
-};
-
-// misc int slots
-enum { M_BAD = 0, M_NONFIN = 1, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 8 };
 
 __device__ __forceinline__ void stamp(const SolveParams& P, int b, int tid, int k) {
   if (P.stamps && tid == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
@@ -587,12 +559,12 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
   {
     const bool allvalid = misc[M_NINV] == 0;
     const bool uniform = (allvalid && misc[M_AGREE]) || misc[M_NINV] == n;
-    unsigned char* wsPt = P.ws + (size_t)b * n;
-    if (tid == 0) P.ws[(size_t)P.B * n + b] = uniform ? 0 : 1;
+    uint16_t* wsPt = reinterpret_cast<uint16_t*>(P.ws + P.W.pt) + (size_t)b * n;
+    if (tid == 0) P.ws[P.W.mode + b] = uniform ? 0 : 1;
     if (uniform) {
       for (int jj = tid; jj < n; jj += kBlock) wsPt[jj] = allvalid ? T[jj] : Ptin[jj];
     } else {
-      unsigned char* rows = P.ws + (size_t)P.B * (n + 1) + (size_t)b * n * n;
+      uint16_t* rows = reinterpret_cast<uint16_t*>(P.ws + P.W.rows) + (size_t)b * n * n;
       for (int k = tid; k < n * n; k += kBlock) {
         const int v = k / n, jj = k - v * n;
         rows[k] = validv[v] ? T[k] : Ptin[jj];
@@ -623,34 +595,21 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
 // ---------------------------------------------------------------------------
 extern "C" acl_status_t acl__set_error(const char* msg);
 
-extern "C" int32_t acl_max_vehicles(void) { return acl_amd::kMaxN; }
+extern "C" int32_t acl_max_vehicles(void) { return acl_amd::kMaxNWide; }
 
 // Diagnostic hook (not part of the public ABI): when set, the next solves
 // record s_memtime at the end of each phase into stamps[B][8].
 static unsigned long long* g_stamps = nullptr;
 extern "C" void acl_internal_set_stamps(unsigned long long* stamps) { g_stamps = stamps; }
 
-#include "control_params.h"
-
 extern "C" size_t acl_solve_workspace_bytes(int32_t n, int32_t B) {
   if (n < 1 || B < 0) return 0;
-  return acl_amd::ws_u_offset(n, B) + (size_t)B * n * 3 * sizeof(double);
+  return acl_amd::ws_layout(n, B).total;
 }
 
 namespace {
-// Second stream + events for the auction -> control pipeline (one set per
-// device, created on first use).
-struct Pipe {
-  hipStream_t ctl = nullptr;
-  hipEvent_t ev[16] = {};
-  hipEvent_t done = nullptr;
-  bool ok = false;
-};
-Pipe g_pipe[16];
-
-// Diagnostic per-launch kernel timing (not part of the public ABI): events on
-// the stream each kernel runs on, so bench.py can time the auction and the
-// control kernel separately while they overlap.
+// Diagnostic per-launch kernel timing (not part of the public ABI): events
+// around each kernel launch, so bench.py can report every kernel's own time.
 struct KTiming {
   bool on = false;
   int n[3] = {0, 0, 0};
@@ -676,7 +635,7 @@ extern "C" void acl_internal_kernel_timing(int enable) {
 }
 
 // Sums the recorded launches: ms[k]/count[k] for k = 0 auction kernel,
-// 1 gain kernel, 2 safety kernel. Synchronises on the recorded events.
+// 1 gain kernel, 2 collision-avoidance kernel. Synchronises on the events.
 extern "C" int acl_internal_kernel_times(double* ms, int* count) {
   for (int k = 0; k < 3; ++k) {
     double t = 0.0;
@@ -693,18 +652,26 @@ extern "C" int acl_internal_kernel_times(double* ms, int* count) {
   return 0;
 }
 
+// The batch runs as three stream-ordered launches: the auction kernel over
+// all B swarms (solve_kernel for n <= 128, tables in LDS; solve_wide_kernel
+// for n <= 512, tables in the workspace), the gain kernel, and the
+// collision-avoidance kernel over the vehicles the gain kernel listed.
+// (Overlapping the auction with the control stage on a second stream was
+// measured slower: both compete for the same CU slots.)
 extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_solve_args_t* a,
                                         void* stream) {
   using namespace acl_amd;
   if (!F || !a) return acl__set_error("acl_solve_batch: null argument");
   const int n = F->n;
-  if (n < 1 || n > kMaxN) return acl__set_error("acl_solve_batch: n out of range [1, 128]");
+  if (n < 1 || n > kMaxNWide) return acl__set_error("acl_solve_batch: n out of range [1, 512]");
   if (a->B < 0) return acl__set_error("acl_solve_batch: B < 0");
   if (a->B == 0) return ACL_OK;
   if (!F->p || !F->adj || !a->fidx || !a->q || !a->P_in || !a->P_out || !a->status)
     return acl__set_error("acl_solve_batch: required pointer is NULL");
-  if (a->do_control && (!F->gains || !F->gain_off || !a->vel || !a->workspace))
-    return acl__set_error("acl_solve_batch: do_control needs gains, gain_off, vel and workspace");
+  if (!a->workspace)
+    return acl__set_error("acl_solve_batch: workspace is NULL (acl_solve_workspace_bytes)");
+  if (a->do_control && (!F->gains || !F->gain_off || !a->vel))
+    return acl__set_error("acl_solve_batch: do_control needs gains, gain_off and vel");
   SolveParams P;
   P.n = n; P.B = a->B; P.F = F->n_formations; P.b0 = 0;
   P.p = F->p; P.adj = F->adj; P.gains = F->gains; P.gain_off = F->gain_off;
@@ -713,73 +680,48 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   P.who = a->who; P.g = a->cntrl; P.s = a->safety;
   P.early_exit = a->early_exit; P.do_control = a->do_control;
   P.ws = (unsigned char*)a->workspace;
+  P.W = ws_layout(n, a->B);
   P.stamps = g_stamps;
-  const Layout L = make_layout(n);
-  static int configured = 0;
-  if (!configured) {
-    if (hipFuncSetAttribute((const void*)solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return acl__set_error("hipFuncSetAttribute failed");
-    configured = 1;
-  }
   hipStream_t s = (hipStream_t)stream;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  Pipe& pp = g_pipe[dev & 15];
-  static const bool serial = [] {
-    const char* e = getenv("ACL_SERIAL");
-    return e && e[0] == '1';
-  }();
-  if (a->do_control && !pp.ok) {
-    if (hipStreamCreateWithFlags(&pp.ctl, hipStreamNonBlocking) != hipSuccess)
-      return acl__set_error("hipStreamCreateWithFlags failed");
-    for (auto& e : pp.ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-    (void)hipEventCreateWithFlags(&pp.done, hipEventDisableTiming);
-    pp.ok = true;
-  }
-  // the control stream may not run ahead of work already queued on `s`
-  if (a->do_control) {
-    (void)hipEventRecord(pp.done, s);
-    (void)hipStreamWaitEvent(pp.ctl, pp.done, 0);
-  }
-  // chunks: the control kernel of chunk k overlaps the auction of chunk k+1
-  const int chunk = a->B <= 4096 ? a->B : ((a->B + 7) / 8 + 255) / 256 * 256;
-  int k = 0;
-  for (int b0 = 0; b0 < a->B; b0 += chunk, ++k) {
-    const int nb = (a->B - b0) < chunk ? (a->B - b0) : chunk;
-    P.b0 = b0;
-    kt_record(0, 0, s);
-    hipLaunchKernelGGL(solve_kernel, dim3(nb), dim3(kBlock), L.total, s, P);
-    kt_record(0, 1, s);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
-    if (a->do_control) {
-      hipEvent_t ev = pp.ev[k & 15];
-      (void)hipEventRecord(ev, s);
-      (void)hipStreamWaitEvent(pp.ctl, ev, 0);
-      CtlParams C;
-      C.n = n; C.B = a->B; C.b0 = b0;
-      C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
-      C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P_out;
-      C.status = a->status;
-      C.u = a->u ? a->u
-                 : (double*)((unsigned char*)a->workspace + ws_u_offset(n, a->B));
-      C.u_safe = a->u_safe; C.ca_flag = a->ca_flag;
-      C.ws = (const unsigned char*)a->workspace; C.g = a->cntrl; C.s = a->safety;
-      for (int which = 0; which < 2; ++which) {
-        // diagnostic: ACL_SERIAL=1 runs every kernel on the caller's stream
-        // (no overlap), so each kernel's time is its own
-        hipStream_t cs = serial ? s : pp.ctl;
-        kt_record(1 + which, 0, cs);
-        e = launch_control(C, nb, which, cs);
-        kt_record(1 + which, 1, cs);
-        if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
-      }
+  hipError_t e;
+  kt_record(0, 0, s);
+  if (n <= kMaxN) {
+    static int configured = 0;
+    if (!configured) {
+      if (hipFuncSetAttribute((const void*)solve_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+        return acl__set_error("hipFuncSetAttribute failed");
+      configured = 1;
     }
+    const Layout L = make_layout(n);
+    hipLaunchKernelGGL(solve_kernel, dim3(a->B), dim3(kBlock), L.total, s, P);
+    e = hipGetLastError();
+  } else {
+    e = launch_wide(P, a->B, s);
   }
-  if (a->do_control) {
-    (void)hipEventRecord(pp.done, pp.ctl);
-    (void)hipStreamWaitEvent(s, pp.done, 0);
+  kt_record(0, 1, s);
+  if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+  if (!a->do_control) return ACL_OK;
+  CtlParams C;
+  C.n = n; C.B = a->B; C.b0 = 0;
+  C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
+  C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P_out;
+  C.status = a->status;
+  C.u = a->u ? a->u : reinterpret_cast<double*>(P.ws + P.W.u);
+  C.u_safe = a->u_safe; C.ca_flag = a->ca_flag;
+  C.wsPt = reinterpret_cast<const uint16_t*>(P.ws + P.W.pt);
+  C.wsMode = P.ws + P.W.mode;
+  C.wsRows = reinterpret_cast<const uint16_t*>(P.ws + P.W.rows);
+  C.ca_list = reinterpret_cast<unsigned*>(P.ws + P.W.calist);
+  C.ca_count = reinterpret_cast<unsigned*>(P.ws + P.W.cacount);
+  C.g = a->cntrl; C.s = a->safety;
+  if (hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
+    return acl__set_error("hipMemsetAsync failed");
+  for (int which = 0; which < 2; ++which) {
+    kt_record(1 + which, 0, s);
+    e = launch_control(C, a->B, which, s);
+    kt_record(1 + which, 1, s);
+    if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
   }
   return ACL_OK;
 }

@@ -1,0 +1,570 @@
+// solve_wide.hip -- the batched auction for 128 < n <= 512 (config C4, N=500).
+//
+// Same algorithm and exactness as solve.hip (alignment, prices, CBAA to the
+// fixed point, adoption; see that file and SURVEY.md App. A), re-laid out
+// for swarms whose CBAA tables do not fit LDS: at n = 500 the price matrix
+// is 1 MB and the `who` table 0.5 MB per swarm, so both live in the solve
+// workspace (HBM, L2-resident while the swarm's workgroup runs):
+//
+//   C  [v][j] f32   row-major: a vehicle's select scans its row (coalesced)
+//   CT [j][v] f32   column-major copy: a column update gathers the prices
+//                   of the column's holders from one 2 KB row
+//   T  [j][u] u16   `who` table, column-major: a dirty-column update reads
+//                   and rewrites one contiguous column in place
+//
+// LDS keeps the per-swarm state every phase touches (~150 KB at n = 512):
+// points, alignments, the formation and vehicle-space neighbourhood
+// bitmasks (8 words per row), the dirty-column and outbid masks. One
+// workgroup of 16 waves per swarm; indices are u16 (the reference's u8
+// vehidx_t caps N at 255; widened as SURVEY.md 8d prescribes for C4).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/aclswarm_amd.h"
+#include "common.h"
+#include "control_params.h"
+#include "umeyama_dev.h"
+
+namespace acl_amd {
+
+constexpr int kWBlock = 1024;
+constexpr int kWWaves = kWBlock / 64;
+constexpr int kWMaxW = kMaxNWide / 64;  // 64-bit words per bitmask row
+constexpr int kWLevels = 3;
+
+struct WLayout {
+  int p, qf, out, sums, adjF, vadj, Pin, Ptin, valid, masks, seen, misc, total;
+};
+
+__host__ __device__ inline int wal(int x) { return (x + 15) & ~15; }
+
+__host__ __device__ inline WLayout make_wlayout(int n) {
+  const int NW = (n + 63) >> 6;
+  WLayout L;
+  int o = 0;
+  L.p = o;     o = wal(o + n * 24);
+  L.qf = o;    o = wal(o + n * 24);   // q in formation order
+  L.out = o;   o = wal(o + n * 48);   // R, t per vehicle
+  L.sums = o;                          // alignment sums, then the price tile
+  {
+    const int a = n * 64, t = 64 * 65 * 4;
+    o = wal(o + (a > t ? a : t));
+  }
+  L.adjF = o;  o = wal(o + n * NW * 8);
+  L.vadj = o;  o = wal(o + n * NW * 8);
+  L.Pin = o;   o = wal(o + n * 2);
+  L.Ptin = o;  o = wal(o + n * 2);
+  L.valid = o; o = wal(o + n);
+  L.masks = o; o = wal(o + 4 * NW * 8);                // dmask[2][NW], obm[2][NW]
+  L.seen = o;  o = wal(o + (kWWaves + 1) * NW * 8);   // permutation checks
+  L.misc = o;  o = wal(o + 64);
+  L.total = o;
+  return L;
+}
+
+// selectTaskAssignment (auctioneer.cpp:517-542) on vehicle v's row: the
+// first task j maximizing C[v][j] among C[v][j] > 0 and C[v][j] > price_j.
+// `fresh`: the row is all `none` (the START bid).
+__device__ int wide_select(int n, int NW, int v, int lane, const float* C, const float* CT,
+                           const uint16_t* T, bool fresh) {
+  unsigned key[kWMaxW];
+  unsigned lm = 0u;
+#pragma unroll
+  for (int c = 0; c < kWMaxW; ++c) {
+    key[c] = 0u;
+    const int j = lane + 64 * c;
+    if (c < NW && j < n) {
+      const float cv = C[(size_t)v * n + j];
+      const int w = fresh ? n : T[(size_t)j * n + v];
+      const float pr = w < n ? CT[(size_t)j * n + w] : 0.0f;
+      if (cv > 0.0f && cv > pr) key[c] = __float_as_uint(cv);
+    }
+    lm = lm > key[c] ? lm : key[c];
+  }
+  const unsigned M = wave_max_u32(lm);
+  if (M == 0u) return -1;
+#pragma unroll
+  for (int c = 0; c < kWMaxW; ++c) {
+    const unsigned long long e = __ballot(key[c] == M);
+    if (e) return 64 * c + __ffsll((long long)e) - 1;
+  }
+  return -1;
+}
+
+__global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = P.n;
+  const int NW = (n + 63) >> 6;
+  const WLayout L = make_wlayout(n);
+  const int b = P.b0 + blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+
+  double* p = reinterpret_cast<double*>(smem + L.p);
+  double* qf = reinterpret_cast<double*>(smem + L.qf);
+  double* out = reinterpret_cast<double*>(smem + L.out);
+  double* sums = reinterpret_cast<double*>(smem + L.sums);
+  float* tile = reinterpret_cast<float*>(smem + L.sums);
+  unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
+  unsigned long long* vadj = reinterpret_cast<unsigned long long*>(smem + L.vadj);
+  uint16_t* Pin = reinterpret_cast<uint16_t*>(smem + L.Pin);
+  uint16_t* Ptin = reinterpret_cast<uint16_t*>(smem + L.Ptin);
+  unsigned char* validv = smem + L.valid;
+  unsigned long long* dmask = reinterpret_cast<unsigned long long*>(smem + L.masks);
+  unsigned long long* obm = dmask + 2 * NW;
+  unsigned long long* seen = reinterpret_cast<unsigned long long*>(smem + L.seen);
+  int* misc = reinterpret_cast<int*>(smem + L.misc);
+
+  unsigned char* wsb = P.ws + P.W.wide + (size_t)b * P.W.wide_stride;
+  float* C = reinterpret_cast<float*>(wsb);
+  float* CT = C + (size_t)n * n;
+  uint16_t* T = reinterpret_cast<uint16_t*>(CT + (size_t)n * n);
+
+  const int f = P.fidx[b];
+  const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+
+  // ---------------- phase 0: load -----------------------------------------
+  {
+    const double* gp = P.p + (size_t)f * n * 3;
+    for (int k = tid; k < 3 * n; k += kWBlock) p[k] = gp[k];
+    const uint64_t* ga = P.adj + (size_t)f * n * NW;
+    for (int k = tid; k < n * NW; k += kWBlock) {
+      unsigned long long x = ga[k];
+      if (k % NW == NW - 1) x &= lastmask;
+      adjF[k] = x;
+    }
+    for (int k = tid; k < 4 * NW; k += kWBlock) dmask[k] = 0ull;
+    for (int k = tid; k < (kWWaves + 1) * NW; k += kWBlock) seen[k] = 0ull;
+    if (tid < 16) misc[tid] = 0;
+  }
+  __syncthreads();
+  if (tid == 0) misc[M_AGREE] = 1;
+  unsigned long long* seenP = seen + kWWaves * NW;
+  for (int v = tid; v < n; v += kWBlock) {
+    const unsigned pv = P.P_in[(size_t)b * n + v];
+    Pin[v] = (uint16_t)pv;
+    if (pv >= (unsigned)n) {
+      misc[M_BAD] = 1;
+    } else {
+      const unsigned long long bit = 1ull << (pv & 63);
+      const unsigned long long prev = atomicOr(&seenP[pv >> 6], bit);
+      if (prev & bit) misc[M_BAD] = 1;
+      Ptin[pv] = (uint16_t)v;
+    }
+  }
+  __syncthreads();
+  if (misc[M_BAD]) {
+    for (int v = tid; v < n; v += kWBlock) {
+      P.P_out[(size_t)b * n + v] = P.P_in[(size_t)b * n + v];
+      if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 0;
+    }
+    for (int k = tid; k < 3 * n; k += kWBlock) {
+      if (P.u) P.u[(size_t)b * n * 3 + k] = 0.0;
+      if (P.u_safe) P.u_safe[(size_t)b * n * 3 + k] = 0.0;
+    }
+    if (P.who)
+      for (int k = tid; k < n * n; k += kWBlock) P.who[(size_t)b * n * n + k] = 0xFFFF;
+    if (tid == 0) {
+      acl_swarm_status_t st = {};
+      st.flags = ACL_SWARM_BAD_INPUT;
+      st.rounds = (uint16_t)(2 * n);
+      P.status[b] = st;
+    }
+    return;
+  }
+  {
+    const double* gq = P.q + (size_t)b * n * 3;
+    for (int k = tid; k < 3 * n; k += kWBlock) {
+      const int j = k / 3, c = k - 3 * j;
+      qf[k] = gq[3 * Ptin[j] + c];
+    }
+  }
+  // vehicle-space closed neighbourhoods (bidIterComplete, auctioneer.cpp:419-437)
+  for (int v = wave; v < n; v += kWWaves) {
+    const int i = Pin[v];
+    for (int c = 0; c < NW; ++c) {
+      const int u = lane + 64 * c;
+      bool e = false;
+      if (u < n) {
+        const int pu = Pin[u];
+        e = (u == v) || ((adjF[i * NW + (pu >> 6)] >> (pu & 63)) & 1ull);
+      }
+      const unsigned long long m = __ballot(e);
+      if (lane == 0) vadj[v * NW + c] = m;
+    }
+  }
+  __syncthreads();
+
+  // ---------------- phase 1: alignment (see solve.hip) --------------------
+  for (int t = tid; t < 4 * n; t += kWBlock) {
+    const int v = t >> 2, c = t & 3;
+    const int i = Pin[v];
+    const double* src = (c < 2) ? (p + c) : (qf + (c - 2));
+    double acc = 0.0;
+    bool first = true;
+    for (int w = 0; w < NW; ++w) {
+      unsigned long long bits = adjF[i * NW + w];
+      if (w == (i >> 6)) bits |= 1ull << (i & 63);
+      for (int jj = 0; jj < 64; jj += 4) {
+        double val[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          const int j = 64 * w + jj + x;
+          val[x] = (j < n) ? src[3 * j] : 0.0;
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          const int j = 64 * w + jj + x;
+          if (j < n && ((bits >> (jj + x)) & 1ull)) {
+            acc = first ? val[x] : acc + val[x];
+            first = false;
+          }
+        }
+      }
+    }
+    sums[8 * v + c] = acc;
+  }
+  __syncthreads();
+  for (int t = tid; t < 4 * n; t += kWBlock) {
+    const int v = t >> 2, c = t & 3;
+    const int i = Pin[v];
+    int k = 0;
+    for (int w = 0; w < NW; ++w) {
+      unsigned long long bits = adjF[i * NW + w];
+      if (w == (i >> 6)) bits |= 1ull << (i & 63);
+      k += __popcll(bits);
+    }
+    const double oon = 1.0 / (double)k;
+    const int di = c >> 1, sj = c & 1;
+    const double smj = sums[8 * v + sj] * oon;
+    const double dmi = sums[8 * v + 2 + di] * oon;
+    const bool lazy = (k + 4) < 20;
+    double acc = 0.0;
+    bool first = true;
+    for (int w = 0; w < NW; ++w) {
+      unsigned long long bits = adjF[i * NW + w];
+      if (w == (i >> 6)) bits |= 1ull << (i & 63);
+      for (int jj = 0; jj < 64; jj += 4) {
+        double sv[4], dv[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          int j = 64 * w + jj + x;
+          j = j < n ? j : 0;
+          sv[x] = p[3 * j + sj];
+          dv[x] = qf[3 * j + di];
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          const int j = 64 * w + jj + x;
+          const double s0 = sv[x] - smj;
+          double d0 = dv[x] - dmi;
+          if (lazy) d0 = oon * d0;
+          if (j < n && ((bits >> (jj + x)) & 1ull)) {
+            acc = (lazy && first) ? d0 * s0 : acc + d0 * s0;
+            first = false;
+          }
+        }
+      }
+    }
+    sums[8 * v + 4 + c] = lazy ? acc : acc * oon;
+  }
+  __syncthreads();
+  for (int v = tid; v < n; v += kWBlock) {
+    const int i = Pin[v];
+    int k = 0;
+    for (int w = 0; w < NW; ++w) {
+      unsigned long long bits = adjF[i * NW + w];
+      if (w == (i >> 6)) bits |= 1ull << (i & 63);
+      k += __popcll(bits);
+    }
+    const double oon = 1.0 / (double)k;
+    const double sm[2] = {sums[8 * v] * oon, sums[8 * v + 1] * oon};
+    const double dm[2] = {sums[8 * v + 2] * oon, sums[8 * v + 3] * oon};
+    const double S[4] = {sums[8 * v + 4], sums[8 * v + 6], sums[8 * v + 5], sums[8 * v + 7]};
+    double R[4], t[2];
+    umeyama_finish(S, sm, dm, R, t);
+    double* o = out + 6 * v;
+    o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
+  }
+  __syncthreads();
+
+  // ---------------- phase 2: prices, in 64 x 64 tiles -----------------------
+  // each tile computed once, written row-major to C and, through LDS,
+  // column-major to CT (both coalesced)
+  int nonfin = 0;
+  for (int tv = 0; tv < n; tv += 64) {
+    for (int tj = 0; tj < n; tj += 64) {
+      for (int e = tid; e < 64 * 64; e += kWBlock) {
+        const int vv = e >> 6, jj = e & 63;
+        const int v = tv + vv, j = tj + jj;
+        if (v < n && j < n) {
+          const double* o = out + 6 * v;
+          const double* qv = qf + 3 * Pin[v];
+          const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
+          const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
+          const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
+          const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
+          const double dx = qv[0] - ax, dy = qv[1] - ay, dz = qv[2] - az;
+          const double nrm = sqrt((dx * dx + dy * dy) + dz * dz);
+          const float cpr = (float)(1.0 / (nrm + 1e-8));
+          tile[vv * 65 + jj] = cpr;
+          C[(size_t)v * n + j] = cpr;
+          nonfin |= (cpr != cpr);
+        }
+      }
+      __syncthreads();
+      for (int e = tid; e < 64 * 64; e += kWBlock) {
+        const int jj = e >> 6, vv = e & 63;
+        const int v = tv + vv, j = tj + jj;
+        if (v < n && j < n) CT[(size_t)j * n + v] = tile[vv * 65 + jj];
+      }
+      __syncthreads();
+    }
+  }
+  if (__any(nonfin) && lane == 0) misc[M_NONFIN] = 1;
+  for (int k = tid; k < n * n; k += kWBlock) T[k] = (uint16_t)n;  // reset: all `none`
+  __syncthreads();
+  const bool nonfinite = misc[M_NONFIN] != 0;
+
+  // ---------------- phase 3: CBAA ------------------------------------------
+  for (int v = wave; v < n; v += kWWaves) {
+    const int task = wide_select(n, NW, v, lane, C, CT, T, true);
+    if (task >= 0 && lane == 0) {
+      T[(size_t)task * n + v] = (uint16_t)v;
+      atomicOr(&dmask[NW + (task >> 6)], 1ull << (task & 63));
+    }
+  }
+  __syncthreads();
+  int eff = 0;
+  const int max_rounds = 2 * n;
+  for (int r = 1; r <= max_rounds; ++r) {
+    const int par = r & 1, npar = par ^ 1;
+    int idx = 0;
+    for (int w = 0; w < NW; ++w) {
+      unsigned long long m = dmask[par * NW + w];
+      while (m) {
+        const int j = 64 * w + __ffsll((long long)m) - 1;
+        m &= m - 1;
+        if ((idx++ % kWWaves) != wave) continue;
+        const uint16_t* Tc = T + (size_t)j * n;
+        const float* CTc = CT + (size_t)j * n;
+        unsigned wu[kWMaxW], key[kWMaxW], nw[kWMaxW];
+        bool dec[kWMaxW], need[kWMaxW];
+#pragma unroll
+        for (int c = 0; c < kWMaxW; ++c) {
+          const int u = lane + 64 * c;
+          const bool ok = c < NW && u < n;
+          wu[c] = ok ? Tc[u] : (unsigned)n;
+          key[c] = ok ? ((wu[c] < (unsigned)n ? __float_as_uint(CTc[wu[c]]) : 0u) + 1u) : 0u;
+          nw[c] = (unsigned)n;
+          dec[c] = !ok;
+          need[c] = false;
+        }
+        unsigned cap = 0xFFFFFFFFu;
+        for (int k = 0; k < kWLevels; ++k) {
+          unsigned lm = 0u;
+#pragma unroll
+          for (int c = 0; c < kWMaxW; ++c) {
+            const unsigned x = key[c] < cap ? key[c] : 0u;
+            lm = lm > x ? lm : x;
+          }
+          const unsigned Mk = wave_max_u32(lm);
+          if (Mk == 0u) break;
+          unsigned long long h[kWMaxW];
+          int wk = -1;
+#pragma unroll
+          for (int c = 0; c < kWMaxW; ++c) {
+            h[c] = __ballot(key[c] == Mk);
+            if (wk < 0 && h[c]) wk = __builtin_amdgcn_readlane((int)wu[c], __ffsll((long long)h[c]) - 1);
+          }
+          bool tl = false;
+#pragma unroll
+          for (int c = 0; c < kWMaxW; ++c) tl |= key[c] == Mk && wu[c] != (unsigned)wk;
+          const bool tk = nonfinite || __ballot(tl) != 0ull;
+          bool und = false;
+#pragma unroll
+          for (int c = 0; c < kWMaxW; ++c) {
+            if (!dec[c]) {
+              const int u = lane + 64 * c;
+              bool hit = false;
+#pragma unroll
+              for (int w2 = 0; w2 < kWMaxW; ++w2)
+                if (h[w2]) hit |= (vadj[u * NW + w2] & h[w2]) != 0ull;
+              if (hit) {
+                nw[c] = (unsigned)wk;
+                dec[c] = true;
+                need[c] = tk;
+              }
+            }
+            und |= !dec[c];
+          }
+          if (__ballot(und) == 0ull) break;
+          cap = Mk;
+        }
+        bool anyneed = false;
+#pragma unroll
+        for (int c = 0; c < kWMaxW; ++c) {
+          need[c] |= !dec[c];
+          anyneed |= need[c];
+        }
+        if (__ballot(anyneed) != 0ull) {
+          // exact ordered scan (ascending vehid, strict >): ties, NaN prices,
+          // vehicles no tracked level decides
+#pragma unroll
+          for (int c = 0; c < kWMaxW; ++c) {
+            if (need[c]) {
+              const int u = lane + 64 * c;
+              float bp = 0.0f;
+              unsigned bw = (unsigned)n;
+              bool first = true;
+              for (int w2 = 0; w2 < NW; ++w2) {
+                unsigned long long mm = vadj[u * NW + w2];
+                while (mm) {
+                  const int uu = 64 * w2 + __ffsll((long long)mm) - 1;
+                  mm &= mm - 1;
+                  const unsigned wx = Tc[uu];
+                  const float px = wx < (unsigned)n ? CTc[wx] : 0.0f;
+                  if (first) { bp = px; bw = wx; first = false; }
+                  else if (px > bp) { bp = px; bw = wx; }
+                }
+              }
+              nw[c] = bw;
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        bool ch = false;
+#pragma unroll
+        for (int c = 0; c < kWMaxW; ++c) {
+          const int u = lane + 64 * c;
+          const bool ok = c < NW && u < n;
+          if (ok) T[(size_t)j * n + u] = (uint16_t)nw[c];
+          const unsigned long long ob =
+              __ballot(ok && wu[c] == (unsigned)u && nw[c] != (unsigned)u);
+          if (ob && lane == 0) atomicOr(&obm[par * NW + c], ob);  // outbid (:502)
+          ch |= nw[c] != wu[c];
+        }
+        if (__ballot(ch) != 0ull && lane == 0)
+          atomicOr(&dmask[npar * NW + (j >> 6)], 1ull << (j & 63));
+      }
+    }
+    __syncthreads();
+    if (tid < NW) {
+      dmask[par * NW + tid] = 0ull;
+      obm[npar * NW + tid] = 0ull;
+    }
+    {
+      int idx2 = 0;
+      for (int w = 0; w < NW; ++w) {
+        unsigned long long m = obm[par * NW + w];
+        while (m) {
+          const int v = 64 * w + __ffsll((long long)m) - 1;
+          m &= m - 1;
+          if ((idx2++ % kWWaves) != wave) continue;
+          const int task = wide_select(n, NW, v, lane, C, CT, T, false);
+          if (task >= 0 && lane == 0) {
+            T[(size_t)task * n + v] = (uint16_t)v;
+            atomicOr(&dmask[npar * NW + (task >> 6)], 1ull << (task & 63));
+          }
+        }
+      }
+    }
+    __syncthreads();
+    bool changed = false;
+    for (int w = 0; w < NW; ++w) changed |= dmask[npar * NW + w] != 0ull;
+    if (changed) eff = r;
+    else if (P.early_exit) break;
+  }
+
+  // ---------------- phase 4: adoption --------------------------------------
+  for (int v = wave; v < n; v += kWWaves) {
+    unsigned long long* sw = seen + wave * NW;
+    if (lane < NW) sw[lane] = 0ull;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    bool bad = false, diff = false;
+    int mine = -1;
+    for (int c = 0; c < NW; ++c) {
+      const int jj = lane + 64 * c;
+      bool ismine = false;
+      if (jj < n) {
+        const int w = T[(size_t)jj * n + v];
+        if (w >= n) bad = true;
+        else atomicOr(&sw[w >> 6], 1ull << (w & 63));
+        diff |= w != T[(size_t)jj * n];
+        ismine = w == v;
+      }
+      const unsigned long long mm = __ballot(ismine);
+      if (mine < 0 && mm) mine = 64 * c + __ffsll((long long)mm) - 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    int cnt = 0;
+    for (int w = 0; w < NW; ++w) cnt += __popcll(sw[w]);
+    const bool valid = !__any(bad) && cnt == n && mine >= 0;
+    const bool agree = !__any(diff);
+    const int adopted = valid ? mine : Pin[v];
+    if (lane == 0) {
+      validv[v] = valid;
+      if (!valid) atomicAdd(&misc[M_NINV], 1);
+      if (!agree) misc[M_AGREE] = 0;
+      if (adopted != Pin[v]) misc[M_CHANGED] = 1;
+      P.P_out[(size_t)b * n + v] = (uint16_t)adopted;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (P.who) {
+    for (int k = tid; k < n * n; k += kWBlock) {
+      const int v = k / n, jj = k - v * n;
+      const int w = T[(size_t)jj * n + v];
+      P.who[(size_t)b * n * n + k] = (w >= n) ? (uint16_t)0xFFFF : (uint16_t)w;
+    }
+  }
+  __syncthreads();
+  {
+    const bool allvalid = misc[M_NINV] == 0;
+    const bool uniform = (allvalid && misc[M_AGREE]) || misc[M_NINV] == n;
+    uint16_t* wsPt = reinterpret_cast<uint16_t*>(P.ws + P.W.pt) + (size_t)b * n;
+    if (tid == 0) P.ws[P.W.mode + b] = uniform ? 0 : 1;
+    if (uniform) {
+      for (int jj = tid; jj < n; jj += kWBlock) wsPt[jj] = allvalid ? T[(size_t)jj * n] : Ptin[jj];
+    } else {
+      uint16_t* rows = reinterpret_cast<uint16_t*>(P.ws + P.W.rows) + (size_t)b * n * n;
+      for (int k = tid; k < n * n; k += kWBlock) {
+        const int v = k / n, jj = k - v * n;
+        rows[k] = validv[v] ? T[(size_t)jj * n + v] : Ptin[jj];
+      }
+    }
+  }
+  if (tid == 0) {
+    acl_swarm_status_t st = {};
+    uint32_t fl = 0;
+    if (misc[M_NINV] == 0) fl |= ACL_SWARM_VALID;
+    if (misc[M_AGREE]) fl |= ACL_SWARM_AGREE;
+    if (misc[M_CHANGED]) fl |= ACL_SWARM_CHANGED;
+    if (nonfinite) fl |= ACL_SWARM_NONFINITE;
+    st.flags = fl;
+    st.eff_rounds = (uint16_t)eff;
+    st.rounds = (uint16_t)(2 * n);
+    st.n_invalid = (uint16_t)misc[M_NINV];
+    P.status[b] = st;
+  }
+}
+
+hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream) {
+  const WLayout L = make_wlayout(P.n);
+  static bool configured = false;
+  if (!configured) {
+    const hipError_t e = hipFuncSetAttribute((const void*)solve_wide_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             160 * 1024);
+    if (e != hipSuccess) return e;
+    configured = true;
+  }
+  hipLaunchKernelGGL(solve_wide_kernel, dim3(nb), dim3(kWBlock), L.total, stream, P);
+  return hipGetLastError();
+}
+
+}  // namespace acl_amd

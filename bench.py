@@ -40,19 +40,20 @@ def algorithmic_bytes(w, lo, hi):
     each output written once), split by the kernel that owns
     them. Auction kernel, per swarm: fidx 4, q 24n, P_in 2n, P_out 2n,
     status 16; per formation used: p 24n, adjacency bits 8nW. Gain kernel
-    (DistCntrl), per swarm: vel 24n, u 24n; per formation used: gain_off 8,
-    gains 72 E_f. Safety kernel, per swarm: u_safe 24n, ca n. Re-reads (the
-    later kernels' q, p, adjacency, P_out, u, the workspace hand-off) are
-    implementation traffic, not counted."""
+    (DistCntrl + saturation + the collision test), per swarm: vel 24n,
+    u 24n, u_safe 24n, ca n; per formation used: gain_off 8, gains 72 E_f.
+    The collision-avoidance kernel touches only the vehicles the gain kernel
+    listed (none in this workload): 0. Re-reads (the later kernels' q, p,
+    adjacency, P_out, the workspace hand-off) are implementation traffic,
+    not counted."""
     n = w["n"]
     W = (n + 63) // 64
     Bc = hi - lo
     used = torch.unique(w["fidx"][lo:hi])
     E = w["E"][used].sum().item()
     auction = Bc * (4 + n * (24 + 2 + 2) + 16) + used.numel() * (24 * n + 8 * n * W)
-    gain = Bc * n * (24 + 24) + used.numel() * 8 + 72 * E
-    safety = Bc * n * (24 + 1)
-    return auction, gain, safety, E / used.numel()
+    gain = Bc * n * (24 + 24 + 24 + 1) + used.numel() * 8 + 72 * E
+    return auction, gain, 0, E / used.numel()
 
 
 def pmc_traffic(n, B, kernel):
@@ -69,8 +70,8 @@ def pmc_traffic(n, B, kernel):
 
 
 def chunk_size(B):
-    """acl_solve_batch's chunking (solve.hip): one launch per chunk."""
-    return B if B <= 4096 else ((B + 7) // 8 + 255) // 256 * 256
+    """acl_solve_batch launches each kernel once over all B swarms."""
+    return B
 
 
 def cpu_baseline(w, out, budget_s, nthreads):
@@ -210,11 +211,11 @@ def main():
     nlaunch = (B + ch - 1) // ch
     a_all, g_all, s_all, e_avg = algorithmic_bytes(w, 0, B)
     c_all = g_all + s_all
-    per_launch = {"auction": a_all / nlaunch, "gain": g_all / nlaunch, "safety": s_all / nlaunch}
+    per_launch = {"auction": a_all / nlaunch, "gain": g_all / nlaunch, "ca": s_all / nlaunch}
     kern = {}
     for k, (name, sym) in enumerate((("auction", "acl_amd::solve_kernel"),
                                      ("gain", "acl_amd::gain_kernel"),
-                                     ("safety", "acl_amd::safety_kernel"))):
+                                     ("ca", "acl_amd::ca_kernel"))):
         avg = kms[k] / max(kcnt[k], 1)
         ach = per_launch[name] / (avg * 1e-3) / 1e9
         traffic, tsrc = pmc_traffic(n, B, sym) if args.formations == 0 else (None, None)
@@ -255,7 +256,7 @@ def main():
             "note": "dominant kernel by time; the auction kernel is LDS/VALU-bound "
                     "(CBAA tables live in LDS), see DESIGN.md",
             "kernels": kern,
-            "pipeline": {"what": "whole acl_solve_batch call (auction overlapped with gain+safety)",
+            "pipeline": {"what": "whole acl_solve_batch call (auction, gain, ca kernels)",
                          "call_ms": call_ms, "bytes": a_all + c_all,
                          "achieved_GBs": pipe_ach, "frac": pipe_ach / HBM_PEAK_GBS},
         },

@@ -3,8 +3,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /root/repo
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_parity.log 2>&1 || { echo "parity failed"; tail -50 gpurun_out/pytest_parity.log; exit 1; }
-tail -2 gpurun_out/pytest_parity.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_parity.log 2>&1 || { echo "parity failed"; tail -50 gpurun_out/pytest_parity.log; exit 1; }
+grep -E "PASS|FAIL|passed|failed" gpurun_out/pytest_parity.log | tail -40
 timeout -k 10 120 python scripts/auction_only.py --B 65536 --reps 3 2>&1 | grep -v amdgpu.ids
 timeout -k 10 300 python scripts/phase_profile.py 2>&1 | grep -v amdgpu.ids | head -9
 timeout -k 10 600 python bench.py --no-cpu ${BENCH_ARGS} > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err || { echo "bench failed"; tail -30 gpurun_out/bench_quick.err; exit 1; }

@@ -38,7 +38,7 @@ def test_defaults_match_reference_values():
     a = L.default_admm_params()  # solver.h:18-31
     assert (a.thrSparseZero, a.thrPlanar, a.epsEig, a.mu, a.thresh, a.threshTr, a.maxItr) == \
         (1e-8, 1e-2, 1e-5, 1.0, 1e-4, 0.10, 10)
-    assert L.lib().acl_max_vehicles() == 128
+    assert L.lib().acl_max_vehicles() == 512
 
 
 def test_pack_adjacency_and_gains():
@@ -79,7 +79,7 @@ def test_solve_batch_argument_errors_without_gpu():
     a.B = 1
     rc = lib.acl_solve_batch(ct.byref(F), ct.byref(a), None)
     assert rc == 1 and b"n out of range" in lib.acl_last_error()
-    F.n = 129
+    F.n = 513
     assert lib.acl_solve_batch(ct.byref(F), ct.byref(a), None) == 1
     F.n = 10
     assert lib.acl_solve_batch(ct.byref(F), ct.byref(a), None) == 1  # NULL pointers

@@ -214,3 +214,58 @@ def test_max_n_128(cuda):
     gpu = _gpu_solve([p], [adj], [G], np.zeros(B, np.int32), q, vel, P_in)
     ref = _oracle([p], [adj], [G], np.zeros(B, np.int32), q, vel, P_in)
     _compare(gpu, ref)
+
+
+def _wide_case(rng, n, B, side, missing):
+    p = H.random_positions(rng, n, side)
+    p[:, 2] = rng.uniform(0.0, 2.0, n)
+    adj = (np.ones((n, n)) - np.eye(n)).astype(np.uint8)
+    for _ in range(missing):
+        i, j = rng.randint(0, n, 2)
+        adj[i, j] = adj[j, i] = 0
+    G = H.synth_gains(rng, adj)
+    q = np.stack([H.random_positions(rng, n, side) for _ in range(B)])
+    vel = rng.normal(0, 0.1, (B, n, 3))
+    P_in = np.stack([H.random_perm(rng, n) if b % 2 else np.arange(n, dtype=np.uint16)
+                     for b in range(B)])
+    return [p], [adj], [G], np.zeros(B, np.int32), q, vel, P_in
+
+
+@pytest.mark.parametrize("n", [129, 200, 320])
+def test_wide_n(cuda, n):
+    """128 < n <= 512: the tables-in-HBM auction kernel (solve_wide.hip) and
+    the control kernels with more than two 64-lane chunks, u16 indices."""
+    rng = np.random.RandomState(n)
+    side = 20.0 * (n / 20.0) ** 0.5
+    args = _wide_case(rng, n, 3, side, n // 2)
+    gpu = _gpu_solve(*args)
+    ref = _oracle(*args)
+    _compare(gpu, ref)
+
+
+def test_wide_collision_avoidance(cuda):
+    """Crowded n = 160 swarms: the collision-avoidance list over three chunks."""
+    rng = np.random.RandomState(160)
+    n = 160
+    p = H.random_positions(rng, n, 56.0)
+    adj = (np.ones((n, n)) - np.eye(n)).astype(np.uint8)
+    G = H.synth_gains(rng, adj, scale=1.0)
+    B = 3
+    q = np.stack([H.dense_positions(rng, n, 14.0 + 2 * b) for b in range(B)])
+    vel = rng.normal(0, 0.5, (B, n, 3))
+    P_in = np.stack([H.random_perm(rng, n) for _ in range(B)])
+    args = ([p], [adj], [G], np.zeros(B, np.int32), q, vel, P_in)
+    gpu = _gpu_solve(*args)
+    ref = _oracle(*args)
+    assert sum(int(r["status"]["n_ca"]) for r in ref) > 20
+    _compare(gpu, ref)
+
+
+def test_n500_config_c4(cuda):
+    """Config C4 size (N=500, noncomplete; u16 indices): one swarm against the
+    CPU restatement."""
+    rng = np.random.RandomState(500)
+    args = _wide_case(rng, 500, 1, 90.0, 400)
+    gpu = _gpu_solve(*args)
+    ref = _oracle(*args)
+    _compare(gpu, ref)
