@@ -102,6 +102,93 @@ __device__ __forceinline__ double acl_atan(double x) {
   return copysign(r, x);
 }
 
+// A wave-uniform double moved to SGPRs (two v_readfirstlane).
+__device__ __forceinline__ double uni(double x) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Fast fp64 kernels for the control law, whose parity is tolerance-based
+// (1e-5 relative): a square root from v_rsq_f64 refined by one Goldschmidt
+// step and a correction (about 1 ulp for normal inputs; 0, +inf and
+// negative inputs as IEEE sqrt), and a quotient from v_rcp_f64 refined by
+// two Newton steps (about 1 ulp; den finite and nonzero).
+__device__ __forceinline__ double sqrt_nr(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = __builtin_fma(-g, h, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  const double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  return (x == 0.0 || __builtin_isinf(x)) ? x : g;
+}
+
+__device__ __forceinline__ double div_nr(double num, double den) {
+  double r = __builtin_amdgcn_rcp(den);
+  r = __builtin_fma(__builtin_fma(-den, r, 1.0), r, r);
+  r = __builtin_fma(__builtin_fma(-den, r, 1.0), r, r);
+  const double q = num * r;
+  return __builtin_fma(__builtin_fma(-den, q, num), r, q);
+}
+
+// acl_atan with the fast quotient and fused multiply-adds (control law only).
+__device__ __forceinline__ double acl_atan_fast(double x) {
+  const double ax = fabs(x);
+  const bool r0 = ax >= 0.4375, r1 = ax >= 0.6875, r2 = ax >= 1.1875, r3 = ax >= 2.4375;
+  double num = ax, den = 1.0, hi = 0.0, lo = 0.0;
+  if (r0) { num = 2.0 * ax - 1.0; den = 2.0 + ax; hi = 4.63647609000806093515e-01; lo = 2.26987774529616870924e-17; }
+  if (r1) { num = ax - 1.0; den = ax + 1.0; hi = 7.85398163397448278999e-01; lo = 3.06161699786838301793e-17; }
+  if (r2) { num = ax - 1.5; den = 1.0 + 1.5 * ax; hi = 9.82793723247329054082e-01; lo = 1.39033110312309984516e-17; }
+  if (r3) { num = -1.0; den = ax; hi = 1.57079632679489655800e+00; lo = 6.12323399573676603587e-17; }
+  const double t = r0 ? div_nr(num, den) : ax;
+  const double z = t * t, w = z * z;
+  const double s1 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, __builtin_fma(w,
+                    __builtin_fma(w, 1.62858201153657823623e-02, 4.97687799461593236017e-02),
+                    6.66107313738753120669e-02), 9.09088713343650656196e-02),
+                    1.42857142725034663711e-01), 3.33333333333329318027e-01);
+  const double s2 = w * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w,
+                    __builtin_fma(w, -3.65315727442169155270e-02, -5.83357013379057348645e-02),
+                    -7.69187620504482999495e-02), -1.11111104054623557880e-01),
+                    -1.99999999998764832476e-01);
+  const double r = r0 ? hi - (__builtin_fma(t, s1 + s2, -lo) - t) : __builtin_fma(-t, s1 + s2, t);
+  return (ax == __builtin_inf()) ? copysign(1.57079632679489655800e+00, x) : copysign(r, x);
+}
+
+// acl_atan_fast with the range reduction read from a table (`tab`, 5 rows
+// of {a, b, c, d, hi, lo}: t = (a|x| + b) / (c|x| + d), atan = hi + ...):
+// three LDS reads instead of four select chains, far fewer live registers.
+// kAtanTab is the table's content; callers stage it in LDS.
+__device__ constexpr double kAtanTab[5][6] = {
+    {1.0, 0.0, 0.0, 1.0, 0.0, 0.0},
+    {2.0, -1.0, 1.0, 2.0, 4.63647609000806093515e-01, 2.26987774529616870924e-17},
+    {1.0, -1.0, 1.0, 1.0, 7.85398163397448278999e-01, 3.06161699786838301793e-17},
+    {1.0, -1.5, 1.5, 1.0, 9.82793723247329054082e-01, 1.39033110312309984516e-17},
+    {0.0, -1.0, 1.0, 0.0, 1.57079632679489655800e+00, 6.12323399573676603587e-17}};
+
+__device__ __forceinline__ double acl_atan_tab(double x, const double* tab) {
+  const double ax = fabs(x);
+  const int id = (ax >= 0.4375) + (ax >= 0.6875) + (ax >= 1.1875) + (ax >= 2.4375);
+  const double* rw = tab + 6 * id;
+  const double num = __builtin_fma(rw[0], ax, rw[1]);
+  const double den = __builtin_fma(rw[2], ax, rw[3]);
+  const double t = id ? div_nr(num, den) : ax;
+  const double z = t * t, w = z * z;
+  const double s1 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, __builtin_fma(w,
+                    __builtin_fma(w, 1.62858201153657823623e-02, 4.97687799461593236017e-02),
+                    6.66107313738753120669e-02), 9.09088713343650656196e-02),
+                    1.42857142725034663711e-01), 3.33333333333329318027e-01);
+  const double s2 = w * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w,
+                    __builtin_fma(w, -3.65315727442169155270e-02, -5.83357013379057348645e-02),
+                    -7.69187620504482999495e-02), -1.11111104054623557880e-01),
+                    -1.99999999998764832476e-01);
+  const double r = id ? rw[4] - (__builtin_fma(t, s1 + s2, -rw[5]) - t)
+                      : __builtin_fma(-t, s1 + s2, t);
+  return (ax == __builtin_inf()) ? copysign(1.57079632679489655800e+00, x) : copysign(r, x);
+}
+
 __device__ __forceinline__ double wrap_to_pi(double a) {  // utils.h:275-280
   if (a > kPi) return a - 2 * kPi;
   if (a < -kPi) return a + 2 * kPi;

@@ -37,7 +37,7 @@ constexpr int kCtlWaves = kCtlBlock / 64;
 __host__ __device__ inline int cal16(int x) { return (x + 15) & ~15; }
 
 struct GainLayout {
-  int q, p, adjF, rowptr, Pt, myi, out, outs, cafl, total;
+  int q, p, adjF, rowptr, Pt, myi, out, outs, cafl, atab, total;
 };
 
 __host__ __device__ inline GainLayout make_gain_layout(int n) {
@@ -53,6 +53,7 @@ __host__ __device__ inline GainLayout make_gain_layout(int n) {
   L.out = o;    o = cal16(o + n * 3 * 8);   // u (DistCntrl)
   L.outs = o;   o = cal16(o + n * 3 * 8);   // u_safe of the vehicles no one is close to
   L.cafl = o;   o = cal16(o + n);
+  L.atab = o;   o = cal16(o + 30 * 8);      // atan range-reduction table
   L.total = o;
   return L;
 }
@@ -89,6 +90,8 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
   double* uo = reinterpret_cast<double*>(smem + L.out);
   double* us = reinterpret_cast<double*>(smem + L.outs);
   unsigned char* cafl = smem + L.cafl;
+  double* atab = reinterpret_cast<double*>(smem + L.atab);
+  if (tid < 30) atab[tid] = kAtanTab[tid / 6][tid % 6];
 
   const int f = P.fidx[b];
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
@@ -141,10 +144,11 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
   const double thr2hi = thr_hi * thr_hi;
   for (int v = wave; v < n; v += kCtlWaves) {
     const int i = myi[v];
+    // the vehicle's values are wave-uniform: held in SGPRs
     const double* gv = P.vel + ((size_t)b * n + v) * 3;
-    const double vel0 = gv[0], vel1 = gv[1], vel2 = gv[2];
-    const double qv0 = q[3 * v], qv1 = q[3 * v + 1], qv2 = q[3 * v + 2];
-    const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
+    const double vel0 = uni(gv[0]), vel1 = uni(gv[1]), vel2 = uni(gv[2]);
+    const double qv0 = uni(q[3 * v]), qv1 = uni(q[3 * v + 1]), qv2 = uni(q[3 * v + 2]);
+    const double pix = uni(p[3 * i]), piy = uni(p[3 * i + 1]), piz = uni(p[3 * i + 2]);
     const double Ni = pix * pix + piy * piy, Nzi = piz * piz;
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
     int ebase = rowptr[i];
@@ -155,6 +159,9 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
       const int e = ebase + __popcll(rowbits & ((1ull << lane) - 1ull));
       ebase += __popcll(rowbits);
       if (has) {
+        // tolerance-based parity (1e-5 relative): fused multiply-adds and the
+        // refined fast sqrt / quotient (common.h) are allowed here
+#pragma clang fp contract(fast)
         double A[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) A[k] = __builtin_nontemporal_load(G + (size_t)k * E + e);
@@ -163,13 +170,22 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
         const double q0 = q[3 * uu] - qv0, q1 = q[3 * uu + 1] - qv1, q2 = q[3 * uu + 2] - qv2;
         const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
         const double Nj = pjx * pjx + pjy * pjy, Nzj = pjz * pjz;
-        const double dxy = sqrt((Ni + Nj) - 2.0 * (pix * pjx + piy * pjy));
-        const double dz = sqrt((Nzi + Nzj) - 2.0 * (piz * pjz));
-        const double e_xy = sqrt(q0 * q0 + q1 * q1) - dxy;
+        const double dxy = sqrt_nr((Ni + Nj) - 2.0 * (pix * pjx + piy * pjy));
+        const double dz = sqrt_nr((Nzi + Nzj) - 2.0 * (piz * pjz));
+        const double e_xy = sqrt_nr(q0 * q0 + q1 * q1) - dxy;
         const double e_z = fabs(q2) - dz;  // |q_ij.z| = sqrt(q2^2) (no over/underflow)
+        // the two gated atan terms, one after the other (register pressure)
         double Fxy = 0.0, Fz = 0.0;
-        if (fabs(e_xy) > g.e_xy_thr) Fxy = g.K1_xy * acl_atan(g.K2_xy * e_xy);
-        if (fabs(e_z) > g.e_z_thr) Fz = g.K1_z * acl_atan(g.K2_z * e_z);
+        const bool gxy = fabs(e_xy) > g.e_xy_thr, gz = fabs(e_z) > g.e_z_thr;
+#pragma unroll 1
+        for (int kk = 0; kk < 2; ++kk) {
+          const bool on = kk ? gz : gxy;
+          if (on) {
+            const double fa = kk ? g.K1_z * acl_atan_tab(g.K2_z * e_z, atab)
+                                 : g.K1_xy * acl_atan_tab(g.K2_xy * e_xy, atab);
+            if (kk) Fz = fa; else Fxy = fa;
+          }
+        }
         const double up0 = ((A[0] * q0 + A[1] * q1) + A[2] * q2) + Fxy * q0;
         const double up1 = ((A[3] * q0 + A[4] * q1) + A[5] * q2) + Fxy * q1;
         const double up2 = ((A[6] * q0 + A[7] * q1) + A[8] * q2) + Fz * q2;

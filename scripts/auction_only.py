@@ -13,23 +13,24 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--B", type=int, default=8192)
 ap.add_argument("--n", type=int, default=100)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--control", action="store_true", help="run the control kernels too")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 gen = torch.Generator(device=dev)
 gen.manual_seed(1)
 w = workload.simform_workload(a.B, a.n, gen, dev)
 T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"])
-engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=False)  # warm
+engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=a.control)  # warm
 torch.cuda.synchronize()
 ms = []
 for _ in range(a.reps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    out = engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=False)
+    out = engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=a.control)
     e1.record()
     torch.cuda.synchronize()
     ms.append(e0.elapsed_time(e1))
 st = engine.status_to_numpy(out["status"])
-print("auction-only B=%d n=%d: %.3f ms (min of %d), %.0f swarms/s; eff_rounds sum %d, valid %d" % (
+print(("solve" if a.control else "auction-only") + " B=%d n=%d: %.3f ms (min of %d), %.0f swarms/s; eff_rounds sum %d, valid %d" % (
     a.B, a.n, min(ms), a.reps, a.B / min(ms) * 1e3, int(st["eff_rounds"].sum()),
     int((st["flags"] & 1).sum())))
