@@ -110,6 +110,12 @@ __device__ __forceinline__ double uni(double x) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+__device__ __forceinline__ unsigned long long uni_u64(unsigned long long u) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+
 // Fast fp64 kernels for the control law, whose parity is tolerance-based
 // (1e-5 relative): a square root from v_rsq_f64 refined by one Goldschmidt
 // step and a correction (about 1 ulp for normal inputs; 0, +inf and

@@ -136,14 +136,22 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
   }
   __syncthreads();
 
-  const int E = rowptr[n];
+  // LDS reads land in VGPRs; values that are wave-uniform are moved to
+  // SGPRs so the gain addressing stays scalar (no per-lane 64-bit addresses,
+  // no waterfall loops around the buffer loads)
+  const int E = __builtin_amdgcn_readfirstlane(rowptr[n]);
   const double* G = P.gains + 9 * P.gain_off[f];
+  // the formation's 9 planes through one buffer resource: a lane's nine
+  // loads share one VGPR offset (plane k at SGPR offset 8kE); a lane with no
+  // edge reads past num_records, which returns 0
+  const __amdgpu_buffer_rsrc_t grs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 9 * E * 8, 0x00020000);
   const acl_cntrl_gains_t g = P.g;
   const acl_safety_params_t sp = P.s;
   const double thr_hi = sp.d_avoid_thresh * (1.0 + 0x1p-40);
   const double thr2hi = thr_hi * thr_hi;
   for (int v = wave; v < n; v += kCtlWaves) {
-    const int i = myi[v];
+    const int i = __builtin_amdgcn_readfirstlane(myi[v]);
     // the vehicle's values are wave-uniform: held in SGPRs
     const double* gv = P.vel + ((size_t)b * n + v) * 3;
     const double vel0 = uni(gv[0]), vel1 = uni(gv[1]), vel2 = uni(gv[2]);
@@ -151,20 +159,24 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
     const double pix = uni(p[3 * i]), piy = uni(p[3 * i + 1]), piz = uni(p[3 * i + 2]);
     const double Ni = pix * pix + piy * piy, Nzi = piz * piz;
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-    int ebase = rowptr[i];
+    int ebase = __builtin_amdgcn_readfirstlane(rowptr[i]);
 #pragma unroll 1
     for (int c = 0; c < NW; ++c) {
-      const unsigned long long rowbits = adjF[i * NW + c];
+      const unsigned long long rowbits = uni_u64(adjF[i * NW + c]);
       const bool has = (rowbits >> lane) & 1ull;
       const int e = ebase + __popcll(rowbits & ((1ull << lane) - 1ull));
       ebase += __popcll(rowbits);
+      const int voff = has ? e * 8 : 0x40000000;
       if (has) {
         // tolerance-based parity (1e-5 relative): fused multiply-adds and the
         // refined fast sqrt / quotient (common.h) are allowed here
 #pragma clang fp contract(fast)
         double A[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) A[k] = __builtin_nontemporal_load(G + (size_t)k * E + e);
+        for (int k = 0; k < 9; ++k) {
+          const auto raw = __builtin_amdgcn_raw_buffer_load_b64(grs, voff, k * E * 8, 2 /* nt */);
+          __builtin_memcpy(&A[k], &raw, 8);
+        }
         const int j = lane + 64 * c;
         const int uu = uniform ? Pt[j] : rows[(size_t)v * n + j];
         const double q0 = q[3 * uu] - qv0, q1 = q[3 * uu + 1] - qv1, q2 = q[3 * uu + 2] - qv2;
