@@ -30,15 +30,19 @@
  * Index width. The reference uses uint8_t vehicle indices
  * (utils.h:25-30, vehidx_t), so N <= 255. The ABI widens indices to
  * uint16_t; for N <= 255 the semantics are identical ("who == -1" casts to
- * 0xFFFF here instead of 0xFF).
+ * 0xFFFF here instead of 0xFF). acl_solve_batch accepts N <= 512 (config
+ * C4 is N = 500): N <= 128 runs the LDS-resident auction kernel, larger N
+ * the kernel whose CBAA tables live in the workspace.
  *
  * Errors. The reference has no error channel (asserts compiled out in
  * Release, aclswarm/CMakeLists.txt:7-10); an invalid auction is a flag
  * (auctioneer.cpp:283-292). Here: argument errors return acl_status_t != 0,
  * per-swarm outcomes are flags in acl_swarm_status_t.
  *
- * Concurrency. All device entry points are stream-ordered on the hipStream_t
- * passed as `void* stream` (NULL = default stream) and never synchronize.
+ * Concurrency. acl_solve_batch is stream-ordered on the hipStream_t passed as
+ * `void* stream` (NULL = default stream) and never synchronizes.
+ * acl_admm_solve_batch synchronizes that stream between ADMM iterations (its
+ * iteration control reads per-formation convergence flags back).
  */
 #ifndef ACLSWARM_AMD_H
 #define ACLSWARM_AMD_H
@@ -162,13 +166,12 @@ typedef struct {
  *   who     [B][n][n]  optional final CBAA tables, vehicle rows (NULL ok);
  *                      0xFFFF = unassigned (who == -1)
  *   workspace          device scratch of acl_solve_workspace_bytes(n, B)
- *                      bytes (required when do_control): the auction kernel
- *                      hands each vehicle's adopted assignment to the
- *                      control kernel through it.
- * The call enqueues, per chunk of swarms, the auction kernel on `stream` and
- * the control kernel on an internal second stream (fork/join with events),
- * so one chunk's gain stream overlaps the next chunk's auction. Completion
- * is ordered on `stream`.
+ *                      bytes (required): the auction kernel hands each
+ *                      vehicle's adopted assignment to the control kernels
+ *                      through it; for n > 128 it also holds the CBAA tables.
+ * The call enqueues three kernels on `stream`: the auction over all B swarms,
+ * the gain kernel (DistCntrl, saturation, the collision test) and the
+ * collision-avoidance kernel for the vehicles the gain kernel listed.
  */
 typedef struct {
   int32_t B;
@@ -190,7 +193,7 @@ typedef struct {
   int32_t do_control; /* 0: auction only */
 } acl_solve_args_t;
 
-/* Largest n the batched solve kernel accepts. */
+/* Largest n acl_solve_batch accepts (512). */
 int32_t acl_max_vehicles(void);
 
 /* Bytes of device workspace acl_solve_batch needs for B swarms of n. */
