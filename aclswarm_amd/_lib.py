@@ -30,6 +30,7 @@ EXPORTS = (
     "acl_default_cntrl_gains", "acl_default_safety_params", "acl_default_admm_params",
     "acl_max_vehicles", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
     "acl_pack_gains", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
+    "acl_control_batch", "acl_write_assignment_log", "acl_read_assignment_log",
     "acl_malloc", "acl_free", "acl_memcpy_h2d", "acl_memcpy_d2h", "acl_memset",
     "acl_stream_synchronize", "acl_last_error",
 )
@@ -67,7 +68,16 @@ class SolveArgs(ct.Structure):
                 ("status", ct.c_void_p), ("u", ct.c_void_p), ("u_safe", ct.c_void_p),
                 ("ca_flag", ct.c_void_p), ("who", ct.c_void_p), ("workspace", ct.c_void_p),
                 ("cntrl", CntrlGains), ("safety", SafetyParams),
-                ("early_exit", ct.c_int32), ("do_control", ct.c_int32)]
+                ("early_exit", ct.c_int32), ("do_control", ct.c_int32),
+                ("align_Rt", ct.c_void_p)]
+
+
+class ControlArgs(ct.Structure):
+    """acl_control_args_t (DistCntrl + Safety for given assignments)."""
+    _fields_ = [("B", ct.c_int32), ("fidx", ct.c_void_p), ("q", ct.c_void_p),
+                ("vel", ct.c_void_p), ("P", ct.c_void_p), ("u", ct.c_void_p),
+                ("u_safe", ct.c_void_p), ("ca_flag", ct.c_void_p), ("status", ct.c_void_p),
+                ("workspace", ct.c_void_p), ("cntrl", CntrlGains), ("safety", SafetyParams)]
 
 
 _lib = None
@@ -100,6 +110,12 @@ def lib():
     L.acl_pack_gains.restype = ct.c_int
     L.acl_admm_solve_batch.argtypes = [I32, I32, VP, VP, VP, VP, ct.POINTER(AdmmParams), VP]
     L.acl_admm_solve_batch.restype = ct.c_int
+    L.acl_control_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(ControlArgs), VP]
+    L.acl_control_batch.restype = ct.c_int
+    L.acl_write_assignment_log.argtypes = [ct.c_char_p, I32, VP, VP, VP, VP, VP, VP]
+    L.acl_write_assignment_log.restype = ct.c_int
+    L.acl_read_assignment_log.argtypes = [ct.c_char_p, ct.POINTER(I32), VP, VP, VP, VP, VP, VP]
+    L.acl_read_assignment_log.restype = ct.c_int
     L.acl_device_count.restype = I32
     L.acl_set_device.argtypes = [I32]
     L.acl_set_device.restype = ct.c_int

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <vector>
 #include <cstring>
 #include <string>
 
@@ -77,6 +78,93 @@ extern "C" acl_status_t acl_pack_gains(int32_t n, const uint8_t* adj, const doub
       ++e;
     }
   return ACL_OK;
+}
+
+// ---- Auctioneer::logAssignment records (auctioneer.cpp:577-597) ----------
+
+namespace {
+// aligned = R p + t with the z row identity, in alignFormation's operation
+// order (the same expression the price kernels evaluate)
+void aligned_points(int n, const double* p, const double* Rt, double* out) {
+  for (int j = 0; j < n; ++j) {
+    const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
+    out[3 * j] = ((Rt[0] * px + Rt[1] * py) + 0.0 * pz) + Rt[4];
+    out[3 * j + 1] = ((Rt[2] * px + Rt[3] * py) + 0.0 * pz) + Rt[5];
+    out[3 * j + 2] = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
+  }
+}
+}  // namespace
+
+extern "C" acl_status_t acl_write_assignment_log(const char* path, int32_t n, const double* q,
+                                                 const uint8_t* adj, const uint16_t* lastP,
+                                                 const double* p, const double* Rt,
+                                                 const uint16_t* P) {
+  if (!path || n < 1 || n > 255 || !q || !adj || !lastP || !p || !Rt || !P)
+    return acl__set_error("acl_write_assignment_log: bad argument (n must be 1..255)");
+  std::vector<double> al(3 * (size_t)n), col(3 * (size_t)n);
+  aligned_points(n, p, Rt, al.data());
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return acl__set_error("acl_write_assignment_log: cannot open file");
+  auto colmajor = [&](const double* rm) {  // PtsMat is n x 3 column-major
+    for (int c = 0; c < 3; ++c)
+      for (int i = 0; i < n; ++i) col[(size_t)c * n + i] = rm[3 * i + c];
+    std::fwrite(col.data(), sizeof(double), col.size(), f);
+  };
+  auto perm = [&](const uint16_t* x) {
+    std::vector<uint8_t> b(n);
+    for (int i = 0; i < n; ++i) b[i] = (uint8_t)x[i];
+    std::fwrite(b.data(), 1, b.size(), f);
+  };
+  const uint8_t n8 = (uint8_t)n;
+  std::fwrite(&n8, 1, 1, f);
+  colmajor(q);
+  std::fwrite(adj, 1, (size_t)n * n, f);
+  perm(lastP);
+  colmajor(p);
+  colmajor(al.data());
+  perm(P);
+  const bool ok = std::ferror(f) == 0;
+  std::fclose(f);
+  return ok ? ACL_OK : acl__set_error("acl_write_assignment_log: write failed");
+}
+
+extern "C" acl_status_t acl_read_assignment_log(const char* path, int32_t* n_out, double* q,
+                                                uint8_t* adj, uint16_t* lastP, double* p,
+                                                double* aligned, uint16_t* P) {
+  if (!path || !n_out) return acl__set_error("acl_read_assignment_log: bad argument");
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return acl__set_error("acl_read_assignment_log: cannot open file");
+  uint8_t n8 = 0;
+  if (std::fread(&n8, 1, 1, f) != 1) {
+    std::fclose(f);
+    return acl__set_error("acl_read_assignment_log: truncated file");
+  }
+  const int n = n8;
+  *n_out = n;
+  if (!q || !adj || !lastP || !p || !aligned || !P) {
+    std::fclose(f);
+    return ACL_OK;  // size query
+  }
+  std::vector<double> col(3 * (size_t)n);
+  bool ok = true;
+  auto rowmajor = [&](double* rm) {
+    ok = ok && std::fread(col.data(), sizeof(double), col.size(), f) == col.size();
+    for (int c = 0; c < 3; ++c)
+      for (int i = 0; i < n; ++i) rm[3 * i + c] = col[(size_t)c * n + i];
+  };
+  auto perm = [&](uint16_t* x) {
+    std::vector<uint8_t> b(n);
+    ok = ok && std::fread(b.data(), 1, b.size(), f) == b.size();
+    for (int i = 0; i < n; ++i) x[i] = b[i];
+  };
+  rowmajor(q);
+  ok = ok && std::fread(adj, 1, (size_t)n * n, f) == (size_t)n * n;
+  perm(lastP);
+  rowmajor(p);
+  rowmajor(aligned);
+  perm(P);
+  std::fclose(f);
+  return ok ? ACL_OK : acl__set_error("acl_read_assignment_log: truncated file");
 }
 
 // ---- device memory -------------------------------------------------------

@@ -405,6 +405,51 @@ __global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
   }
 }
 
+// acl_control_batch's hand-off: P must be a permutation (else BAD_INPUT and
+// zero commands, as for the auction's P_in); the inverse assignment is the
+// shared row the gain kernel reads.
+__global__ void __launch_bounds__(256) control_prep_kernel(const CtlParams P,
+                                                           const uint16_t* Pg) {
+  __shared__ unsigned long long seen[kMaxNWide / 64];
+  __shared__ int bad;
+  const int n = P.n, b = blockIdx.x, tid = threadIdx.x;
+  if (tid < kMaxNWide / 64) seen[tid] = 0ull;
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  uint16_t* wsPt = const_cast<uint16_t*>(P.wsPt) + (size_t)b * n;
+  for (int v = tid; v < n; v += 256) {
+    const unsigned pv = Pg[(size_t)b * n + v];
+    if (pv >= (unsigned)n) {
+      bad = 1;
+    } else {
+      const unsigned long long bit = 1ull << (pv & 63);
+      if (atomicOr(&seen[pv >> 6], bit) & bit) bad = 1;
+      wsPt[pv] = (uint16_t)v;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const_cast<uint8_t*>(P.wsMode)[b] = 0;
+    acl_swarm_status_t st = {};
+    st.flags = bad ? ACL_SWARM_BAD_INPUT : 0u;
+    P.status[b] = st;
+  }
+  if (bad) {
+    for (int k = tid; k < 3 * n; k += 256) {
+      P.u[(size_t)b * n * 3 + k] = 0.0;
+      if (P.u_safe) P.u_safe[(size_t)b * n * 3 + k] = 0.0;
+    }
+    if (P.ca_flag)
+      for (int v = tid; v < n; v += 256) P.ca_flag[(size_t)b * n + v] = 0;
+  }
+}
+
+hipError_t launch_control_prep(const CtlParams& P, const uint16_t* Pgiven, int nb,
+                               hipStream_t stream) {
+  hipLaunchKernelGGL(control_prep_kernel, dim3(nb), dim3(256), 0, stream, P, Pgiven);
+  return hipGetLastError();
+}
+
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream) {
   if (which == 0) {
     const GainLayout L = make_gain_layout(P.n);

@@ -62,6 +62,7 @@ struct SolveParams {
   double* u_safe;
   uint8_t* ca_flag;
   uint16_t* who;
+  double* align_Rt;
   acl_cntrl_gains_t g;
   acl_safety_params_t s;
   int early_exit;
@@ -101,6 +102,11 @@ enum { M_BAD = 0, M_NONFIN = 1, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 
 // [P.b0, P.b0 + nb) (DistCntrl::compute, saturation, the collision test),
 // 1 the collisionAvoidance kernel over the listed vehicles.
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream);
+
+// Hand-off of given assignments to the control kernels (acl_control_batch):
+// permutation check, inverse assignment, status.
+hipError_t launch_control_prep(const CtlParams& P, const uint16_t* Pgiven, int nb,
+                               hipStream_t stream);
 
 // The n > 128 auction kernel (solve_wide.hip).
 hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream);

@@ -326,6 +326,8 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
     o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
   }
   __syncthreads();
+  if (P.align_Rt)
+    for (int k = tid; k < 6 * n; k += kBlock) P.align_Rt[(size_t)b * n * 6 + k] = out[k];
   stamp(P, b, tid, 2);
 
   // ---------------- phase 2: prices ---------------------------------------
@@ -677,7 +679,7 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   P.p = F->p; P.adj = F->adj; P.gains = F->gains; P.gain_off = F->gain_off;
   P.fidx = a->fidx; P.q = a->q; P.vel = a->vel; P.P_in = a->P_in; P.P_out = a->P_out;
   P.status = a->status; P.u = a->u; P.u_safe = a->u_safe; P.ca_flag = a->ca_flag;
-  P.who = a->who; P.g = a->cntrl; P.s = a->safety;
+  P.who = a->who; P.align_Rt = a->align_Rt; P.g = a->cntrl; P.s = a->safety;
   P.early_exit = a->early_exit; P.do_control = a->do_control;
   P.ws = (unsigned char*)a->workspace;
   P.W = ws_layout(n, a->B);
@@ -721,6 +723,44 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
     kt_record(1 + which, 0, s);
     e = launch_control(C, a->B, which, s);
     kt_record(1 + which, 1, s);
+    if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+  }
+  return ACL_OK;
+}
+
+extern "C" acl_status_t acl_control_batch(const acl_formations_t* F, const acl_control_args_t* a,
+                                          void* stream) {
+  using namespace acl_amd;
+  if (!F || !a) return acl__set_error("acl_control_batch: null argument");
+  const int n = F->n;
+  if (n < 1 || n > kMaxNWide) return acl__set_error("acl_control_batch: n out of range [1, 512]");
+  if (a->B < 0) return acl__set_error("acl_control_batch: B < 0");
+  if (a->B == 0) return ACL_OK;
+  if (!F->p || !F->adj || !F->gains || !F->gain_off || !a->fidx || !a->q || !a->vel || !a->P ||
+      !a->status || !a->workspace)
+    return acl__set_error("acl_control_batch: required pointer is NULL");
+  const WsLayout W = ws_layout(n, a->B);
+  unsigned char* ws = (unsigned char*)a->workspace;
+  CtlParams C;
+  C.n = n; C.B = a->B; C.b0 = 0;
+  C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
+  C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P;
+  C.status = a->status;
+  C.u = a->u ? a->u : reinterpret_cast<double*>(ws + W.u);
+  C.u_safe = a->u_safe; C.ca_flag = a->ca_flag;
+  C.wsPt = reinterpret_cast<const uint16_t*>(ws + W.pt);
+  C.wsMode = ws + W.mode;
+  C.wsRows = reinterpret_cast<const uint16_t*>(ws + W.rows);
+  C.ca_list = reinterpret_cast<unsigned*>(ws + W.calist);
+  C.ca_count = reinterpret_cast<unsigned*>(ws + W.cacount);
+  C.g = a->cntrl; C.s = a->safety;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
+    return acl__set_error("hipMemsetAsync failed");
+  hipError_t e = launch_control_prep(C, a->P, a->B, s);
+  if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+  for (int which = 0; which < 2; ++which) {
+    e = launch_control(C, a->B, which, s);
     if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
   }
   return ACL_OK;

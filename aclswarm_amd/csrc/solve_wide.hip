@@ -288,6 +288,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
   }
   __syncthreads();
+  if (P.align_Rt)
+    for (int k = tid; k < 6 * n; k += kWBlock) P.align_Rt[(size_t)b * n * 6 + k] = out[k];
 
   // ---------------- phase 2: prices, in 64 x 64 tiles -----------------------
   // each tile computed once, written row-major to C and, through LDS,

@@ -91,7 +91,7 @@ def workspace(n, B, device):
 
 
 def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
-          do_control=True, want_who=False, out=None, stream=None):
+          do_control=True, want_who=False, want_align=False, out=None, stream=None):
     """Run acl_solve_batch for B = q.shape[0] swarms. All tensors on device.
 
     fidx [B] int32, q/vel [B][n][3] f64, P_in [B][n] int16 (uint16 bits).
@@ -111,6 +111,8 @@ def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
         }
         if want_who:
             out["who"] = torch.empty((B, n, n), dtype=torch.int16, device=dev)
+        if want_align:
+            out["align_Rt"] = torch.empty((B, n, 6), dtype=torch.float64, device=dev)
     a = L.SolveArgs()
     a.B = B
     a.fidx = fidx.data_ptr(); a.q = q.data_ptr(); a.vel = vel.data_ptr()
@@ -120,6 +122,7 @@ def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
     a.u_safe = out["u_safe"].data_ptr() if out.get("u_safe") is not None else None
     a.ca_flag = out["ca_flag"].data_ptr() if out.get("ca_flag") is not None else None
     a.who = out["who"].data_ptr() if out.get("who") is not None else None
+    a.align_Rt = out["align_Rt"].data_ptr() if out.get("align_Rt") is not None else None
     a.workspace = workspace(n, B, dev).data_ptr()
     a.cntrl = cntrl or L.default_gains()
     a.safety = safety or L.default_safety()
@@ -162,3 +165,67 @@ def admm_design(pts, adj, params=None, stream=None):
                                      iters.data_ptr(), ct.byref(prm), ct.c_void_p(stream)),
             "acl_admm_solve_batch")
     return out.transpose(1, 2), iters
+
+
+def control(table, fidx, q, vel, P, cntrl=None, safety=None, stream=None):
+    """acl_control_batch: DistCntrl::compute + Safety for B swarms with given
+    assignments P [B][n] (int16 holding uint16 bits). Returns u, u_safe,
+    ca_flag, status (device tensors)."""
+    lib = L.lib()
+    B, n = int(q.shape[0]), table.n
+    dev = q.device
+    out = {
+        "u": torch.empty((B, n, 3), dtype=torch.float64, device=dev),
+        "u_safe": torch.empty((B, n, 3), dtype=torch.float64, device=dev),
+        "ca_flag": torch.empty((B, n), dtype=torch.uint8, device=dev),
+        "status": torch.empty((B, 16), dtype=torch.uint8, device=dev),
+    }
+    a = L.ControlArgs()
+    a.B = B
+    a.fidx = fidx.data_ptr(); a.q = q.data_ptr(); a.vel = vel.data_ptr(); a.P = P.data_ptr()
+    a.u = out["u"].data_ptr(); a.u_safe = out["u_safe"].data_ptr()
+    a.ca_flag = out["ca_flag"].data_ptr(); a.status = out["status"].data_ptr()
+    a.workspace = workspace(n, B, dev).data_ptr()
+    a.cntrl = cntrl or L.default_gains()
+    a.safety = safety or L.default_safety()
+    F = table.struct()
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    L.check(lib.acl_control_batch(ct.byref(F), ct.byref(a), ct.c_void_p(stream)),
+            "acl_control_batch")
+    return out
+
+
+def write_assignment_log(path, q, adj, lastP, p, align_Rt, P):
+    """Auctioneer::logAssignment's binary record (auctioneer.cpp:577-597),
+    host arrays: q, p [n][3]; adj [n][n] (adj[i][j] = adjmat(i,j)); lastP, P
+    [n]; align_Rt [6] (the logging vehicle's alignment)."""
+    lib = L.lib()
+    q = np.ascontiguousarray(q, np.float64)
+    p = np.ascontiguousarray(p, np.float64)
+    adj_cm = np.ascontiguousarray(np.asarray(adj, np.uint8).T)
+    lastP = np.ascontiguousarray(lastP, np.uint16)
+    P = np.ascontiguousarray(P, np.uint16)
+    Rt = np.ascontiguousarray(align_Rt, np.float64)
+    L.check(lib.acl_write_assignment_log(str(path).encode(), q.shape[0], q.ctypes.data,
+                                         adj_cm.ctypes.data, lastP.ctypes.data, p.ctypes.data,
+                                         Rt.ctypes.data, P.ctypes.data), "write_assignment_log")
+
+
+def read_assignment_log(path):
+    """Reads a logAssignment record: dict of q, adj, lastP, p, aligned, P."""
+    lib = L.lib()
+    n = ct.c_int32(0)
+    L.check(lib.acl_read_assignment_log(str(path).encode(), ct.byref(n), None, None, None,
+                                        None, None, None), "read_assignment_log")
+    n = n.value
+    r = {"q": np.zeros((n, 3)), "adj_cm": np.zeros((n, n), np.uint8),
+         "lastP": np.zeros(n, np.uint16), "p": np.zeros((n, 3)),
+         "aligned": np.zeros((n, 3)), "P": np.zeros(n, np.uint16)}
+    nn = ct.c_int32(0)
+    L.check(lib.acl_read_assignment_log(str(path).encode(), ct.byref(nn), r["q"].ctypes.data,
+                                        r["adj_cm"].ctypes.data, r["lastP"].ctypes.data,
+                                        r["p"].ctypes.data, r["aligned"].ctypes.data,
+                                        r["P"].ctypes.data), "read_assignment_log")
+    r["adj"] = r.pop("adj_cm").T.copy()
+    return r

@@ -191,6 +191,11 @@ typedef struct {
   int32_t early_exit; /* 1: stop at the first fixed point (bit-exact), 0: run
                          all 2N rounds like the reference */
   int32_t do_control; /* 0: auction only */
+  double* align_Rt;   /* [B][n][6] optional (NULL ok): vehicle v's 2-D
+                         alignment of the formation to its neighbourhood,
+                         R row-major 2x2 then t (Auctioneer::alignFormation,
+                         auctioneer.cpp:347-415); the `aligned` points of
+                         logAssignment are R p + t (z unchanged) */
 } acl_solve_args_t;
 
 /* Largest n acl_solve_batch accepts (512). */
@@ -213,6 +218,50 @@ acl_status_t acl_pack_adjacency(int32_t n, const uint8_t* adj_colmajor,
  * (E = acl_count_edges). */
 acl_status_t acl_pack_gains(int32_t n, const uint8_t* adj_colmajor,
                             const double* gains_colmajor, double* out_planes);
+
+/* ---- DistCntrl + Safety for given assignments (no auction) ---------------
+ * DistCntrl::setAssignment + compute (distcntrl.cpp:38-102) and
+ * Safety::cmdinCb/collisionAvoidance for B swarms whose assignment P is
+ * already known (e.g. between auto-auctions, coordination_ros.cpp:370-378).
+ * P [B][n] vehicle -> formation point; a P that is not a permutation gives
+ * status BAD_INPUT and zero commands. status [B] gets flags (BAD_INPUT,
+ * CA_ACTIVE) and n_ca; the other fields are zero. Device pointers; workspace
+ * of acl_solve_workspace_bytes(n, B). Stream-ordered. */
+typedef struct {
+  int32_t B;
+  const int32_t* fidx;
+  const double* q;
+  const double* vel;
+  const uint16_t* P;
+  double* u;
+  double* u_safe;
+  uint8_t* ca_flag;
+  acl_swarm_status_t* status;
+  void* workspace;
+  acl_cntrl_gains_t cntrl;
+  acl_safety_params_t safety;
+} acl_control_args_t;
+
+acl_status_t acl_control_batch(const acl_formations_t* formations,
+                               const acl_control_args_t* args, void* stream);
+
+/* ---- Auctioneer::logAssignment files (auctioneer.cpp:577-597) -----------
+ * The reference's binary record, byte for byte (reader:
+ * matlab/Helpers/read_alignment.m:1-19): u8 n, q f64[n*3] column-major,
+ * adjmat u8[n*n] column-major, lastP u8[n], p f64[n*3] column-major,
+ * aligned f64[n*3] column-major, P u8[n]. Host pointers; q and p are
+ * [n][3] row-major here, adj is the column-major AdjMat, aligned is computed
+ * from align_Rt exactly as alignFormation does (R p + t, z row identity).
+ * n <= 255 (the format's u8 count). */
+acl_status_t acl_write_assignment_log(const char* path, int32_t n, const double* q,
+                                      const uint8_t* adj_colmajor, const uint16_t* lastP,
+                                      const double* p, const double* align_Rt,
+                                      const uint16_t* P);
+/* Reads a record back: *n first (pass NULL buffers to query n), then the
+ * arrays in the layouts acl_write_assignment_log takes (aligned [n][3]). */
+acl_status_t acl_read_assignment_log(const char* path, int32_t* n, double* q,
+                                     uint8_t* adj_colmajor, uint16_t* lastP, double* p,
+                                     double* aligned, uint16_t* P);
 
 /* ---- ADMM formation-gain design (admm::Solver::solve, solver.cpp:28-79) -
  * F formations of n points: pts [F][3][n] column-major 3 x n per formation

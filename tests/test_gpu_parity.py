@@ -269,3 +269,73 @@ def test_n500_config_c4(cuda):
     gpu = _gpu_solve(*args)
     ref = _oracle(*args)
     _compare(gpu, ref)
+
+
+def test_control_batch_given_assignment(cuda):
+    """acl_control_batch (DistCntrl + Safety with given P, no auction) against
+    the oracle's DistCntrl::compute / saturation / collisionAvoidance, and a
+    non-permutation P -> BAD_INPUT."""
+    import torch
+    from aclswarm_amd import engine
+    P20, A20 = H.simform("simform20_fc")
+    rng = np.random.RandomState(21)
+    pts = [P20[0, 0], P20[1, 1]]
+    adjs = [A20[0], A20[1]]
+    gains = [H.synth_gains(rng, a, scale=1.0) for a in adjs]
+    B, n = 12, 20
+    fidx = np.arange(B) % 2
+    q = np.stack([H.dense_positions(rng, n, 6.0 + b) for b in range(B)])
+    vel = rng.normal(0, 0.3, (B, n, 3))
+    P = np.stack([H.random_perm(rng, n) for _ in range(B)])
+    P[3, 4] = P[3, 5]                                   # not a permutation
+    dev = torch.device("cuda:0")
+    T = engine.FormationTable.from_host(pts, adjs, gains, device=dev)
+    out = engine.control(T, torch.from_numpy(fidx.astype(np.int32)).to(dev),
+                         torch.from_numpy(q).to(dev), torch.from_numpy(vel).to(dev),
+                         torch.from_numpy(P.astype(np.uint16).view(np.int16)).to(dev))
+    torch.cuda.synchronize()
+    u = out["u"].cpu().numpy(); us = out["u_safe"].cpu().numpy()
+    ca = out["ca_flag"].cpu().numpy()
+    st = engine.status_to_numpy(out["status"])
+    assert st["flags"][3] & 0x10 and not np.any(us[3])
+    nca = 0
+    for b in range(B):
+        if b == 3:
+            continue
+        f = fidx[b]
+        Pt = np.argsort(P[b]).astype(np.uint16)
+        for v in range(n):
+            ur = O.control(v, q[b], vel[b, v], Pt, adjs[f], gains[f], pts[f])
+            sr, mod = O.collision_avoidance(v, q[b], O.saturate(ur))
+            np.testing.assert_allclose(u[b, v], ur, rtol=U_RTOL, atol=U_RTOL)
+            np.testing.assert_allclose(us[b, v], sr, rtol=U_RTOL, atol=U_RTOL)
+            assert bool(ca[b, v]) == mod
+            nca += mod
+        assert int(st["n_ca"][b]) == int(ca[b].sum())
+    assert nca > 10
+
+
+def test_align_rt_output(cuda):
+    """solve's optional align_Rt is each vehicle's Auctioneer::alignFormation
+    (R, t), bit-exact against the oracle (the logAssignment `aligned`)."""
+    import torch
+    from aclswarm_amd import engine
+    P20, A20 = H.simform("simform20_nc")
+    rng = np.random.RandomState(5)
+    pts = [P20[0, 0]]
+    adjs = [A20[0]]
+    gains = [H.synth_gains(rng, A20[0])]
+    for n_, (pts_, adjs_, gains_) in ((20, (pts, adjs, gains)),):
+        B = 6
+        q = np.stack([H.random_positions(rng, n_, 20.0) for _ in range(B)])
+        Pin = np.stack([H.random_perm(rng, n_) for _ in range(B)])
+        dev = torch.device("cuda:0")
+        T = engine.FormationTable.from_host(pts_, adjs_, gains_, device=dev)
+        out = engine.solve(T, torch.zeros(B, dtype=torch.int32, device=dev),
+                           torch.from_numpy(q).to(dev), torch.zeros((B, n_, 3), dtype=torch.float64, device=dev),
+                           torch.from_numpy(Pin.view(np.int16)).to(dev), want_align=True)
+        torch.cuda.synchronize()
+        Rt = out["align_Rt"].cpu().numpy()
+        for b in range(B):
+            _, Rt_ref = O.prices(q[b], pts_[0], adjs_[0], Pin[b])
+            np.testing.assert_array_equal(Rt[b], Rt_ref)
