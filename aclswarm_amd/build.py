@@ -11,6 +11,10 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "lib", "libaclswarm_amd.so")
+ROOT = os.path.dirname(HERE)
+# C++ facade exerciser (include/aclswarm_amd.hpp), run by tests/test_gpu_facade.py
+DRIVER_SRC = os.path.join(ROOT, "tests", "facade_driver.cpp")
+DRIVER = os.path.join(HERE, "lib", "libfacade_driver.so")
 SOURCES = ["solve.hip", "solve_wide.hip", "control.hip", "admm.hip", "api.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
@@ -26,8 +30,26 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+def build_driver(force=False, verbose=False):
+    """g++ against the library, found next to the binary ($ORIGIN)."""
+    deps = [DRIVER_SRC, OUT, os.path.join(ROOT, "include", "aclswarm_amd.hpp")]
+    if not force and os.path.exists(DRIVER) and all(
+            os.path.getmtime(d) <= os.path.getmtime(DRIVER) for d in deps):
+        return DRIVER
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fPIC", "-shared",
+           "-I" + os.path.join(ROOT, "include"), DRIVER_SRC,
+           "-L" + os.path.dirname(OUT), "-laclswarm_amd", "-Wl,-rpath,$ORIGIN",
+           "-o", DRIVER + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(DRIVER + ".tmp", DRIVER)
+    return DRIVER
+
+
 def build(force=False, verbose=False):
     if not force and not _stale():
+        build_driver(force, verbose)
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     cmd = [HIPCC] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", OUT + ".tmp"]
@@ -35,6 +57,7 @@ def build(force=False, verbose=False):
         print(" ".join(cmd))
     subprocess.check_call(cmd)
     os.replace(OUT + ".tmp", OUT)
+    build_driver(True, verbose)
     return OUT
 
 

@@ -94,3 +94,16 @@ def test_solve_batch_argument_errors_without_gpu():
 def test_status_record_is_16_bytes():
     from aclswarm_amd import _lib as L
     assert L.STATUS_DTYPE.itemsize == 16
+
+
+def test_cpp_facade_compiles_and_exports():
+    """include/aclswarm_amd.hpp (Auctioneer / DistCntrl / admm::Solver facade)
+    compiles warning-free as C++17 and the built exerciser exports facade_run."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.check_call(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror",
+                           "-I" + os.path.join(root, "include"),
+                           os.path.join(root, "tests", "facade_driver.cpp")])
+    from aclswarm_amd import build
+    so = build.build_driver()
+    assert hasattr(ct.CDLL(so), "facade_run")

@@ -1,0 +1,119 @@
+"""The C++ facade (include/aclswarm_amd.hpp) driven the way the reference's
+CoordinationROS drives its objects: one Auctioneer and one DistCntrl per
+vehicle, one admm::Solver (tests/facade_driver.cpp, built into
+aclswarm_amd/lib/libfacade_driver.so and loaded here by ctypes).
+
+Checked against the CPU restatement: each vehicle adopts its own final CBAA
+table exactly as auctioneer.cpp:250-295 does (bit-exact), DistCntrl::compute
+within 1e-5 relative, and the ADMM gains of test_admm.cpp's cases within the
+reference test's own tolerance.
+"""
+import ctypes as ct
+import os
+
+import numpy as np
+import pytest
+
+import helpers as H
+import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+U_RTOL = 1e-5  # north_star: control commands within 1e-5 relative (fp64)
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "aclswarm_amd", "lib", "libfacade_driver.so")
+
+
+def _run(tmp_path, p, adj, gains, q, vel, P_in, pts=None, adjf=None):
+    n = p.shape[0]
+    m = 0 if pts is None else pts.shape[0]
+    fin, fout = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
+    with open(fin, "wb") as f:
+        f.write(np.int32(n).tobytes())
+        f.write(np.asfortranarray(p, np.float64).tobytes(order="F"))
+        f.write(np.asarray(adj, np.uint8).tobytes(order="F"))
+        f.write(np.asarray(gains, np.float64).tobytes(order="F"))
+        f.write(np.asarray(q, np.float64).tobytes(order="F"))
+        f.write(np.ascontiguousarray(vel, np.float64).tobytes())
+        f.write(np.asarray(P_in, np.uint8).tobytes())
+        f.write(np.int32(m).tobytes())
+        if m:
+            f.write(np.ascontiguousarray(pts, np.float64).tobytes())  # 3 x m column-major
+            f.write(np.asarray(adjf, np.float64).tobytes(order="F"))
+    if not os.path.exists(LIB):
+        raise RuntimeError(f"{LIB} missing: run python -m aclswarm_amd.build")
+    lib = ct.CDLL(LIB)
+    lib.facade_run.argtypes = [ct.c_char_p, ct.c_char_p]
+    assert lib.facade_run(fin.encode(), fout.encode()) == 0
+    raw = open(fout, "rb").read()
+    o = 0
+    P, inv, calls = [], [], []
+    for _ in range(n):
+        P.append(np.frombuffer(raw, np.uint8, n, o)); o += n
+        inv.append(raw[o]); calls.append(raw[o + 1]); o += 2
+    u = np.frombuffer(raw, np.float64, 3 * n, o).reshape(n, 3); o += 24 * n
+    its = np.frombuffer(raw, np.int32, 2, o); o += 8
+    A = np.frombuffer(raw, np.float64, 9 * m * m, o).reshape(3 * m, 3 * m, order="F")
+    return dict(P=np.array(P), invalid=np.array(inv), calls=np.array(calls), u=u,
+                iters=its, A=A)
+
+
+def _expect(p, adj, gains, q, vel, P_in):
+    """Per vehicle: its final table (oracle), adopted as auctioneer.cpp:250-295
+    does after setFormation (adopt when valid, flag when not)."""
+    n = p.shape[0]
+    r = O.solve(q, np.zeros_like(q), p, adj, gains, np.asarray(P_in, np.uint16))
+    P, inv = [], []
+    for v in range(n):
+        who = r["who"][v].astype(np.int64)
+        if np.array_equal(np.sort(who), np.arange(n)):
+            Pv = np.empty(n, np.int64); Pv[who] = np.arange(n)
+            P.append(Pv); inv.append(0)
+        else:
+            P.append(np.arange(n)); inv.append(1)   # setFormation reset P to identity
+    u = np.stack([O.control(v, q, vel[v], np.argsort(P[v]).astype(np.uint16), adj, gains, p)
+                  for v in range(n)])
+    return np.array(P), np.array(inv), u
+
+
+def _check(got, p, adj, gains, q, vel, P_in):
+    P, inv, u = _expect(p, adj, gains, q, vel, P_in)
+    np.testing.assert_array_equal(got["invalid"], inv)
+    np.testing.assert_array_equal(got["calls"], 1 - inv)
+    for v in range(p.shape[0]):
+        if not inv[v]:
+            np.testing.assert_array_equal(got["P"][v], P[v], err_msg=f"vehicle {v}")
+    err = np.abs(got["u"] - u) / np.maximum(np.abs(u), 1.0)
+    assert err.max() <= U_RTOL, err.max()
+
+
+def test_facade_swarm6_and_test_admm(tmp_path):
+    """formations.yaml swarm6_3d with its given gains from a perturbed
+    start.sh grid, plus admm::Solver on test_admm.cpp's first case."""
+    pts, adj, gains, q0 = H.swarm6()
+    rng = np.random.RandomState(61)
+    q = q0 + rng.normal(0, 0.3, q0.shape)
+    vel = rng.normal(0, 0.1, q.shape)
+    P_in = H.random_perm(rng, 6)
+    d = H.load_json("admm_test_admm.json")
+    c = d["cases"][0]
+    pa = np.array(c["p"], np.float64)
+    got = _run(tmp_path, pts[1], adj[1], gains[1], q, vel, P_in,
+               pts=pa, adjf=np.array(c["adj"], np.float64))
+    _check(got, pts[1], adj[1], gains[1], q, vel, P_in)
+    assert np.linalg.norm(got["A"] - np.array(c["A"])) < d["tol"]
+    assert (got["iters"] > 0).all()
+
+
+@pytest.mark.parametrize("name", ["simform20_fc", "simform20_nc"])
+def test_facade_simform20(tmp_path, name):
+    """n = 20 generator formations with synthetic gains, random P_in."""
+    Pf, Af = H.simform(name)
+    rng = np.random.RandomState(7)
+    p, adj = Pf[1, 0], Af[1]
+    gains = H.synth_gains(rng, adj)
+    q = H.random_positions(rng, 20, 20.0)
+    vel = rng.normal(0, 0.2, q.shape)
+    P_in = H.random_perm(rng, 20)
+    got = _run(tmp_path, p, adj, gains, q, vel, P_in)
+    _check(got, p, adj, gains, q, vel, P_in)
