@@ -9,8 +9,10 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
-                        "libaclswarm_amd.so")
+# ACLSWARM_AMD_LIB points at another build of the same library (kernel
+# experiments); the default is the in-tree build.
+LIB_PATH = os.environ.get("ACLSWARM_AMD_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "lib", "libaclswarm_amd.so")
 
 ACL_OK = 0
 
@@ -29,7 +31,7 @@ STATUS_DTYPE = np.dtype([("flags", "<u4"), ("eff_rounds", "<u2"),
 EXPORTS = (
     "acl_default_cntrl_gains", "acl_default_safety_params", "acl_default_admm_params",
     "acl_max_vehicles", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
-    "acl_pack_gains", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
+    "acl_pack_gains", "acl_gain_planes", "acl_pack_gains_planes", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
     "acl_control_batch", "acl_write_assignment_log", "acl_read_assignment_log",
     "acl_malloc", "acl_free", "acl_memcpy_h2d", "acl_memcpy_d2h", "acl_memset",
     "acl_stream_synchronize", "acl_last_error",
@@ -59,7 +61,7 @@ class AdmmParams(ct.Structure):
 class Formations(ct.Structure):
     _fields_ = [("n", ct.c_int32), ("n_formations", ct.c_int32),
                 ("p", ct.c_void_p), ("adj", ct.c_void_p), ("gains", ct.c_void_p),
-                ("gain_off", ct.c_void_p)]
+                ("gain_off", ct.c_void_p), ("gain_planes", ct.c_int32)]
 
 
 class SolveArgs(ct.Structure):
@@ -108,6 +110,10 @@ def lib():
     L.acl_pack_adjacency.restype = ct.c_int
     L.acl_pack_gains.argtypes = [I32, VP, VP, VP]
     L.acl_pack_gains.restype = ct.c_int
+    L.acl_gain_planes.argtypes = [I32, VP, VP]
+    L.acl_gain_planes.restype = I32
+    L.acl_pack_gains_planes.argtypes = [I32, VP, VP, I32, VP]
+    L.acl_pack_gains_planes.restype = ct.c_int
     L.acl_admm_solve_batch.argtypes = [I32, I32, VP, VP, VP, VP, ct.POINTER(AdmmParams), VP]
     L.acl_admm_solve_batch.restype = ct.c_int
     L.acl_control_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(ControlArgs), VP]

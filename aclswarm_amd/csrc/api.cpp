@@ -63,21 +63,63 @@ extern "C" acl_status_t acl_pack_adjacency(int32_t n, const uint8_t* adj, uint64
   return ACL_OK;
 }
 
-extern "C" acl_status_t acl_pack_gains(int32_t n, const uint8_t* adj, const double* gains,
-                                       double* out) {
-  if (n < 1 || !adj || !gains || !out) return acl__set_error("acl_pack_gains: bad argument");
+namespace {
+// (r, c) of the 5 stored entries of the record layout; the other four entries
+// of every block are the structural zeros of admm::Solver::solve
+constexpr int kPlanes5[5][2] = {{0, 0}, {0, 1}, {1, 0}, {1, 1}, {2, 2}};
+
+bool is_pos_zero(double x) {
+  uint64_t u;
+  std::memcpy(&u, &x, 8);
+  return u == 0;
+}
+}  // namespace
+
+extern "C" int32_t acl_gain_planes(int32_t n, const uint8_t* adj, const double* gains) {
+  if (n < 1 || !adj || !gains) return 9;
+  const size_t ld = (size_t)3 * n;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      if (!adj[(size_t)j * n + i]) continue;
+      const double* blk = gains + (3 * (size_t)j) * ld + 3 * (size_t)i;  // column-major
+      // (0,2), (1,2), (2,0), (2,1)
+      if (!is_pos_zero(blk[2 * ld + 0]) || !is_pos_zero(blk[2 * ld + 1]) ||
+          !is_pos_zero(blk[0 * ld + 2]) || !is_pos_zero(blk[1 * ld + 2]))
+        return 9;
+    }
+  return 5;
+}
+
+extern "C" acl_status_t acl_pack_gains_planes(int32_t n, const uint8_t* adj, const double* gains,
+                                              int32_t planes, double* out) {
+  if (n < 1 || !adj || !gains || !out || (planes != 9 && planes != 5))
+    return acl__set_error("acl_pack_gains_planes: bad argument");
+  if (planes == 5 && acl_gain_planes(n, adj, gains) != 5)
+    return acl__set_error("acl_pack_gains_planes: a gain block has a nonzero (or -0.0) "
+                          "entry outside the 5-entry structure");
   const int64_t E = acl_count_edges(n, adj);
   const size_t ld = (size_t)3 * n;  // column-major leading dimension
   int64_t e = 0;
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) {
       if (!adj[(size_t)j * n + i]) continue;
-      for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c)
-          out[(size_t)(3 * r + c) * E + e] = gains[(3 * (size_t)j + c) * ld + 3 * (size_t)i + r];
+      const double* blk = gains + (3 * (size_t)j) * ld + 3 * (size_t)i;
+      if (planes == 9) {
+        for (int r = 0; r < 3; ++r)
+          for (int c = 0; c < 3; ++c) out[(size_t)(3 * r + c) * E + e] = blk[(size_t)c * ld + r];
+      } else {  // one record of 5 doubles per edge
+        for (int k = 0; k < 5; ++k)
+          out[(size_t)5 * e + k] = blk[(size_t)kPlanes5[k][1] * ld + kPlanes5[k][0]];
+      }
       ++e;
     }
   return ACL_OK;
+}
+
+extern "C" acl_status_t acl_pack_gains(int32_t n, const uint8_t* adj, const double* gains,
+                                       double* out) {
+  if (n < 1 || !adj || !gains || !out) return acl__set_error("acl_pack_gains: bad argument");
+  return acl_pack_gains_planes(n, adj, gains, 9, out);
 }
 
 // ---- Auctioneer::logAssignment records (auctioneer.cpp:577-597) ----------

@@ -4,7 +4,8 @@
 // swarms. Two kernels:
 //
 //   gain_kernel    DistCntrl::compute (aclswarm/src/distcntrl.cpp:46-102):
-//                  the HBM stream (72 B of gain block per directed edge).
+//                  the HBM stream (72 B of gain block per directed edge, 40 B
+//                  in the 5-entry record layout of ADMM-structured blocks).
 //                  One wave per vehicle v, lanes = formation neighbours j of
 //                  v's adopted point i (chunks of 64), the 3x3 block A_ij read
 //                  from the 9 coalesced planes, pdistmat's Gram-formula
@@ -36,8 +37,32 @@ constexpr int kCtlWaves = kCtlBlock / 64;
 
 __host__ __device__ inline int cal16(int x) { return (x + 15) & ~15; }
 
+// Lane segments of the gain kernel: a wave processes G vehicles at once, each
+// on S consecutive lanes, in `it` passes (j = s + S t), so that n columns fill
+// the 64 lanes well (n = 100: S = 20, G = 3, 5 passes, 94% of the lanes busy,
+// against 78% for one vehicle per wave).
+struct GainSeg {
+  int S, G, it;
+};
+
+__host__ __device__ inline GainSeg gain_segments(int n) {
+  GainSeg best = {64, 1, (n + 63) / 64};
+  double bu = -1.0;
+  for (int it = 1; it <= 16; ++it) {
+    const int S = (n + it - 1) / it;
+    if (S > 64) continue;
+    const int G = 64 / S;
+    const double u = (double)n * G / (64.0 * it);
+    if (u > bu + 1e-9) {
+      bu = u;
+      best = {S, G, it};
+    }
+  }
+  return best;
+}
+
 struct GainLayout {
-  int q, p, adjF, rowptr, Pt, myi, out, outs, cafl, atab, total;
+  int q, p, pn, adjF, rowpre, Pt, myi, out, red, atab, total;
 };
 
 __host__ __device__ inline GainLayout make_gain_layout(int n) {
@@ -46,14 +71,14 @@ __host__ __device__ inline GainLayout make_gain_layout(int n) {
   int o = 0;
   L.q = o;      o = cal16(o + n * 3 * 8);
   L.p = o;      o = cal16(o + n * 3 * 8);
+  L.pn = o;     o = cal16(o + n * 2 * 8);       // |p_xy|^2, p_z^2 per point
   L.adjF = o;   o = cal16(o + n * NW * 8);
-  L.rowptr = o; o = cal16(o + (n + 1) * 4);
+  L.rowpre = o; o = cal16(o + (n * NW + 1) * 4);  // edge index of each row word's first bit
   L.Pt = o;     o = cal16(o + n * 2);
   L.myi = o;    o = cal16(o + n * 2);
-  L.out = o;    o = cal16(o + n * 3 * 8);   // u (DistCntrl)
-  L.outs = o;   o = cal16(o + n * 3 * 8);   // u_safe of the vehicles no one is close to
-  L.cafl = o;   o = cal16(o + n);
-  L.atab = o;   o = cal16(o + 30 * 8);      // atan range-reduction table
+  L.out = o;    o = cal16(o + n * 3 * 8);       // u (DistCntrl)
+  L.red = o;    o = cal16(o + kCtlWaves * 64 * 3 * 8);  // per-lane partial sums
+  L.atab = o;   o = cal16(o + 30 * 8);          // atan range-reduction table
   L.total = o;
   return L;
 }
@@ -70,6 +95,9 @@ __device__ __forceinline__ void saturate(const acl_safety_params_t& sp, double& 
   if (velz > sp.max_vel_z) c2 = c2 / velz * sp.max_vel_z;
 }
 
+// NP = 9: general 3x3 gain blocks; NP = 5: the ADMM block structure, the four
+// structural zeros supplied as constants (acl_formations_t::gain_planes)
+template <int NP>
 __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
@@ -83,13 +111,13 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
 
   double* q = reinterpret_cast<double*>(smem + L.q);
   double* p = reinterpret_cast<double*>(smem + L.p);
+  double* pn = reinterpret_cast<double*>(smem + L.pn);
   unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
-  int* rowptr = reinterpret_cast<int*>(smem + L.rowptr);
+  int* rowpre = reinterpret_cast<int*>(smem + L.rowpre);
   uint16_t* Pt = reinterpret_cast<uint16_t*>(smem + L.Pt);
   uint16_t* myi = reinterpret_cast<uint16_t*>(smem + L.myi);
   double* uo = reinterpret_cast<double*>(smem + L.out);
-  double* us = reinterpret_cast<double*>(smem + L.outs);
-  unsigned char* cafl = smem + L.cafl;
+  double* red = reinterpret_cast<double*>(smem + L.red) + wave * 64 * 3;
   double* atab = reinterpret_cast<double*>(smem + L.atab);
   if (tid < 30) atab[tid] = kAtanTab[tid / 6][tid % 6];
 
@@ -104,6 +132,11 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
       q[k] = gq[k];
       p[k] = gp[k];
     }
+    for (int j = tid; j < n; j += kCtlBlock) {
+      const double x = gp[3 * j], y = gp[3 * j + 1], z = gp[3 * j + 2];
+      pn[2 * j] = x * x + y * y;
+      pn[2 * j + 1] = z * z;
+    }
     const uint64_t* ga = P.adj + (size_t)f * n * NW;
     for (int k = tid; k < n * NW; k += kCtlBlock) {
       unsigned long long x = ga[k];
@@ -116,74 +149,113 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
     }
   }
   __syncthreads();
-  // formation CSR row starts (edges enumerated row-major, diagonal included)
+  // edge index of the first bit of every row word: formation edges are
+  // enumerated row-major (i, then j ascending), diagonal included
   if (wave == 0) {
     int base = 0;
-    for (int c = 0; c < NW; ++c) {
-      const int i = lane + 64 * c;
-      int cnt = 0;
-      if (i < n)
-        for (int w = 0; w < NW; ++w) cnt += __popcll(adjF[i * NW + w]);
+    for (int w = 0; w < NW * n; w += 64) {
+      const int k = w + lane;
+      const int cnt = (k < n * NW) ? __popcll(adjF[k]) : 0;
       int x = cnt;  // inclusive wave scan
       for (int o = 1; o < 64; o <<= 1) {
         const int y = __shfl_up(x, o, 64);
         if (lane >= o) x += y;
       }
-      if (i < n) rowptr[i] = base + x - cnt;
+      if (k < n * NW) rowpre[k] = base + x - cnt;
       base += __shfl(x, 63, 64);
     }
-    if (lane == 0) rowptr[n] = base;
+    if (lane == 0) rowpre[n * NW] = base;
   }
   __syncthreads();
 
-  // LDS reads land in VGPRs; values that are wave-uniform are moved to
-  // SGPRs so the gain addressing stays scalar (no per-lane 64-bit addresses,
-  // no waterfall loops around the buffer loads)
-  const int E = __builtin_amdgcn_readfirstlane(rowptr[n]);
-  const double* G = P.gains + 9 * P.gain_off[f];
-  // the formation's 9 planes through one buffer resource: a lane's nine
-  // loads share one VGPR offset (plane k at SGPR offset 8kE); a lane with no
-  // edge reads past num_records, which returns 0
+  const int E = __builtin_amdgcn_readfirstlane(rowpre[n * NW]);
+  const double* G = P.gains + NP * P.gain_off[f];
+  // the formation's gains through one buffer resource (9 planes: plane k at
+  // SGPR offset 8kE, one VGPR offset per lane; 5: one 40-byte record per
+  // edge); a lane with no edge reads past num_records, which returns 0
   const __amdgpu_buffer_rsrc_t grs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 9 * E * 8, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, NP * E * 8, 0x00020000);
   const acl_cntrl_gains_t g = P.g;
-  const acl_safety_params_t sp = P.s;
-  const double thr_hi = sp.d_avoid_thresh * (1.0 + 0x1p-40);
-  const double thr2hi = thr_hi * thr_hi;
-  for (int v = wave; v < n; v += kCtlWaves) {
-    const int i = __builtin_amdgcn_readfirstlane(myi[v]);
-    // the vehicle's values are wave-uniform: held in SGPRs
-    const double* gv = P.vel + ((size_t)b * n + v) * 3;
-    const double vel0 = uni(gv[0]), vel1 = uni(gv[1]), vel2 = uni(gv[2]);
-    const double qv0 = uni(q[3 * v]), qv1 = uni(q[3 * v + 1]), qv2 = uni(q[3 * v + 2]);
-    const double pix = uni(p[3 * i]), piy = uni(p[3 * i + 1]), piz = uni(p[3 * i + 2]);
-    const double Ni = pix * pix + piy * piy, Nzi = piz * piz;
+  const GainSeg sg = gain_segments(n);
+  const int S = sg.S, GV = sg.G, IT = sg.it;
+  const int seg = lane / S, s = lane - seg * S;
+  const int ngroups = (n + GV - 1) / GV;
+  // Groups walk formation rows in order when every vehicle holds the same
+  // assignment (vehicle v = Pt[i] of row i): consecutive rows are consecutive
+  // edge ranges, so the gain stream is read nearly sequentially.
+  // Otherwise groups walk vehicles, each with its own adopted point.
+  for (int grp = wave; grp < ngroups; grp += kCtlWaves) {
+    const int r = grp * GV + seg;
+    const bool act = seg < GV && r < n;
+    const int rr = act ? r : 0;
+    const int vv = uniform ? (int)Pt[rr] : rr;
+    const int v = vv;
+    const int i = uniform ? rr : (int)myi[vv];
+    const double* gv = P.vel + ((size_t)b * n + vv) * 3;
+    const double vel0 = gv[0], vel1 = gv[1], vel2 = gv[2];
+    const double qv0 = q[3 * vv], qv1 = q[3 * vv + 1], qv2 = q[3 * vv + 2];
+    const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
+    const double Ni = pn[2 * i], Nzi = pn[2 * i + 1];
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-    int ebase = __builtin_amdgcn_readfirstlane(rowptr[i]);
+    // edge of pass t for this lane (-1: none); the gain loads of pass t + 1
+    // are issued before pass t's math so that each wave keeps one pass of
+    // the gain stream in flight while it computes
+    auto edge_of = [&](int t) -> int {
+      const int j = s + S * t;
+      const int jw = j >> 6, jb = j & 63;
+      const unsigned long long word = (act && j < n) ? adjF[i * NW + jw] : 0ull;
+      if (!((word >> jb) & 1ull)) return -1;
+      return rowpre[i * NW + jw] + __popcll(word & ((1ull << jb) - 1ull));
+    };
+    auto load_planes = [&](int e, double (&Lg)[NP]) {
+      if constexpr (NP == 9) {
+        const int voff = e >= 0 ? e * 8 : 0x40000000;  // past num_records -> 0
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const auto raw = __builtin_amdgcn_raw_buffer_load_b64(grs, voff, k * E * 8, 0);
+          __builtin_memcpy(&Lg[k], &raw, 8);
+        }
+      } else {
+        // one 40-byte record per edge: two 16-byte loads and one 8-byte load
+        const int voff = e >= 0 ? e * 40 : 0x40000000;
+        const auto r0 = __builtin_amdgcn_raw_buffer_load_b128(grs, voff, 0, 0);
+        const auto r1 = __builtin_amdgcn_raw_buffer_load_b128(grs, voff, 16, 0);
+        const auto r2 = __builtin_amdgcn_raw_buffer_load_b64(grs, voff, 32, 0);
+        __builtin_memcpy(&Lg[0], &r0, 16);
+        __builtin_memcpy(&Lg[2], &r1, 16);
+        __builtin_memcpy(&Lg[4], &r2, 8);
+      }
+    };
+    int e_cur = edge_of(0);
+    double Lc[NP];
+    load_planes(e_cur, Lc);
 #pragma unroll 1
-    for (int c = 0; c < NW; ++c) {
-      const unsigned long long rowbits = uni_u64(adjF[i * NW + c]);
-      const bool has = (rowbits >> lane) & 1ull;
-      const int e = ebase + __popcll(rowbits & ((1ull << lane) - 1ull));
-      ebase += __popcll(rowbits);
-      const int voff = has ? e * 8 : 0x40000000;
-      if (has) {
+    for (int t = 0; t < IT; ++t) {
+      int e_nxt = -1;
+      double Ln[NP];
+      if (t + 1 < IT) e_nxt = edge_of(t + 1);
+      load_planes(e_nxt, Ln);
+      if (e_cur >= 0) {
         // tolerance-based parity (1e-5 relative): fused multiply-adds and the
         // refined fast sqrt / quotient (common.h) are allowed here
 #pragma clang fp contract(fast)
+        const int j = s + S * t;
         double A[9];
+        if constexpr (NP == 9) {
 #pragma unroll
-        for (int k = 0; k < 9; ++k) {
-          const auto raw = __builtin_amdgcn_raw_buffer_load_b64(grs, voff, k * E * 8, 2 /* nt */);
-          __builtin_memcpy(&A[k], &raw, 8);
+          for (int k = 0; k < 9; ++k) A[k] = Lc[k];
+        } else {
+          // (0,0) (0,1) (1,0) (1,1) (2,2) stored; +0.0 elsewhere (solver.cpp:49-77).
+          // The zeros still multiply q below, as in the 9-plane layout.
+          A[0] = Lc[0]; A[1] = Lc[1]; A[2] = 0.0;
+          A[3] = Lc[2]; A[4] = Lc[3]; A[5] = 0.0;
+          A[6] = 0.0;   A[7] = 0.0;   A[8] = Lc[4];
         }
-        const int j = lane + 64 * c;
         const int uu = uniform ? Pt[j] : rows[(size_t)v * n + j];
         const double q0 = q[3 * uu] - qv0, q1 = q[3 * uu + 1] - qv1, q2 = q[3 * uu + 2] - qv2;
         const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
-        const double Nj = pjx * pjx + pjy * pjy, Nzj = pjz * pjz;
-        const double dxy = sqrt_nr((Ni + Nj) - 2.0 * (pix * pjx + piy * pjy));
-        const double dz = sqrt_nr((Nzi + Nzj) - 2.0 * (piz * pjz));
+        const double dxy = sqrt_nr((Ni + pn[2 * j]) - 2.0 * (pix * pjx + piy * pjy));
+        const double dz = sqrt_nr((Nzi + pn[2 * j + 1]) - 2.0 * (piz * pjz));
         const double e_xy = sqrt_nr(q0 * q0 + q1 * q1) - dxy;
         const double e_z = fabs(q2) - dz;  // |q_ij.z| = sqrt(q2^2) (no over/underflow)
         // the two gated atan terms, one after the other (register pressure)
@@ -201,45 +273,72 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
         const double up0 = ((A[0] * q0 + A[1] * q1) + A[2] * q2) + Fxy * q0;
         const double up1 = ((A[3] * q0 + A[4] * q1) + A[5] * q2) + Fxy * q1;
         const double up2 = ((A[6] * q0 + A[7] * q1) + A[8] * q2) + Fz * q2;
+#ifdef ACL_EXP_GAIN_STREAM_ONLY
+        acc0 += A[0] + A[1]; acc1 += A[3] + A[4]; acc2 += A[8];
+        (void)up0; (void)up1; (void)up2;
+#else
         acc0 += g.kp * up0 + g.kd * (-vel0);
         acc1 += g.kp * up1 + g.kd * (-vel1);
         acc2 += g.kp * up2 + g.kd * (-vel2);
+#endif
       }
+      e_cur = e_nxt;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) Lc[k] = Ln[k];
     }
-    double cmd0 = wave_sum(acc0), cmd1 = wave_sum(acc1), cmd2 = wave_sum(acc2);
-    if (lane == 0) {
-      uo[3 * v] = cmd0; uo[3 * v + 1] = cmd1; uo[3 * v + 2] = cmd2;
-    }
-    saturate(sp, cmd0, cmd1, cmd2);
-    // collisionAvoidance's first test: any other vehicle with
-    // !(|dq_xy| > d_avoid_thresh)? |dq_xy|^2 above (thr (1 + 2^-40))^2 is
-    // far for certain, so the sqrt is taken only near the threshold.
-    bool close = false;
-    for (int c = 0; c < NW; ++c) {
-      const int j = lane + 64 * c;
-      if (j < n && j != v) {
-        const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
-        const double s2 = dx * dx + dy * dy;
-        if (!(s2 > thr2hi)) close |= !(sqrt(s2) > sp.d_avoid_thresh);
+    // segment sums: each vehicle's S lane partials, in lane order
+    red[3 * lane] = acc0; red[3 * lane + 1] = acc1; red[3 * lane + 2] = acc2;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (lane < GV && grp * GV + lane < n) {
+      const double* r = red + 3 * S * lane;
+      double c0 = r[0], c1 = r[1], c2 = r[2];
+      for (int k = 1; k < S; ++k) {
+        c0 += r[3 * k]; c1 += r[3 * k + 1]; c2 += r[3 * k + 2];
       }
+      const int w = uniform ? (int)Pt[grp * GV + lane] : grp * GV + lane;
+      uo[3 * w] = c0; uo[3 * w + 1] = c1; uo[3 * w + 2] = c2;
     }
-    const bool anyclose = __ballot(close) != 0ull;
-    if (lane == 0) {
-      us[3 * v] = cmd0; us[3 * v + 1] = cmd1; us[3 * v + 2] = cmd2;
-      cafl[v] = 0;
-      if (anyclose) {  // the rest of collisionAvoidance runs in ca_kernel
-        const unsigned slot = atomicAdd(P.ca_count, 1u);
-        P.ca_list[slot] = (unsigned)(b * n + v);
-      }
-    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
   }
   __syncthreads();
-  for (int k = tid; k < 3 * n; k += kCtlBlock) {
-    P.u[(size_t)b * n * 3 + k] = uo[k];
-    if (P.u_safe) P.u_safe[(size_t)b * n * 3 + k] = us[k];
+  // per vehicle (lanes over vehicles): Safety::cmdinCb saturation and the
+  // first test of collisionAvoidance -- any other vehicle with
+  // !(|dq_xy| > d_avoid_thresh)? |dq_xy|^2 above (thr (1 + 2^-40))^2 is far
+  // for certain, so the sqrt is taken only near the threshold.
+  const acl_safety_params_t sp = P.s;
+  const double thr_hi = sp.d_avoid_thresh * (1.0 + 0x1p-40);
+  const double thr2hi = thr_hi * thr_hi;
+  for (int v = tid; v < n; v += kCtlBlock) {
+    double cmd0 = uo[3 * v], cmd1 = uo[3 * v + 1], cmd2 = uo[3 * v + 2];
+    double* gu = P.u + ((size_t)b * n + v) * 3;
+    gu[0] = cmd0; gu[1] = cmd1; gu[2] = cmd2;
+    saturate(sp, cmd0, cmd1, cmd2);
+    const double qv0 = q[3 * v], qv1 = q[3 * v + 1];
+    bool near = false;  // any j != v with !(s2 > thr2hi) (NaN included)
+    for (int j = 0; j < n; ++j) {
+      const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
+      near |= (j != v) && !(dx * dx + dy * dy > thr2hi);
+    }
+    bool close = false;
+    if (near) {
+      for (int j = 0; j < n; ++j) {
+        const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
+        const double s2 = dx * dx + dy * dy;
+        if (j != v && !(s2 > thr2hi)) close |= !(sqrt(s2) > sp.d_avoid_thresh);
+      }
+    }
+    if (P.u_safe) {
+      double* o = P.u_safe + ((size_t)b * n + v) * 3;
+      o[0] = cmd0; o[1] = cmd1; o[2] = cmd2;
+    }
+    if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 0;
+    if (close) {  // the rest of collisionAvoidance runs in ca_kernel
+      const unsigned slot = atomicAdd(P.ca_count, 1u);
+      P.ca_list[slot] = (unsigned)(b * n + v);
+    }
   }
-  if (P.ca_flag)
-    for (int v = tid; v < n; v += kCtlBlock) P.ca_flag[(size_t)b * n + v] = cafl[v];
 }
 
 // collisionAvoidance (safety.cpp:412-541) for the vehicles gain_kernel
@@ -453,10 +552,13 @@ hipError_t launch_control_prep(const CtlParams& P, const uint16_t* Pgiven, int n
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream) {
   if (which == 0) {
     const GainLayout L = make_gain_layout(P.n);
+    const void* k = P.gain_planes == 5 ? (const void*)gain_kernel<5> : (const void*)gain_kernel<9>;
     if (L.total > 64 * 1024)
-      (void)hipFuncSetAttribute((const void*)gain_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, L.total);
-    hipLaunchKernelGGL(gain_kernel, dim3(nb), dim3(kCtlBlock), L.total, stream, P);
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, L.total);
+    if (P.gain_planes == 5)
+      hipLaunchKernelGGL(gain_kernel<5>, dim3(nb), dim3(kCtlBlock), L.total, stream, P);
+    else
+      hipLaunchKernelGGL(gain_kernel<9>, dim3(nb), dim3(kCtlBlock), L.total, stream, P);
   } else {
     // a fixed grid striding over the device-side count of listed vehicles
     const int lds = kCaWaves * ca_wave_bytes(P.n);

@@ -78,6 +78,7 @@ struct CtlParams {
   const uint64_t* adj;
   const double* gains;
   const int64_t* gain_off;
+  int gain_planes;  // 9 or 5 (acl_formations_t::gain_planes)
   const int32_t* fidx;
   const double* q;
   const double* vel;

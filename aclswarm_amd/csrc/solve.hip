@@ -674,6 +674,8 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
     return acl__set_error("acl_solve_batch: workspace is NULL (acl_solve_workspace_bytes)");
   if (a->do_control && (!F->gains || !F->gain_off || !a->vel))
     return acl__set_error("acl_solve_batch: do_control needs gains, gain_off and vel");
+  if (a->do_control && F->gain_planes != 0 && F->gain_planes != 9 && F->gain_planes != 5)
+    return acl__set_error("acl_solve_batch: gain_planes must be 9 (or 0) or 5");
   SolveParams P;
   P.n = n; P.B = a->B; P.F = F->n_formations; P.b0 = 0;
   P.p = F->p; P.adj = F->adj; P.gains = F->gains; P.gain_off = F->gain_off;
@@ -707,6 +709,7 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   CtlParams C;
   C.n = n; C.B = a->B; C.b0 = 0;
   C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
+  C.gain_planes = F->gain_planes == 5 ? 5 : 9;
   C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P_out;
   C.status = a->status;
   C.u = a->u ? a->u : reinterpret_cast<double*>(P.ws + P.W.u);
@@ -739,11 +742,14 @@ extern "C" acl_status_t acl_control_batch(const acl_formations_t* F, const acl_c
   if (!F->p || !F->adj || !F->gains || !F->gain_off || !a->fidx || !a->q || !a->vel || !a->P ||
       !a->status || !a->workspace)
     return acl__set_error("acl_control_batch: required pointer is NULL");
+  if (F->gain_planes != 0 && F->gain_planes != 9 && F->gain_planes != 5)
+    return acl__set_error("acl_control_batch: gain_planes must be 9 (or 0) or 5");
   const WsLayout W = ws_layout(n, a->B);
   unsigned char* ws = (unsigned char*)a->workspace;
   CtlParams C;
   C.n = n; C.B = a->B; C.b0 = 0;
   C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
+  C.gain_planes = F->gain_planes == 5 ? 5 : 9;
   C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P;
   C.status = a->status;
   C.u = a->u ? a->u : reinterpret_cast<double*>(ws + W.u);

@@ -17,12 +17,24 @@ def _ptr(t):
     return ct.c_void_p(t.data_ptr()) if t is not None else ct.c_void_p(0)
 
 
-def pack_formation_host(points, adj, gains=None):
-    """One formation -> (p [n][3], adj bits [n][W] u64, gain planes [9*E] f64).
+def gain_planes_host(adj, gains):
+    """5 when every edge block of the GainMat has the ADMM structure (exact
+    +0.0 at (0,2), (1,2), (2,0), (2,1)), else 9 (acl_gain_planes)."""
+    lib = L.lib()
+    n = np.asarray(adj).shape[0]
+    adj_cm = np.ascontiguousarray(np.asarray(adj, dtype=np.uint8).T)
+    g_cm = np.ascontiguousarray(np.asarray(gains, dtype=np.float64).T)
+    return int(lib.acl_gain_planes(n, adj_cm.ctypes.data, g_cm.ctypes.data))
+
+
+def pack_formation_host(points, adj, gains=None, planes=9):
+    """One formation -> (p [n][3], adj bits [n][W] u64, gain planes
+    [planes*E] f64, E).
 
     points [n][3]; adj [n][n] with adj[i][j] = adjmat(i,j); gains [3n][3n]
     with gains[r][c] = GainMat(r,c). Uses the ABI's packers, which take the
-    reference's column-major Eigen layouts.
+    reference's column-major Eigen layouts. planes = 9 (general blocks) or 5
+    (ADMM-structured blocks, acl_formations_t::gain_planes).
     """
     lib = L.lib()
     points = np.ascontiguousarray(points, dtype=np.float64)
@@ -32,33 +44,42 @@ def pack_formation_host(points, adj, gains=None):
     bits = np.zeros((n, W), np.uint64)
     L.check(lib.acl_pack_adjacency(n, adj_cm.ctypes.data, bits.ctypes.data), "pack_adjacency")
     E = int(lib.acl_count_edges(n, adj_cm.ctypes.data))
-    planes = np.zeros(9 * E, np.float64)
+    out = np.zeros(planes * E, np.float64)
     if gains is not None:
         g_cm = np.ascontiguousarray(np.asarray(gains, dtype=np.float64).T)
-        L.check(lib.acl_pack_gains(n, adj_cm.ctypes.data, g_cm.ctypes.data,
-                                   planes.ctypes.data), "pack_gains")
-    return points, bits, planes, E
+        L.check(lib.acl_pack_gains_planes(n, adj_cm.ctypes.data, g_cm.ctypes.data, planes,
+                                          out.ctypes.data), "pack_gains_planes")
+    return points, bits, out, E
 
 
 class FormationTable:
-    """Device formation table (acl_formations_t): F formations of n points."""
+    """Device formation table (acl_formations_t): F formations of n points,
+    gains as `gain_planes` (9 or 5) edge planes per formation."""
 
-    def __init__(self, n, p, adj_bits, gains, gain_off):
+    def __init__(self, n, p, adj_bits, gains, gain_off, gain_planes=9):
         self.n = int(n)
         self.p = p
         self.adj = adj_bits
         self.gains = gains
         self.gain_off = gain_off
+        self.gain_planes = int(gain_planes)
         self.F = int(p.shape[0])
 
     @classmethod
-    def from_host(cls, points, adjs, gains=None, device="cuda"):
+    def from_host(cls, points, adjs, gains=None, device="cuda", planes=None):
+        """planes=None picks 5 when every formation's GainMat has the ADMM
+        block structure, else 9."""
         F = len(points)
+        if planes is None:
+            planes = 9
+            if gains is not None and all(gain_planes_host(adjs[f], gains[f]) == 5
+                                         for f in range(F)):
+                planes = 5
         ps, bs, gs, offs = [], [], [], []
         off = 0
         for f in range(F):
             p, b, g, E = pack_formation_host(points[f], adjs[f],
-                                             None if gains is None else gains[f])
+                                             None if gains is None else gains[f], planes)
             ps.append(p); bs.append(b); gs.append(g); offs.append(off)
             off += E
         n = ps[0].shape[0]
@@ -69,11 +90,11 @@ class FormationTable:
             g = np.zeros(9)
         g = torch.from_numpy(g).to(device)
         goff = torch.tensor(offs, dtype=torch.int64, device=device)
-        return cls(n, p, bits, g, goff)
+        return cls(n, p, bits, g, goff, planes)
 
     def struct(self):
         return L.Formations(self.n, self.F, self.p.data_ptr(), self.adj.data_ptr(),
-                            self.gains.data_ptr(), self.gain_off.data_ptr())
+                            self.gains.data_ptr(), self.gain_off.data_ptr(), self.gain_planes)
 
 
 _WS = {}

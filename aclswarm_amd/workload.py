@@ -77,12 +77,16 @@ def pack_bits(adj):
     return (pad.view(B, n, W, 64) << shifts).sum(dim=-1)
 
 
-def simform_workload(B, n, gen, device, F=None, L=None, complete=False, gains_scale=0.05):
+def simform_workload(B, n, gen, device, F=None, L=None, complete=False, gains_scale=0.05,
+                     planes=5):
     """Config C3 (n=100, noncomplete, L=40) style batch.
 
     F=None: every swarm has its own formation (points, graph, gains): the
     Monte-Carlo setting of the north star, and the one whose bytes are
     dominated by the per-swarm gains stream.
+    planes=5: gain blocks with the structure admm::Solver::solve produces
+    ([a b 0; c d 0; 0 0 e], solver.cpp:49-77), 5-entry records per edge;
+    planes=9: unstructured random 3x3 blocks as 9 planes.
     Returns dict of device tensors (formation table + swarm inputs).
     """
     if L is None:
@@ -95,14 +99,14 @@ def simform_workload(B, n, gen, device, F=None, L=None, complete=False, gains_sc
     goff = torch.zeros(nf, dtype=torch.int64, device=device)
     goff[1:] = torch.cumsum(E, 0)[:-1]
     Etot = int(E.sum().item())
-    gains = torch.empty(9 * Etot, dtype=torch.float64, device=device)
+    gains = torch.empty(planes * Etot, dtype=torch.float64, device=device)
     gains.uniform_(-gains_scale, gains_scale, generator=gen)
     side = 20.0 * (n / 20.0) ** 0.5
     q = nonoverlapping_points(B, n, side, side, 1.0, 1.0, 1.5, gen, device)
     vel = 0.1 * torch.randn((B, n, 3), generator=gen, device=device, dtype=torch.float64)
     P_in = torch.arange(n, dtype=torch.int16, device=device).expand(B, n).contiguous()
     fidx = (torch.arange(B, device=device) % nf).to(torch.int32)
-    return dict(n=n, F=nf, p=p, adj=adj, bits=bits, E=E, gain_off=goff, gains=gains,
+    return dict(n=n, F=nf, p=p, adj=adj, bits=bits, E=E, gain_off=goff, gains=gains, planes=planes,
                 q=q, vel=vel, P_in=P_in, fidx=fidx)
 
 
@@ -114,10 +118,14 @@ def dense_gains_host(w, f):
     adj = w["adj"][f].cpu().numpy()
     E = int(w["E"][f].item())
     off = int(w["gain_off"][f].item())
-    planes = w["gains"][9 * off: 9 * off + 9 * E].view(9, E).cpu().numpy()
+    NP = w.get("planes", 9)
+    flat = w["gains"][NP * off: NP * off + NP * E]
+    # 9: planes of E; 5: one record of 5 per edge
+    planes = (flat.view(9, E) if NP == 9 else flat.view(E, 5).t()).cpu().numpy()
     ii, jj = np.nonzero(adj)
     G = np.zeros((3 * n, 3 * n))
-    for r in range(3):
-        for c in range(3):
-            G[3 * ii + r, 3 * jj + c] = planes[3 * r + c]
+    rc = [(r, c) for r in range(3) for c in range(3)] if NP == 9 else \
+        [(0, 0), (0, 1), (1, 0), (1, 1), (2, 2)]
+    for k, (r, c) in enumerate(rc):
+        G[3 * ii + r, 3 * jj + c] = planes[k]
     return G

@@ -3,7 +3,8 @@
 
 One step = one acl_solve_batch over B swarms (config C3: simform100
 noncomplete graphs, every swarm with its own formation -- points, graph and
-3x3 gain blocks -- so the per-swarm gain stream dominates the bytes), i.e.
+3x3 gain blocks with the structure admm::Solver::solve gives them, streamed
+as 40-byte records per edge -- so the per-swarm gain stream dominates the bytes), i.e.
 for every swarm: all vehicles' 2-D Umeyama alignment, CBAA to consensus
 (bit-exact, exact fixed-point exit), adoption, one DistCntrl step,
 saturation and collision avoidance. Inputs are resident in HBM before the
@@ -41,7 +42,8 @@ def algorithmic_bytes(w, lo, hi):
     them. Auction kernel, per swarm: fidx 4, q 24n, P_in 2n, P_out 2n,
     status 16; per formation used: p 24n, adjacency bits 8nW. Gain kernel
     (DistCntrl + saturation + the collision test), per swarm: vel 24n,
-    u 24n, u_safe 24n, ca n; per formation used: gain_off 8, gains 72 E_f.
+    u 24n, u_safe 24n, ca n; per formation used: gain_off 8, gains 8 G E_f
+    (G = 5 stored planes for ADMM-structured blocks, 9 for general ones).
     The collision-avoidance kernel touches only the vehicles the gain kernel
     listed (none in this workload): 0. Re-reads (the later kernels' q, p,
     adjacency, P_out, the workspace hand-off) are implementation traffic,
@@ -52,7 +54,7 @@ def algorithmic_bytes(w, lo, hi):
     used = torch.unique(w["fidx"][lo:hi])
     E = w["E"][used].sum().item()
     auction = Bc * (4 + n * (24 + 2 + 2) + 16) + used.numel() * (24 * n + 8 * n * W)
-    gain = Bc * n * (24 + 24 + 24 + 1) + used.numel() * 8 + 72 * E
+    gain = Bc * n * (24 + 24 + 24 + 1) + used.numel() * 8 + 8 * w["planes"] * E
     return auction, gain, 0, E / used.numel()
 
 
@@ -137,6 +139,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--gain-planes", type=int, default=5, choices=(5, 9),
+                    help="5: ADMM-structured gain blocks (the reference's gains); "
+                         "9: general 3x3 blocks")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -152,10 +157,12 @@ def main():
     gen.manual_seed(args.seed + 7919 * rank)
     t0 = time.time()
     w = workload.simform_workload(args.B, args.n, gen, dev,
-                                  F=(args.formations or None), complete=False)
+                                  F=(args.formations or None), complete=False,
+                                  planes=args.gain_planes)
     torch.cuda.synchronize()
     t_gen = time.time() - t0
-    T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"])
+    T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"],
+                              w["planes"])
     B, n = args.B, args.n
     out = {
         "P_out": torch.empty((B, n), dtype=torch.int16, device=dev),
@@ -214,7 +221,7 @@ def main():
     per_launch = {"auction": a_all / nlaunch, "gain": g_all / nlaunch, "ca": s_all / nlaunch}
     kern = {}
     for k, (name, sym) in enumerate((("auction", "acl_amd::solve_kernel"),
-                                     ("gain", "acl_amd::gain_kernel"),
+                                     ("gain", f"acl_amd::gain_kernel<{w['planes']}>"),
                                      ("ca", "acl_amd::ca_kernel"))):
         avg = kms[k] / max(kcnt[k], 1)
         ach = per_launch[name] / (avg * 1e-3) / 1e9
@@ -245,7 +252,9 @@ def main():
             "edges_per_formation_avg": e_avg,
             "cbaa": "all 2N rounds" if args.full_rounds else "exact fixed-point exit",
             "parallelism": f"swarm-sharded x{world}",
-            "gains": "synthetic random 3x3 blocks (values do not affect throughput)",
+            "gains": ("synthetic ADMM-structured blocks [a b 0; c d 0; 0 0 e] "
+                      "(solver.cpp:49-77), 5-entry records = 40 B/edge" if w["planes"] == 5 else
+                      "synthetic random 3x3 blocks, 9 planes = 72 B/edge"),
         },
         "roofline": {
             "bound": "hbm", "achieved": kern[dom]["achieved_GBs"], "peak": HBM_PEAK_GBS,

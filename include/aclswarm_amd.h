@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define ACL_ABI_VERSION 1
+#define ACL_ABI_VERSION 2
 
 typedef enum {
   ACL_OK = 0,
@@ -127,6 +127,18 @@ typedef struct {
  *            (distcntrl.cpp:66) is stored as 9 planes: element (r,c) of edge e
  *            at gains[9*gain_off[f] + (3r+c)*E_f + e].
  *   gain_off [F] i64         edge offset of formation f (prefix sum of E_f).
+ *   gain_planes              9 (or 0): the layout above. 5: every block has
+ *            the structure admm::Solver::solve assembles (solver.cpp:49-77:
+ *            A = MatrixXd::Zero, the xy 2x2 block from the 2-D design, (2,2)
+ *            from the 1-D design), i.e. exact +0.0 at (0,2), (1,2), (2,0),
+ *            (2,1); only (0,0), (0,1), (1,0), (1,1), (2,2) are stored, as
+ *            one 40-byte record per edge: entry k of edge e at
+ *            gains[5*gain_off[f] + 5*e + k]. The control law still
+ *            multiplies the structural zeros (0.0 * q in the same operation
+ *            order), so both layouts give identical commands, NaN/Inf
+ *            propagation included; the record stream is 40 B per edge
+ *            instead of 72. acl_gain_planes tells which layout a GainMat
+ *            admits.
  */
 typedef struct {
   int32_t n;
@@ -135,6 +147,7 @@ typedef struct {
   const uint64_t* adj;
   const double* gains;
   const int64_t* gain_off;
+  int32_t gain_planes;
 } acl_formations_t;
 
 /* ---- the batched solve --------------------------------------------------
@@ -218,6 +231,15 @@ acl_status_t acl_pack_adjacency(int32_t n, const uint8_t* adj_colmajor,
  * (E = acl_count_edges). */
 acl_status_t acl_pack_gains(int32_t n, const uint8_t* adj_colmajor,
                             const double* gains_colmajor, double* out_planes);
+/* 5 when every edge block of the GainMat has bit-exact +0.0 at (0,2), (1,2),
+ * (2,0), (2,1) (ADMM-designed gains, solver.cpp:49-77), else 9. */
+int32_t acl_gain_planes(int32_t n, const uint8_t* adj_colmajor, const double* gains_colmajor);
+/* acl_pack_gains for either layout: planes = 9 as above, planes = 5 one
+ * record (0,0), (0,1), (1,0), (1,1), (2,2) per edge, 5 E doubles (ACL_ERR if
+ * a block breaks the structure). */
+acl_status_t acl_pack_gains_planes(int32_t n, const uint8_t* adj_colmajor,
+                                   const double* gains_colmajor, int32_t planes,
+                                   double* out_planes);
 
 /* ---- DistCntrl + Safety for given assignments (no auction) ---------------
  * DistCntrl::setAssignment + compute (distcntrl.cpp:38-102) and

@@ -118,6 +118,7 @@ class DeviceBuffer {
  * table"): points [n][3], adjacency bit rows, 9 gain edge planes. */
 struct DeviceFormation {
   int n = 0;
+  int planes = 9;
   bool has_gains = false;
   DeviceBuffer p, adj, gains, off;
 
@@ -136,10 +137,12 @@ struct DeviceFormation {
     off.upload(&zero, 8);
     has_gains = gains_colmajor != nullptr;
     if (has_gains) {
+      // the 40-byte record stream when the blocks have the ADMM structure
+      planes = acl_gain_planes(n, adj_colmajor, gains_colmajor);
       const int64_t E = acl_count_edges(n, adj_colmajor);
-      std::vector<double> planes((size_t)(9 * (E > 0 ? E : 1)), 0.0);
-      check(acl_pack_gains(n, adj_colmajor, gains_colmajor, planes.data()));
-      gains.upload(planes.data(), planes.size() * 8);
+      std::vector<double> pl((size_t)(planes * (E > 0 ? E : 1)), 0.0);
+      check(acl_pack_gains_planes(n, adj_colmajor, gains_colmajor, planes, pl.data()));
+      gains.upload(pl.data(), pl.size() * 8);
     }
   }
 
@@ -151,6 +154,7 @@ struct DeviceFormation {
     F.adj = adj.as<const uint64_t>();
     F.gains = has_gains ? gains.as<const double>() : nullptr;
     F.gain_off = off.as<const int64_t>();
+    F.gain_planes = planes;
     return F;
   }
 };

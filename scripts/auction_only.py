@@ -19,7 +19,8 @@ dev = torch.device("cuda:0")
 gen = torch.Generator(device=dev)
 gen.manual_seed(1)
 w = workload.simform_workload(a.B, a.n, gen, dev)
-T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"])
+T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"],
+                              w["planes"])
 engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=a.control)  # warm
 torch.cuda.synchronize()
 ms = []

@@ -25,7 +25,8 @@ dev = torch.device("cuda:0")
 gen = torch.Generator(device=dev)
 gen.manual_seed(1)
 w = workload.simform_workload(args.B, args.n, gen, dev, F=(args.formations or None))
-T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"])
+T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"],
+                              w["planes"])
 lib = L.lib()
 lib.acl_internal_set_stamps.argtypes = [ct.c_void_p]
 st = torch.zeros((args.B, 16), dtype=torch.int64, device=dev)

@@ -26,7 +26,7 @@ def main(src, dst):
     for C in ("FETCH_SIZE", "WRITE_SIZE"):
         acc = collections.defaultdict(list)
         for r in csv.DictReader(open(os.path.join(src, C + ".csv"))):
-            acc[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]) * 1024.0)
+            acc[r["Kernel_Name"].split("(")[0].replace("void ", "")].append(float(r["Counter_Value"]) * 1024.0)
         for k, v in acc.items():
             vals[k][C] = sum(v) / len(v)
             vals[k]["launches"] = len(v)

@@ -61,3 +61,15 @@ def synth_gains(rng, adj, scale=0.3):
 
 def random_perm(rng, n):
     return rng.permutation(n).astype(np.uint16)
+
+
+def random_block_gains(rng, adj, scale=0.3):
+    """A GainMat with unstructured random 3x3 blocks on the edges (the
+    general 9-plane layout; no ADMM structure)."""
+    n = adj.shape[0]
+    G = np.zeros((3 * n, 3 * n))
+    for i in range(n):
+        for j in range(n):
+            if adj[i, j]:
+                G[3 * i:3 * i + 3, 3 * j:3 * j + 3] = rng.uniform(-scale, scale, (3, 3))
+    return G

@@ -5,6 +5,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 
 import helpers as H
 
@@ -107,3 +108,41 @@ def test_cpp_facade_compiles_and_exports():
     from aclswarm_amd import build
     so = build.build_driver()
     assert hasattr(ct.CDLL(so), "facade_run")
+
+
+def test_gain_planes_detection_and_packing():
+    """acl_gain_planes / acl_pack_gains_planes: the 5-entry record layout exists only
+    for blocks with bit-exact +0.0 at (0,2), (1,2), (2,0), (2,1) (the ADMM
+    assembly, solver.cpp:49-77); its per-edge records hold (0,0) (0,1) (1,0)
+    (1,1) (2,2) of the 9-plane layout."""
+    from aclswarm_amd import _lib as L
+    from aclswarm_amd import engine
+    lib = L.lib()
+    rng = np.random.RandomState(3)
+    n = 12
+    A = (rng.rand(n, n) < 0.5).astype(np.uint8)
+    np.fill_diagonal(A, 0)
+    G = H.synth_gains(rng, A)
+    pts = rng.rand(n, 3)
+    assert engine.gain_planes_host(A, G) == 5
+    _, _, g9, E = engine.pack_formation_host(pts, A, G, 9)
+    _, _, g5, E5 = engine.pack_formation_host(pts, A, G, 5)
+    assert E == E5 == int(A.sum())
+    np.testing.assert_array_equal(g5.reshape(E, 5).T, g9.reshape(9, E)[[0, 1, 3, 4, 8]])
+    # the real formations.yaml gains (ADMM outputs) have the structure
+    _, adj6, gains6, _ = H.swarm6()
+    assert all(engine.gain_planes_host(a, g) == 5 for a, g in zip(adj6, gains6))
+    # a nonzero or a -0.0 in a structural-zero slot of an edge block -> 9
+    i, j = map(int, np.argwhere(A)[0])
+    for val in (1e-300, -0.0):
+        G2 = G.copy()
+        G2[3 * i + 2, 3 * j] = val
+        assert engine.gain_planes_host(A, G2) == 9
+        with pytest.raises(RuntimeError):
+            engine.pack_formation_host(pts, A, G2, 5)
+    # a non-edge block is never read
+    k, l = map(int, np.argwhere(A == 0)[1])
+    G3 = G.copy()
+    G3[3 * k, 3 * l + 2] = 7.0
+    assert engine.gain_planes_host(A, G3) == 5
+    assert lib.acl_pack_gains_planes(n, None, None, 7, None) == 1

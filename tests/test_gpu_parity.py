@@ -339,3 +339,41 @@ def test_align_rt_output(cuda):
         for b in range(B):
             _, Rt_ref = O.prices(q[b], pts_[0], adjs_[0], Pin[b])
             np.testing.assert_array_equal(Rt[b], Rt_ref)
+
+
+def test_gain_layouts_5_and_9_planes(cuda):
+    """ADMM-structured gains: the 5-entry record table gives bit-identical commands to
+    the 9-plane table of the same GainMat; unstructured blocks (9 planes
+    only) match the oracle."""
+    import torch
+    from aclswarm_amd import engine
+    P20, A20 = H.simform("simform20_nc")
+    rng = np.random.RandomState(59)
+    pts = [P20[s, 0] for s in range(4)]
+    adjs = [A20[s] for s in range(4)]
+    B, n = 64, 20
+    fidx = np.arange(B) % 4
+    q = np.stack([H.dense_positions(rng, n, 9.0 + b % 5) for b in range(B)])
+    vel = rng.normal(0, 0.3, (B, n, 3))
+    P_in = np.stack([H.random_perm(rng, n) for _ in range(B)])
+    dev = torch.device("cuda:0")
+
+    def run(gains, planes):
+        T = engine.FormationTable.from_host(pts, adjs, gains, device=dev, planes=planes)
+        assert T.gain_planes == (planes or T.gain_planes)
+        out = engine.solve(T, torch.from_numpy(fidx.astype(np.int32)).to(dev),
+                           torch.from_numpy(q).to(dev), torch.from_numpy(vel).to(dev),
+                           torch.from_numpy(P_in.astype(np.uint16).view(np.int16)).to(dev))
+        torch.cuda.synchronize()
+        return {k: v.cpu().numpy() for k, v in out.items()}, T.gain_planes
+
+    structured = [H.synth_gains(rng, a, scale=1.0) for a in adjs]
+    r5, np5 = run(structured, None)
+    r9, np9 = run(structured, 9)
+    assert (np5, np9) == (5, 9)
+    for k in ("u", "u_safe", "ca_flag", "P_out"):
+        np.testing.assert_array_equal(r5[k], r9[k], err_msg=k)
+    general = [H.random_block_gains(rng, a, scale=1.0) for a in adjs]
+    gpu = _gpu_solve(pts, adjs, general, fidx, q, vel, P_in)
+    ref = _oracle(pts, adjs, general, fidx, q, vel, P_in)
+    _compare(gpu, ref)
