@@ -33,6 +33,9 @@
 namespace acl_amd {
 
 constexpr int kCtlBlock = 256;
+#ifndef ACL_GAIN_WAVES
+#define ACL_GAIN_WAVES 5  // waves per SIMD the record-layout gain kernel is built for
+#endif
 constexpr int kCtlWaves = kCtlBlock / 64;
 
 __host__ __device__ inline int cal16(int x) { return (x + 15) & ~15; }
@@ -98,7 +101,7 @@ __device__ __forceinline__ void saturate(const acl_safety_params_t& sp, double& 
 // NP = 9: general 3x3 gain blocks; NP = 5: the ADMM block structure, the four
 // structural zeros supplied as constants (acl_formations_t::gain_planes)
 template <int NP>
-__global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
+__global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const int NW = (n + 63) >> 6;
@@ -191,12 +194,8 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
     const int vv = uniform ? (int)Pt[rr] : rr;
     const int v = vv;
     const int i = uniform ? rr : (int)myi[vv];
-    const double* gv = P.vel + ((size_t)b * n + vv) * 3;
-    const double vel0 = gv[0], vel1 = gv[1], vel2 = gv[2];
-    const double qv0 = q[3 * vv], qv1 = q[3 * vv + 1], qv2 = q[3 * vv + 2];
-    const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
-    const double Ni = pn[2 * i], Nzi = pn[2 * i + 1];
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+    int nedge = 0;  // the damping term kd (-vel) is added once per edge, below
     // edge of pass t for this lane (-1: none); the gain loads of pass t + 1
     // are issued before pass t's math so that each wave keeps one pass of
     // the gain stream in flight while it computes
@@ -231,6 +230,12 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
     load_planes(e_cur, Lc);
 #pragma unroll 1
     for (int t = 0; t < IT; ++t) {
+      // the vehicle's values are re-read from LDS every pass (short live
+      // ranges: fewer VGPRs, more waves per SIMD)
+      asm volatile("" ::: "memory");
+      const double qv0 = q[3 * vv], qv1 = q[3 * vv + 1], qv2 = q[3 * vv + 2];
+      const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
+      const double Ni = pn[2 * i], Nzi = pn[2 * i + 1];
       int e_nxt = -1;
       double Ln[NP];
       if (t + 1 < IT) e_nxt = edge_of(t + 1);
@@ -277,14 +282,24 @@ __global__ void __launch_bounds__(kCtlBlock, 4) gain_kernel(const CtlParams P) {
         acc0 += A[0] + A[1]; acc1 += A[3] + A[4]; acc2 += A[8];
         (void)up0; (void)up1; (void)up2;
 #else
-        acc0 += g.kp * up0 + g.kd * (-vel0);
-        acc1 += g.kp * up1 + g.kd * (-vel1);
-        acc2 += g.kp * up2 + g.kd * (-vel2);
+        acc0 += g.kp * up0;
+        acc1 += g.kp * up1;
+        acc2 += g.kp * up2;
+        ++nedge;
 #endif
       }
       e_cur = e_nxt;
 #pragma unroll
       for (int k = 0; k < NP; ++k) Lc[k] = Ln[k];
+    }
+    // + kd (-vel) for each of the lane's edges (distcntrl.cpp:85-95 adds it
+    // per neighbour)
+    if (nedge) {
+      const double* gv = P.vel + ((size_t)b * n + vv) * 3;
+      const double cn = (double)nedge;
+      acc0 += cn * (g.kd * (-gv[0]));
+      acc1 += cn * (g.kd * (-gv[1]));
+      acc2 += cn * (g.kd * (-gv[2]));
     }
     // segment sums: each vehicle's S lane partials, in lane order
     red[3 * lane] = acc0; red[3 * lane + 1] = acc1; red[3 * lane + 2] = acc2;

@@ -248,27 +248,26 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
     const int i = act ? Pin[v] : 0;
     unsigned long long r0 = adjF[2 * i], r1 = adjF[2 * i + 1];
     if (i < 64) r0 |= 1ull << i; else r1 |= 1ull << (i - 64);
-    // pass 1: rowwise().sum() of src (p) and dst (q in formation space)
+    // pass 1: rowwise().sum() of src (p) and dst (q in formation space).
+    // Branch-free: the sum starts at -0.0, the additive identity of IEEE
+    // addition (x + -0.0 == x for every x, +0.0 and NaN included), and a
+    // point outside the neighbourhood adds -0.0 -- the same roundings as
+    // Eigen's "first element, then += the rest".
     const double* src = (c < 2) ? (p + c) : (qf + (c - 2));
-    double acc = 0.0;
-    bool first = true;
-    for (int j0 = 0; j0 < n; j0 += 4) {
-      double val[4];
+    double acc = -0.0;
+    for (int jb = 0; jb < n; jb += 32) {
+      const unsigned m = (unsigned)((jb < 64 ? r0 : r1) >> (jb & 63));
 #pragma unroll
-      for (int x = 0; x < 4; ++x) val[x] = (j0 + x < n) ? src[(j0 + x) * 3] : 0.0;
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int j = j0 + x;
-        const bool in = (j < n) && (((j < 64 ? r0 : r1) >> (j & 63)) & 1ull);
-        if (in) {
-          acc = first ? val[x] : acc + val[x];
-          first = false;
-        }
+      for (int x = 0; x < 32; ++x) {
+        const int j = jb + x < n ? jb + x : n - 1;
+        const double val = src[j * 3];
+        acc += ((m >> x) & 1u) ? val : -0.0;  // bits past n are 0
       }
     }
     if (act) sums[8 * v + c] = acc;
   }
   __syncthreads();
+  stamp(P, b, tid, 8);
   {
     const int v = tid >> 2, c = tid & 3;
     const bool act = v < n;
@@ -284,32 +283,26 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
     // sigma = one_over_n * dst_demean * src_demean^T: lazy product (scaled
     // lhs) when k + 4 < 20, GEMM (alpha after the sum) otherwise
     const bool lazy = (k + 4) < 20;
-    double acc = 0.0;
-    bool first = true;
-    for (int j0 = 0; j0 < n; j0 += 4) {
-      double sv[4], dv[4];
+    // branch-free as pass 1: the lazy product starts at its first term
+    // (-0.0 start), the GEMM form at 0.0; excluded points add -0.0; the
+    // lazy scaling multiplies by oon, the other form by 1.0 (exact)
+    const double scale = lazy ? oon : 1.0;
+    double acc = lazy ? -0.0 : 0.0;
+    for (int jb = 0; jb < n; jb += 32) {
+      const unsigned m = (unsigned)((jb < 64 ? r0 : r1) >> (jb & 63));
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int j = (j0 + x < n) ? j0 + x : 0;
-        sv[x] = p[3 * j + sj];
-        dv[x] = qf[3 * j + di];
-      }
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int j = j0 + x;
-        const bool in = (j < n) && (((j < 64 ? r0 : r1) >> (j & 63)) & 1ull);
-        const double s0 = sv[x] - smj;
-        double d0 = dv[x] - dmi;
-        if (lazy) d0 = oon * d0;
-        if (in) {
-          acc = (lazy && first) ? d0 * s0 : acc + d0 * s0;
-          first = false;
-        }
+      for (int x = 0; x < 32; ++x) {
+        const int j = jb + x < n ? jb + x : n - 1;
+        const double s0 = p[3 * j + sj] - smj;
+        const double d0 = scale * (qf[3 * j + di] - dmi);
+        const double pr = d0 * s0;
+        acc += ((m >> x) & 1u) ? pr : -0.0;
       }
     }
     if (act) sums[8 * v + 4 + c] = lazy ? acc : acc * oon;
   }
   __syncthreads();
+  stamp(P, b, tid, 9);
   for (int v = tid; v < n; v += kBlock) {
     const int i = Pin[v];
     unsigned long long r0 = adjF[2 * i], r1 = adjF[2 * i + 1];
@@ -384,9 +377,14 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
   int eff = 0;
   const int max_rounds = 2 * n;  // cbaa_max_iter_ = n * diameter (:50-51)
   const bool ok0 = lane < n, ok1 = lane + 64 < n;
+  // diagnostic counters (stamps only): cycles of the column part and of the
+  // select part as seen by thread 0, dirty columns, outbid vehicles
+  unsigned long long tA = 0, tB = 0, nDirty = 0, nOut = 0;
   for (int r = 1; r <= max_rounds; ++r) {
     const int par = r & 1, npar = par ^ 1;
     const unsigned long long D0 = dmask[2 * par], D1 = dmask[2 * par + 1];
+    const unsigned long long t0 = P.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (P.stamps) nDirty += __popcll(D0) + __popcll(D1);
     // One wave per dirty column j, lanes = vehicles (two chunks of 64). A
     // column none of whose entries changed last round is a fixed point of
     // updateTaskAssignment (it reads only that column, and a select always
@@ -474,6 +472,8 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
       }
     }
     __syncthreads();
+    const unsigned long long t1 = P.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (P.stamps) nOut += __popcll(obm[2 * par]) + __popcll(obm[2 * par + 1]);
     // outbid vehicles re-select on their updated rows (auctioneer.cpp:224)
     {
       if (tid == 0) {
@@ -502,11 +502,20 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
       }
     }
     __syncthreads();
+    if (P.stamps) {
+      const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+      tA += t1 - t0;
+      tB += t2 - t1;
+    }
     const bool changed = (dmask[2 * npar] | dmask[2 * npar + 1]) != 0ull;
     if (changed) eff = r;
     else if (P.early_exit) break;  // fixed point
   }
   stamp(P, b, tid, 4);
+  if (P.stamps && tid == 0) {
+    unsigned long long* st = P.stamps + (size_t)b * 16;
+    st[10] = tA; st[11] = tB; st[12] = nDirty; st[13] = nOut;
+  }
 
   // ---------------- phase 4: adoption --------------------------------------
   // isValidAssignment (auctioneer.cpp:325-343) on each vehicle's table: one

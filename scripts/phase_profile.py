@@ -42,7 +42,12 @@ tot = d.sum(1)
 print(f"per-swarm cycles: mean {tot.mean():.0f}  median {np.median(tot):.0f}")
 for k, nm in enumerate(NAMES):
     print(f"  {nm:16s} mean {d[:, k].mean():10.0f}  share {d[:, k].sum() / tot.sum() * 100:5.1f}%")
-sub = s[:, 8:12]
-for k, nm in enumerate(["  dirty cols A+B", "  select", "  #dirty cols", "  #cols wave0"]):
+# alignment sub-phases: stamps 8 (pass 1 sums) and 9 (pass 2 cross sums)
+a1 = s[:, 8] - s[:, 1]
+a2 = s[:, 9] - s[:, 8]
+a3 = s[:, 2] - s[:, 9]
+for nm, x in (("  align pass 1", a1), ("  align pass 2", a2), ("  align finish", a3)):
+    print(f"  {nm:16s} mean {x.mean():10.0f}")
+sub = s[:, 10:14]
+for k, nm in enumerate(["  cbaa columns", "  cbaa selects", "  #dirty cols", "  #outbid"]):
     print(f"  {nm:16s} mean {sub[:, k].mean():10.0f}")
-print("  wave0 cols needing scan", s[:, 12].mean(), " wave0 in-column cycles", s[:, 13].mean())
