@@ -325,12 +325,16 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
 
   // ---------------- phase 2: prices ---------------------------------------
   {
+    // thread -> fixed task j, vehicles v0, v0 + per, ... (no per-entry
+    // index division; p_j stays in registers)
     int nonfin = 0;
-    for (int k = tid; k < n * n; k += kBlock) {
-      const int v = k / n, j = k - v * n;
+    const int per = kBlock / n;
+    const int j = tid % n, v0 = tid / n;
+    const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
+    for (int v = v0; v0 < per && v < n; v += per) {
+      const int k = v * n + j;
       const double* o = out + 6 * v;
       const double* qv = qf + 3 * Pin[v];
-      const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
       const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
       const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
       const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
@@ -518,38 +522,57 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
   }
 
   // ---------------- phase 4: adoption --------------------------------------
-  // isValidAssignment (auctioneer.cpp:325-343) on each vehicle's table: one
-  // wave per vehicle, lanes over tasks; a permutation <=> every entry < n and
-  // the OR of the one-hot entries has n bits.
+  // AGREE: is every vehicle's table equal to vehicle 0's?
   for (int v = wave; v < n; v += kWaves) {
-    const unsigned char* row = T + v * n;
-    int w[2];
-    unsigned lo[4] = {0u, 0u, 0u, 0u};
-    bool bad = false, diff = false, ismine[2];
+    bool diff = false;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int jj = lane + 64 * c;
-      w[c] = (jj < n) ? row[jj] : -1;
-      ismine[c] = (jj < n) && (w[c] == v);
+      if (jj < n) diff |= T[v * n + jj] != T[jj];
+    }
+    if (__any(diff) && lane == 0) misc[M_AGREE] = 0;
+  }
+  __syncthreads();
+  const bool allagree = misc[M_AGREE] != 0;
+  // isValidAssignment (auctioneer.cpp:325-343) of a table row: one wave,
+  // lanes over tasks; a permutation <=> every entry < n and the OR of the
+  // one-hot entries has n bits
+  auto row_valid = [&](const unsigned char* row) -> bool {
+    unsigned lo[4] = {0u, 0u, 0u, 0u};
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int jj = lane + 64 * c;
       if (jj < n) {
-        if (w[c] >= n) bad = true;
-        else lo[w[c] >> 5] |= 1u << (w[c] & 31);
-        diff |= (w[c] != T[jj]);
+        const int w = row[jj];
+        if (w >= n) bad = true;
+        else lo[w >> 5] |= 1u << (w & 31);
       }
     }
     int cnt = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) cnt += __popc(wave_or_u32(lo[k]));
+    return !__any(bad) && cnt == n;
+  };
+  // with all tables equal, vehicle 0's verdict is every vehicle's (each
+  // wave checks row 0 itself: no further barrier)
+  const bool valid0 = allagree && row_valid(T);
+  for (int v = wave; v < n; v += kWaves) {
+    const unsigned char* row = T + v * n;
+    bool ismine[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int jj = lane + 64 * c;
+      ismine[c] = (jj < n) && (row[jj] == v);
+    }
     const unsigned long long mm0 = __ballot(ismine[0]), mm1 = __ballot(ismine[1]);
-    const bool valid = !__any(bad) && cnt == n && (mm0 | mm1) != 0ull;
-    const bool agree = !__any(diff);
+    const bool valid = (allagree ? valid0 : row_valid(row)) && (mm0 | mm1) != 0ull;
     const int mine = valid ? (mm0 ? __ffsll((long long)mm0) - 1 : 64 + __ffsll((long long)mm1) - 1)
                            : Pin[v];
     if (lane == 0) {
       validv[v] = valid;
       myi[v] = (unsigned char)mine;
       if (!valid) atomicAdd(&misc[M_NINV], 1);
-      if (!agree) misc[M_AGREE] = 0;
       if (mine != Pin[v]) misc[M_CHANGED] = 1;
       P.P_out[(size_t)b * n + v] = (uint16_t)mine;
     }
