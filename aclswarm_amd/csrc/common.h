@@ -174,6 +174,22 @@ __device__ constexpr double kAtanTab[5][6] = {
     {1.0, -1.5, 1.5, 1.0, 9.82793723247329054082e-01, 1.39033110312309984516e-17},
     {0.0, -1.0, 1.0, 0.0, 1.57079632679489655800e+00, 6.12323399573676603587e-17}};
 
+// a * b + C for a compile-time constant C: the constant is built in a
+// reserved SGPR pair by two s_mov_b32 (scalar issue, beside the vector
+// stream) and used by one VOP3 v_fma_f64. Written out because the compiler
+// turns Horner steps with a constant addend into v_mov_b64 + v_fmac_f64 (a
+// vector copy per step) or keeps the constants live in SGPRs (spills).
+template <unsigned long long C>
+__device__ __forceinline__ double fma_k(double a, double b) {
+  double r;
+  asm("s_mov_b32 s98, %3\n\ts_mov_b32 s99, %4\n\tv_fma_f64 %0, %1, %2, s[98:99]"
+      : "=v"(r)
+      : "v"(a), "v"(b), "i"((unsigned)(C & 0xffffffffu)), "i"((unsigned)(C >> 32))
+      : "s98", "s99");
+  return r;
+}
+#define ACL_FMA_K(a, b, c) fma_k<__builtin_bit_cast(unsigned long long, (double)(c))>(a, b)
+
 __device__ __forceinline__ double acl_atan_tab(double x, const double* tab) {
   const double ax = fabs(x);
   const int id = (ax >= 0.4375) + (ax >= 0.6875) + (ax >= 1.1875) + (ax >= 2.4375);
@@ -182,14 +198,18 @@ __device__ __forceinline__ double acl_atan_tab(double x, const double* tab) {
   const double den = __builtin_fma(rw[2], ax, rw[3]);
   const double t = id ? div_nr(num, den) : ax;
   const double z = t * t, w = z * z;
-  const double s1 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, __builtin_fma(w,
-                    __builtin_fma(w, 1.62858201153657823623e-02, 4.97687799461593236017e-02),
-                    6.66107313738753120669e-02), 9.09088713343650656196e-02),
-                    1.42857142725034663711e-01), 3.33333333333329318027e-01);
-  const double s2 = w * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w,
-                    __builtin_fma(w, -3.65315727442169155270e-02, -5.83357013379057348645e-02),
-                    -7.69187620504482999495e-02), -1.11111104054623557880e-01),
-                    -1.99999999998764832476e-01);
+  // fdlibm's coefficients, Horner in w
+  double p1 = ACL_FMA_K(w, 1.62858201153657823623e-02, 4.97687799461593236017e-02);
+  p1 = ACL_FMA_K(w, p1, 6.66107313738753120669e-02);
+  p1 = ACL_FMA_K(w, p1, 9.09088713343650656196e-02);
+  p1 = ACL_FMA_K(w, p1, 1.42857142725034663711e-01);
+  p1 = ACL_FMA_K(w, p1, 3.33333333333329318027e-01);
+  double p2 = ACL_FMA_K(w, -3.65315727442169155270e-02, -5.83357013379057348645e-02);
+  p2 = ACL_FMA_K(w, p2, -7.69187620504482999495e-02);
+  p2 = ACL_FMA_K(w, p2, -1.11111104054623557880e-01);
+  p2 = ACL_FMA_K(w, p2, -1.99999999998764832476e-01);
+  const double s1 = z * p1;
+  const double s2 = w * p2;
   const double r = id ? rw[4] - (__builtin_fma(t, s1 + s2, -rw[5]) - t)
                       : __builtin_fma(-t, s1 + s2, t);
   return (ax == __builtin_inf()) ? copysign(1.57079632679489655800e+00, x) : copysign(r, x);
