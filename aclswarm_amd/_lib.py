@@ -33,6 +33,7 @@ EXPORTS = (
     "acl_max_vehicles", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
     "acl_pack_gains", "acl_gain_planes", "acl_pack_gains_planes", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
     "acl_control_batch", "acl_write_assignment_log", "acl_read_assignment_log",
+    "acl_hungarian_batch",
     "acl_malloc", "acl_free", "acl_memcpy_h2d", "acl_memcpy_d2h", "acl_memset",
     "acl_stream_synchronize", "acl_last_error",
 )
@@ -82,6 +83,17 @@ class ControlArgs(ct.Structure):
                 ("workspace", ct.c_void_p), ("cntrl", CntrlGains), ("safety", SafetyParams)]
 
 
+class HungarianArgs(ct.Structure):
+    """acl_hungarian_args_t (assignment.py:94-137, batched)."""
+    _fields_ = [("B", ct.c_int32), ("fidx", ct.c_void_p), ("q", ct.c_void_p),
+                ("P_last", ct.c_void_p), ("P_cmp", ct.c_void_p), ("P_opt", ct.c_void_p),
+                ("cost", ct.c_void_p), ("align_Rt", ct.c_void_p), ("status", ct.c_void_p)]
+
+
+HUNG_BAD_INPUT = 0x01
+HUNG_NONFINITE = 0x02
+HUNG_CMP_INVALID = 0x04
+
 _lib = None
 
 
@@ -118,6 +130,8 @@ def lib():
     L.acl_admm_solve_batch.restype = ct.c_int
     L.acl_control_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(ControlArgs), VP]
     L.acl_control_batch.restype = ct.c_int
+    L.acl_hungarian_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(HungarianArgs), VP]
+    L.acl_hungarian_batch.restype = ct.c_int
     L.acl_write_assignment_log.argtypes = [ct.c_char_p, I32, VP, VP, VP, VP, VP, VP]
     L.acl_write_assignment_log.restype = ct.c_int
     L.acl_read_assignment_log.argtypes = [ct.c_char_p, ct.POINTER(I32), VP, VP, VP, VP, VP, VP]

@@ -217,6 +217,38 @@ def control(table, fidx, q, vel, P, cntrl=None, safety=None, stream=None):
     return out
 
 
+def hungarian(table, fidx, q, P_last=None, P_cmp=None, want_Rt=False, stream=None):
+    """acl_hungarian_batch: the reference's centralized comparator
+    (assignment.py:94-137 find_optimal_assignment) for B swarms. P_last /
+    P_cmp [B][n] int16 holding uint16 bits (None = identity / not priced).
+    Returns P_opt [B][n] int16, cost [B][2] f64, status [B] i32 and, with
+    want_Rt, align_Rt [B][4] (device tensors)."""
+    lib = L.lib()
+    B, n = int(q.shape[0]), table.n
+    dev = q.device
+    out = {
+        "P_opt": torch.empty((B, n), dtype=torch.int16, device=dev),
+        "cost": torch.empty((B, 2), dtype=torch.float64, device=dev),
+        "status": torch.empty((B,), dtype=torch.int32, device=dev),
+    }
+    if want_Rt:
+        out["align_Rt"] = torch.empty((B, 4), dtype=torch.float64, device=dev)
+    a = L.HungarianArgs()
+    a.B = B
+    a.fidx = fidx.data_ptr(); a.q = q.data_ptr()
+    a.P_last = P_last.data_ptr() if P_last is not None else None
+    a.P_cmp = P_cmp.data_ptr() if P_cmp is not None else None
+    a.P_opt = out["P_opt"].data_ptr(); a.cost = out["cost"].data_ptr()
+    a.align_Rt = out["align_Rt"].data_ptr() if want_Rt else None
+    a.status = out["status"].data_ptr()
+    F = table.struct()
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    L.check(lib.acl_hungarian_batch(ct.byref(F), ct.byref(a), ct.c_void_p(stream)),
+            "acl_hungarian_batch")
+    return out
+
+
 def write_assignment_log(path, q, adj, lastP, p, align_Rt, P):
     """Auctioneer::logAssignment's binary record (auctioneer.cpp:577-597),
     host arrays: q, p [n][3]; adj [n][n] (adj[i][j] = adjmat(i,j)); lastP, P

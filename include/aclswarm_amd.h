@@ -285,6 +285,48 @@ acl_status_t acl_read_assignment_log(const char* path, int32_t* n, double* q,
                                      uint8_t* adj_colmajor, uint16_t* lastP, double* p,
                                      double* aligned, uint16_t* P);
 
+/* ---- centralized Hungarian comparator -----------------
+ * Replaces aclswarm/src/aclswarm/assignment.py:94-137
+ * find_optimal_assignment(q, p, last), the reference's centralized baseline
+ * for CBAA: align the formation to the whole swarm with 2-D Arun
+ * (assignment.py:15-92, using the last assignment), cost S[v][j] =
+ * ||q_v - paligned_j|| (scipy cdist), P = linear_sum_assignment(S)[1]
+ * (SciPy's Crouse shortest-augmenting-path LSAP, tie-breaking included).
+ * One wavefront per swarm; n <= 512. Device pointers:
+ *   fidx    [B]        formation of swarm b (p of the formation table is used)
+ *   q       [B][n][3]  vehicle positions
+ *   P_last  [B][n]     last assignment, vehicle -> formation point (NULL =
+ *                      identity, assignment.py:112-113)
+ *   P_cmp   [B][n]     optional assignment to price under the same S (e.g.
+ *                      acl_solve_batch's P_out): the optimality gap of CBAA
+ *   P_opt   [B][n]     out: optimal vehicle -> formation point (0xFFFF on
+ *                      BAD_INPUT / NONFINITE)
+ *   cost    [B][2]     out: sum_v S[v][P_opt[v]], sum_v S[v][P_cmp[v]]
+ *                      (NaN when P_cmp is NULL or not a permutation)
+ *   align_Rt[B][4]     optional out {c, s, tx, ty}: paligned = (c px - s py
+ *                      + tx, s px + c py + ty, pz)
+ *   status  [B]        out: 0 or ACL_HUNG_* bits
+ * Stream-ordered, no workspace. */
+#define ACL_HUNG_BAD_INPUT   0x01 /* P_last not a permutation: swarm skipped */
+#define ACL_HUNG_NONFINITE   0x02 /* a cost is NaN / -inf, or the matrix is
+                                     infeasible (scipy raises ValueError) */
+#define ACL_HUNG_CMP_INVALID 0x04 /* P_cmp given but not a permutation */
+
+typedef struct {
+  int32_t B;
+  const int32_t* fidx;
+  const double* q;
+  const uint16_t* P_last;
+  const uint16_t* P_cmp;
+  uint16_t* P_opt;
+  double* cost;
+  double* align_Rt;
+  int32_t* status;
+} acl_hungarian_args_t;
+
+acl_status_t acl_hungarian_batch(const acl_formations_t* formations,
+                                 const acl_hungarian_args_t* args, void* stream);
+
 /* ---- ADMM formation-gain design (admm::Solver::solve, solver.cpp:28-79) -
  * F formations of n points: pts [F][3][n] column-major 3 x n per formation
  * (Eigen::Matrix<double,3,Dynamic>), adj [F][n][n] f64 (symmetric 0/1),

@@ -114,6 +114,14 @@ double orc_solve_batch(int B, int n, int nthreads, const int32_t* fidx,
                        uint16_t* P_out, acl_swarm_status_t* st, double* u,
                        double* u_safe, uint8_t* ca);
 
+/* ---- centralized comparator (hungarian_oracle.c) -------------------------
+ * assignment.py:15-137 restated; see hungarian_oracle.c for the pinning. */
+int orc_lsap(int n, const double* cost, int32_t* col4row);
+void orc_arun2(int n, const double* qq, const double* p, double Rt[4]);
+int orc_hungarian(int n, const double* q, const double* p,
+                  const uint16_t* P_last, const uint16_t* P_cmp,
+                  uint16_t* P_opt, double cost[2], double* Rt_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -81,6 +81,11 @@ def lib():
                                       ct.POINTER(SafetyParams), ct.c_int, U16,
                                       ct.c_void_p, D, D, U8]
         L.orc_solve_batch.restype = ct.c_double
+        L.orc_lsap.argtypes = [ct.c_int, D, I32]
+        L.orc_lsap.restype = ct.c_int
+        L.orc_arun2.argtypes = [ct.c_int, D, D, D]
+        L.orc_hungarian.argtypes = [ct.c_int, D, D, U16, U16, U16, D, D]
+        L.orc_hungarian.restype = ct.c_int
         _lib = L
     return _lib
 
@@ -199,3 +204,30 @@ def solve_batch(fidx, q, vel, p, adj, gains, P_in, nthreads=1, g=None, s=None,
                               st.ctypes.data_as(ct.c_void_p), _p(u, ct.c_double),
                               _p(us, ct.c_double), _p(ca, ct.c_uint8))
     return dict(P_out=P_out, status=st, u=u, u_safe=us, ca=ca), t
+
+
+def lsap(C):
+    """orc_lsap: SciPy's linear_sum_assignment restated (square, minimise).
+    Returns col4row (int32) or None when SciPy would raise."""
+    C = _c(C, np.float64)
+    n = C.shape[0]
+    out = np.empty(n, np.int32)
+    rc = lib().orc_lsap(n, _p(C, ct.c_double), _p(out, ct.c_int32))
+    return None if rc else out
+
+
+def hungarian(q, p, P_last=None, P_cmp=None):
+    """orc_hungarian: assignment.py:94-137 for one swarm. q, p [n][3].
+    Returns (P_opt u16, cost[2], Rt[4], status)."""
+    q = _c(q, np.float64); p = _c(p, np.float64)
+    n = q.shape[0]
+    Pl = None if P_last is None else _c(P_last, np.uint16)
+    Pc = None if P_cmp is None else _c(P_cmp, np.uint16)
+    P = np.empty(n, np.uint16)
+    cost = np.empty(2, np.float64)
+    Rt = np.full(4, np.nan)
+    st = lib().orc_hungarian(n, _p(q, ct.c_double), _p(p, ct.c_double),
+                             None if Pl is None else _p(Pl, ct.c_uint16),
+                             None if Pc is None else _p(Pc, ct.c_uint16),
+                             _p(P, ct.c_uint16), _p(cost, ct.c_double), _p(Rt, ct.c_double))
+    return P, cost, Rt, st
