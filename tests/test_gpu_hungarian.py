@@ -143,3 +143,19 @@ def test_cbaa_optimality_gap():
     g = _check_vs_oracle(list(points), fidx, q, P_in, P_cbaa)
     assert (g["status"] == 0).all()
     assert (g["cost"][:, 1] >= g["cost"][:, 0] * (1 - 1e-12)).all()
+
+
+def test_reference_shaped_module():
+    # aclswarm_amd.assignment mirrors assignment.py's names and returns
+    from aclswarm_amd import assignment as A
+    with open(os.path.join(HERE, "golden", "hungarian_golden.json")) as fh:
+        cases = json.load(fh)["cases"][:4]
+    for c in cases:
+        q, p = np.array(c["q"]).T, np.array(c["p"]).T   # d x n, as the reference takes
+        P, pal = A.find_optimal_assignment(q, p, c["last"])
+        assert P == c["P"]
+        np.testing.assert_allclose(pal, np.array(c["paligned"]).T, rtol=0, atol=1e-12)
+        np.testing.assert_allclose(A.align(q, p).shape, p.shape)
+    q, p = np.array(cases[0]["q"]).T, np.array(cases[0]["p"]).T
+    with pytest.raises(ValueError):
+        A.find_optimal_assignment(q, p, [0] * q.shape[1])
