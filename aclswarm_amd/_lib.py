@@ -34,6 +34,7 @@ EXPORTS = (
     "acl_pack_gains", "acl_gain_planes", "acl_pack_gains_planes", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
     "acl_control_batch", "acl_write_assignment_log", "acl_read_assignment_log",
     "acl_hungarian_batch",
+    "acl_default_episode_params", "acl_episode_workspace_bytes", "acl_episode_batch",
     "acl_malloc", "acl_free", "acl_memcpy_h2d", "acl_memcpy_d2h", "acl_memset",
     "acl_stream_synchronize", "acl_last_error",
 )
@@ -90,6 +91,35 @@ class HungarianArgs(ct.Structure):
                 ("cost", ct.c_void_p), ("align_Rt", ct.c_void_p), ("status", ct.c_void_p)]
 
 
+class EpisodeParams(ct.Structure):
+    """acl_episode_params_t (coordination.launch:6,24-25, safety.cpp:45-46,
+    trial.sh:96, supervisor.py:47,61-62,121)."""
+    _fields_ = [("control_dt", ct.c_double), ("auction_every", ct.c_int32),
+                ("sample_every", ct.c_int32), ("bufflen", ct.c_int32),
+                ("reserved", ct.c_int32), ("max_accel_xy", ct.c_double),
+                ("max_accel_z", ct.c_double), ("bounds_min", ct.c_double * 3),
+                ("bounds_max", ct.c_double * 3), ("orig_zero_vel_thr", ct.c_double),
+                ("avg_active_ca_thr", ct.c_double)]
+
+
+EPISODE_STATUS_DTYPE = np.dtype([("converged_step", "<i4"), ("gridlock_step", "<i4"),
+                                 ("converged", "<i4"), ("gridlocked", "<i4"),
+                                 ("n_auctions", "<u2"), ("n_invalid", "<u2"),
+                                 ("n_skipped", "<u2"), ("n_disagree", "<u2"),
+                                 ("n_samples", "<u4"), ("n_ca_steps", "<u4")])
+
+
+class EpisodeArgs(ct.Structure):
+    """acl_episode_args_t (closed-loop batched episodes)."""
+    _fields_ = [("B", ct.c_int32), ("fidx", ct.c_void_p), ("q", ct.c_void_p),
+                ("vel", ct.c_void_p), ("P", ct.c_void_p), ("flush", ct.c_void_p),
+                ("est", ct.c_void_p), ("ring_u", ct.c_void_p), ("ring_ca", ct.c_void_p),
+                ("step0", ct.c_int32), ("steps", ct.c_int32), ("q_hist", ct.c_void_p),
+                ("vel_hist", ct.c_void_p), ("u_hist", ct.c_void_p), ("ca_hist", ct.c_void_p), ("P_hist", ct.c_void_p),
+                ("workspace", ct.c_void_p), ("cntrl", CntrlGains), ("safety", SafetyParams),
+                ("ep", EpisodeParams)]
+
+
 HUNG_BAD_INPUT = 0x01
 HUNG_NONFINITE = 0x02
 HUNG_CMP_INVALID = 0x04
@@ -130,6 +160,12 @@ def lib():
     L.acl_admm_solve_batch.restype = ct.c_int
     L.acl_control_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(ControlArgs), VP]
     L.acl_control_batch.restype = ct.c_int
+    L.acl_default_episode_params.argtypes = [ct.POINTER(EpisodeParams)]
+    L.acl_default_episode_params.restype = None
+    L.acl_episode_workspace_bytes.argtypes = [I32, I32]
+    L.acl_episode_workspace_bytes.restype = SZ
+    L.acl_episode_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(EpisodeArgs), VP]
+    L.acl_episode_batch.restype = ct.c_int
     L.acl_hungarian_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(HungarianArgs), VP]
     L.acl_hungarian_batch.restype = ct.c_int
     L.acl_write_assignment_log.argtypes = [ct.c_char_p, I32, VP, VP, VP, VP, VP, VP]
@@ -166,6 +202,12 @@ def check(rc, what="aclswarm_amd"):
     if rc != ACL_OK:
         msg = lib().acl_last_error().decode(errors="replace")
         raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def default_episode_params():
+    e = EpisodeParams()
+    lib().acl_default_episode_params(ct.byref(e))
+    return e
 
 
 def default_gains():

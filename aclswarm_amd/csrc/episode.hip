@@ -1,0 +1,295 @@
+// episode.hip -- closed-loop batched episodes.
+//
+// acl_episode_batch flies B swarms for a number of control periods in
+// lockstep, reusing the decision-loop kernels of acl_solve_batch /
+// acl_control_batch and adding two small kernels:
+//
+//   adopt_kernel   after an auto-auction: the flush/skip rule of
+//                  CoordinationROS::autoauctionCb (coordination_ros.cpp:339-
+//                  345) and adoption of a valid, agreed assignment
+//                  (auctioneer.cpp:283-292, newAssignmentCb :284-303)
+//   traj_kernel    Safety::makeSafeTraj (safety.cpp:330-408) with the
+//                  utils::rateLimit / clamp helpers (utils.h:213-264), the
+//                  perfectly tracking vehicle (q <- goal.pos, vel <-
+//                  goal.vel), and the supervisor's windowed predicates
+//                  has_converged / has_gridlocked (supervisor.py:297-337)
+//
+// One workgroup per swarm, threads over vehicles. Both kernels are O(n) per
+// swarm and latency-bound; the step's time is the gain stream of the control
+// stage (control.hip). Compiled with -ffp-contract=off: every operation is
+// one IEEE rounding, so the trajectory step and the supervisor's window sums
+// are bit-identical to the restatement in oracle/episode_oracle.py.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/aclswarm_amd.h"
+#include "control_params.h"
+
+extern "C" acl_status_t acl__set_error(const char* msg);
+
+namespace acl_amd {
+
+constexpr int kEpBlock = 128;
+
+// Episode workspace: the solve/control workspace, then the auction's output
+// and the control stage's output of the current step.
+struct EpLayout {
+  size_t solve, Pnew, st, cst, u, us, ca, total;
+};
+
+inline EpLayout ep_layout(int n, int B) {
+  EpLayout L;
+  const size_t nb = (size_t)n, bb = (size_t)B;
+  size_t o = 0;
+  L.solve = o; o = ws_al(o + ws_layout(n, B).total);
+  L.Pnew = o;  o = ws_al(o + bb * nb * 2);
+  L.st = o;    o = ws_al(o + bb * sizeof(acl_swarm_status_t));
+  L.cst = o;   o = ws_al(o + bb * sizeof(acl_swarm_status_t));
+  L.u = o;     o = ws_al(o + bb * nb * 3 * 8);
+  L.us = o;    o = ws_al(o + bb * nb * 3 * 8);
+  L.ca = o;    o = ws_al(o + bb * nb);
+  L.total = o;
+  return L;
+}
+
+// autoauctionCb after the auction of this tick: a swarm flagged by the last
+// auction (didConvergeOnInvalidAssignment) flushes and skips this one;
+// otherwise an agreed valid result is adopted, an agreed invalid one sets
+// the flag, and a disagreeing swarm keeps its assignment.
+__global__ void __launch_bounds__(64) adopt_kernel(int n, uint16_t* P, const uint16_t* Pnew,
+                                                   const acl_swarm_status_t* st, uint8_t* flush,
+                                                   acl_episode_status_t* est) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const bool fl = flush[b] != 0;
+  const uint32_t flags = st[b].flags;
+  const bool valid = (flags & ACL_SWARM_VALID) != 0, agree = (flags & ACL_SWARM_AGREE) != 0;
+  if (tid == 0) {
+    acl_episode_status_t e = est[b];
+    if (fl) {
+      flush[b] = 0;
+      ++e.n_skipped;
+    } else {
+      ++e.n_auctions;
+      if (agree && !valid) {
+        flush[b] = 1;
+        ++e.n_invalid;
+      } else if (!agree) {
+        ++e.n_disagree;
+      }
+    }
+    est[b] = e;
+  }
+  if (!fl && agree && valid)
+    for (int v = tid; v < n; v += 64) P[(size_t)b * n + v] = Pnew[(size_t)b * n + v];
+}
+
+struct TrajParams {
+  int n, B, step, k, tick;
+  double* q;
+  double* vel;
+  const double* u;
+  const double* us;
+  const uint8_t* ca;
+  const uint16_t* P;
+  acl_episode_status_t* est;
+  double* ring_u;
+  uint8_t* ring_ca;
+  double* q_hist;
+  double* vel_hist;
+  double* u_hist;
+  uint8_t* ca_hist;
+  uint16_t* P_hist;
+  acl_episode_params_t ep;
+};
+
+// utils::rateLimit (utils.h:254-264)
+__device__ __forceinline__ void rate_limit(double dt, double lo, double hi, double v0, double& v1) {
+  const double upper = v0 + hi * dt;
+  const double lower = v0 + lo * dt;
+  if (v1 > upper) v1 = upper;
+  if (v1 < lower) v1 = lower;
+}
+
+// utils::clamp (utils.h:213-227)
+__device__ __forceinline__ double clamp_ind(double val, double lower, double upper, bool& clamped) {
+  if (val < lower) { clamped = true; return lower; }
+  if (val > upper) { clamped = true; return upper; }
+  clamped = false;
+  return val;
+}
+
+__global__ void __launch_bounds__(kEpBlock) traj_kernel(const TrajParams T) {
+  __shared__ int s_all_conv, s_any_grid, s_nca;
+  const int n = T.n, b = blockIdx.x, tid = threadIdx.x;
+  const acl_episode_params_t ep = T.ep;
+  if (tid == 0) {
+    s_all_conv = 1;
+    s_any_grid = 0;
+    s_nca = 0;
+  }
+  __syncthreads();
+  const uint32_t m0 = T.est[b].n_samples;  // ticks before this one
+  const int L = ep.bufflen;
+  const double dt = ep.control_dt;
+  int nca = 0;
+  for (int v = tid; v < n; v += kEpBlock) {
+    const size_t iv = (size_t)b * n + v;
+    double gp[3] = {T.q[3 * iv], T.q[3 * iv + 1], T.q[3 * iv + 2]};
+    double gv[3] = {T.vel[3 * iv], T.vel[3 * iv + 1], T.vel[3 * iv + 2]};
+    double c[3] = {T.us[3 * iv], T.us[3 * iv + 1], T.us[3 * iv + 2]};
+    // Safety::makeSafeTraj (safety.cpp:330-408)
+    const double amax[3] = {ep.max_accel_xy, ep.max_accel_xy, ep.max_accel_z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) rate_limit(dt, -amax[a], amax[a], gv[a], c[a]);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const double next = gp[a] + c[a] * dt;
+      bool clamped = false;
+      // std::min / std::max (b < a ? b : a, a < b ? b : a)
+      const double lo = gp[a] < ep.bounds_min[a] ? gp[a] : ep.bounds_min[a];
+      const double hi = ep.bounds_max[a] < gp[a] ? gp[a] : ep.bounds_max[a];
+      gp[a] = clamp_ind(next, lo, hi, clamped);
+      if (clamped) {
+        c[a] = 0.0;
+        rate_limit(dt, -amax[a], amax[a], gv[a], c[a]);
+      }
+      gv[a] = c[a];
+    }
+    // the vehicle tracks its goal exactly
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      T.q[3 * iv + a] = gp[a];
+      T.vel[3 * iv + a] = gv[a];
+    }
+    const uint8_t cav = T.ca[iv];
+    nca += cav != 0;
+    const size_t ih = (size_t)T.k * T.B * n + iv;
+    if (T.q_hist)
+      for (int a = 0; a < 3; ++a) T.q_hist[3 * ih + a] = gp[a];
+    if (T.vel_hist)
+      for (int a = 0; a < 3; ++a) T.vel_hist[3 * ih + a] = gv[a];
+    if (T.u_hist)
+      for (int a = 0; a < 3; ++a) T.u_hist[3 * ih + a] = T.u[3 * iv + a];
+    if (T.ca_hist) T.ca_hist[ih] = cav;
+    if (T.P_hist) T.P_hist[ih] = T.P[iv];
+    if (T.tick) {
+      // supervisor tick: |voriggoal| (the DistCntrl command) and the CA flag
+      // enter the ring; with a full window, the per-vehicle means
+      const double u0 = T.u[3 * iv], u1 = T.u[3 * iv + 1], u2 = T.u[3 * iv + 2];
+      const double speed = sqrt((u0 * u0 + u1 * u1) + u2 * u2);
+      double* ru = T.ring_u + (size_t)b * L * n;
+      uint8_t* rc = T.ring_ca + (size_t)b * L * n;
+      ru[(size_t)(m0 % L) * n + v] = speed;
+      rc[(size_t)(m0 % L) * n + v] = cav;
+      const uint32_t m = m0 + 1;
+      if (m >= (uint32_t)L) {
+        double su = 0.0, sc = 0.0;
+        for (int i = 0; i < L; ++i) {  // oldest -> newest (deque order)
+          const size_t slot = (size_t)((m - L + i) % L) * n + v;
+          su = su + ru[slot];
+          sc = sc + (double)rc[slot];
+        }
+        const double mu = su / (double)L, mc = sc / (double)L;
+        if (!(mu < ep.orig_zero_vel_thr)) atomicAnd(&s_all_conv, 0);
+        if (mc > ep.avg_active_ca_thr) atomicOr(&s_any_grid, 1);
+      }
+    }
+  }
+  if (nca) atomicAdd(&s_nca, nca);
+  __syncthreads();
+  if (tid == 0) {
+    acl_episode_status_t e = T.est[b];
+    e.n_ca_steps += (uint32_t)s_nca;
+    if (T.tick) {
+      e.n_samples = m0 + 1;
+      if (m0 + 1 >= (uint32_t)L) {
+        e.converged = s_all_conv;
+        e.gridlocked = s_any_grid;
+        if (s_all_conv && e.converged_step < 0) e.converged_step = T.step;
+        if (s_any_grid && e.gridlock_step < 0) e.gridlock_step = T.step;
+      }
+    }
+    T.est[b] = e;
+  }
+}
+
+}  // namespace acl_amd
+
+extern "C" void acl_default_episode_params(acl_episode_params_t* e) {
+  e->control_dt = 0.01;
+  e->auction_every = 120;
+  e->sample_every = 2;
+  e->bufflen = 50;
+  e->reserved = 0;
+  e->max_accel_xy = 0.5;
+  e->max_accel_z = 0.8;
+  e->bounds_min[0] = -100.0; e->bounds_min[1] = -100.0; e->bounds_min[2] = 0.0;
+  e->bounds_max[0] = 100.0;  e->bounds_max[1] = 100.0;  e->bounds_max[2] = 30.0;
+  e->orig_zero_vel_thr = 1.0;
+  e->avg_active_ca_thr = 0.95;
+}
+
+extern "C" size_t acl_episode_workspace_bytes(int32_t n, int32_t B) {
+  if (n < 1 || B < 0) return 0;
+  return acl_amd::ep_layout(n, B).total;
+}
+
+extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_episode_args_t* a,
+                                          void* stream) {
+  using namespace acl_amd;
+  if (!F || !a) return acl__set_error("acl_episode_batch: null argument");
+  const int n = F->n, B = a->B;
+  if (n < 1 || n > kMaxNWide) return acl__set_error("acl_episode_batch: n out of range [1, 512]");
+  if (B < 0 || a->steps < 0 || a->step0 < 0)
+    return acl__set_error("acl_episode_batch: B, steps and step0 must be >= 0");
+  if (B == 0 || a->steps == 0) return ACL_OK;
+  if (!a->fidx || !a->q || !a->vel || !a->P || !a->flush || !a->est || !a->ring_u ||
+      !a->ring_ca || !a->workspace)
+    return acl__set_error("acl_episode_batch: required pointer is NULL");
+  const acl_episode_params_t& ep = a->ep;
+  if (ep.auction_every < 1 || ep.sample_every < 1 || ep.bufflen < 1 || !(ep.control_dt > 0.0))
+    return acl__set_error("acl_episode_batch: auction_every, sample_every, bufflen must be "
+                          ">= 1 and control_dt > 0");
+  const EpLayout W = ep_layout(n, B);
+  unsigned char* ws = (unsigned char*)a->workspace;
+  hipStream_t s = (hipStream_t)stream;
+  uint16_t* Pnew = reinterpret_cast<uint16_t*>(ws + W.Pnew);
+  acl_swarm_status_t* st = reinterpret_cast<acl_swarm_status_t*>(ws + W.st);
+  double* u = reinterpret_cast<double*>(ws + W.u);
+  double* us = reinterpret_cast<double*>(ws + W.us);
+  uint8_t* ca = ws + W.ca;
+
+  acl_solve_args_t sa = {};
+  sa.B = B; sa.fidx = a->fidx; sa.q = a->q; sa.vel = a->vel; sa.P_in = a->P; sa.P_out = Pnew;
+  sa.status = st; sa.workspace = ws + W.solve;
+  sa.cntrl = a->cntrl; sa.safety = a->safety; sa.early_exit = 1; sa.do_control = 0;
+  acl_control_args_t cs = {};
+  cs.B = B; cs.fidx = a->fidx; cs.q = a->q; cs.vel = a->vel; cs.P = a->P;
+  cs.u = u; cs.u_safe = us; cs.ca_flag = ca;
+  cs.status = reinterpret_cast<acl_swarm_status_t*>(ws + W.cst);
+  cs.workspace = ws + W.solve; cs.cntrl = a->cntrl; cs.safety = a->safety;
+
+  TrajParams T;
+  T.n = n; T.B = B; T.q = a->q; T.vel = a->vel; T.u = u; T.us = us; T.ca = ca; T.P = a->P;
+  T.est = a->est; T.ring_u = a->ring_u; T.ring_ca = a->ring_ca;
+  T.q_hist = a->q_hist; T.vel_hist = a->vel_hist; T.u_hist = a->u_hist; T.ca_hist = a->ca_hist; T.P_hist = a->P_hist;
+  T.ep = ep;
+  for (int k = 0; k < a->steps; ++k) {
+    const int step = a->step0 + k;
+    if (step % ep.auction_every == 0) {
+      const acl_status_t r = acl_solve_batch(F, &sa, stream);
+      if (r != ACL_OK) return r;
+      hipLaunchKernelGGL(adopt_kernel, dim3(B), dim3(64), 0, s, n, a->P, Pnew, st, a->flush,
+                         a->est);
+      if (hipGetLastError() != hipSuccess) return acl__set_error("adopt_kernel launch failed");
+    }
+    const acl_status_t r = acl_control_batch(F, &cs, stream);
+    if (r != ACL_OK) return r;
+    T.step = step;
+    T.k = k;
+    T.tick = (step % ep.sample_every) == 0;
+    hipLaunchKernelGGL(traj_kernel, dim3(B), dim3(kEpBlock), 0, s, T);
+    if (hipGetLastError() != hipSuccess) return acl__set_error("traj_kernel launch failed");
+  }
+  return ACL_OK;
+}

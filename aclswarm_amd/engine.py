@@ -282,3 +282,77 @@ def read_assignment_log(path):
                                         r["P"].ctypes.data), "read_assignment_log")
     r["adj"] = r.pop("adj_cm").T.copy()
     return r
+
+
+class Episode:
+    """Closed-loop batched episodes (acl_episode_batch):
+    the per-swarm state that persists across calls -- positions, velocities,
+    carried assignment, the flush flag, the supervisor's ring buffers and the
+    episode counters -- so an episode can be flown in chunks of steps.
+
+    fidx [B] int32, q/vel [B][n][3] f64, P [B][n] int16 (uint16 bits), all on
+    the device; they are copied, the caller's tensors are not modified.
+    """
+
+    def __init__(self, table, fidx, q, vel, P, params=None, cntrl=None, safety=None):
+        dev = q.device
+        self.table = table
+        self.B, self.n = int(q.shape[0]), table.n
+        self.ep = params or L.default_episode_params()
+        self.cntrl = cntrl or L.default_gains()
+        self.safety = safety or L.default_safety()
+        self.fidx = fidx.contiguous()
+        self.q = q.clone().contiguous()
+        self.vel = vel.clone().contiguous()
+        self.P = P.clone().contiguous()
+        self.flush = torch.zeros(self.B, dtype=torch.uint8, device=dev)
+        est = np.zeros(self.B, L.EPISODE_STATUS_DTYPE)
+        est["converged_step"] = -1
+        est["gridlock_step"] = -1
+        self.est = torch.from_numpy(est.view(np.uint8).reshape(self.B, -1).copy()).to(dev)
+        Lb = int(self.ep.bufflen)
+        self.ring_u = torch.zeros((self.B, Lb, self.n), dtype=torch.float64, device=dev)
+        self.ring_ca = torch.zeros((self.B, Lb, self.n), dtype=torch.uint8, device=dev)
+        need = int(L.lib().acl_episode_workspace_bytes(self.n, self.B))
+        self.ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        self.step = 0
+
+    def run(self, steps, history=False, stream=None):
+        """Fly `steps` control periods. With history=True returns per-step
+        device tensors q/vel/u [steps][B][n][3], ca [steps][B][n],
+        P [steps][B][n] (int16); else None."""
+        dev = self.q.device
+        B, n = self.B, self.n
+        hist = None
+        if history:
+            hist = {
+                "q": torch.empty((steps, B, n, 3), dtype=torch.float64, device=dev),
+                "vel": torch.empty((steps, B, n, 3), dtype=torch.float64, device=dev),
+                "u": torch.empty((steps, B, n, 3), dtype=torch.float64, device=dev),
+                "ca": torch.empty((steps, B, n), dtype=torch.uint8, device=dev),
+                "P": torch.empty((steps, B, n), dtype=torch.int16, device=dev),
+            }
+        a = L.EpisodeArgs()
+        a.B = B
+        a.fidx = self.fidx.data_ptr(); a.q = self.q.data_ptr(); a.vel = self.vel.data_ptr()
+        a.P = self.P.data_ptr(); a.flush = self.flush.data_ptr(); a.est = self.est.data_ptr()
+        a.ring_u = self.ring_u.data_ptr(); a.ring_ca = self.ring_ca.data_ptr()
+        a.step0 = self.step; a.steps = steps
+        if hist is not None:
+            a.q_hist = hist["q"].data_ptr(); a.vel_hist = hist["vel"].data_ptr()
+            a.u_hist = hist["u"].data_ptr(); a.ca_hist = hist["ca"].data_ptr()
+            a.P_hist = hist["P"].data_ptr()
+        a.workspace = self.ws.data_ptr()
+        a.cntrl = self.cntrl; a.safety = self.safety; a.ep = self.ep
+        F = self.table.struct()
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+        L.check(L.lib().acl_episode_batch(ct.byref(F), ct.byref(a), ct.c_void_p(stream)),
+                "acl_episode_batch")
+        self.step += steps
+        return hist
+
+    def status(self):
+        """Episode counters as a structured numpy array [B]."""
+        arr = np.ascontiguousarray(self.est.cpu().numpy())
+        return arr.view(L.EPISODE_STATUS_DTYPE).reshape(-1)

@@ -327,6 +327,102 @@ typedef struct {
 acl_status_t acl_hungarian_batch(const acl_formations_t* formations,
                                  const acl_hungarian_args_t* args, void* stream);
 
+/* ---- closed-loop batched episodes ---------------------
+ * B swarms flown for `steps` control periods in lockstep: the discrete-time
+ * model of one vehicle's node graph (CoordinationROS + Safety) with a
+ * perfectly tracking outer loop. Per control step k (global index
+ * s = step0 + k):
+ *   1. if s % auction_every == 0, the auto-auction
+ *      (CoordinationROS::autoauctionCb, coordination_ros.cpp:322-359): a swarm
+ *      whose previous auction converged on an invalid assignment flushes and
+ *      skips this one (:339-345, Auctioneer::flush); otherwise CBAA from the
+ *      current q with the carried assignment P (acl_solve_batch's auction),
+ *      adopted when valid and agreed (auctioneer.cpp:283-292); an invalid
+ *      result sets `flush`;
+ *   2. DistCntrl::compute with P and vel (controlCb, coordination_ros.cpp:
+ *      365-378), Safety::cmdinCb saturation and collisionAvoidance
+ *      (safety.cpp:172-197,412-541) -> the velocity goal;
+ *   3. Safety::makeSafeTraj(control_dt, goal) (safety.cpp:330-408): rate
+ *      limits on the goal velocity, room-bound clamps, goal position
+ *      integration; the vehicle tracks the goal exactly (q <- goal.pos,
+ *      vel <- goal.vel; the snap-stack outer loop and simulator are out of
+ *      scope). Yaw is not carried: DIST goals have r = 0 (safety.cpp:181);
+ *   4. if s % sample_every == 0, a supervisor tick (supervisor.py:297-337):
+ *      |u| of every vehicle's DistCntrl command (voriggoal) and its
+ *      collision_avoidance_active flag enter a ring of `bufflen` samples; once
+ *      full, converged <=> every vehicle's window mean |u| <
+ *      orig_zero_vel_thr, gridlocked <=> some vehicle's window mean CA flag >
+ *      avg_active_ca_thr (means: sequential sum oldest -> newest, / bufflen).
+ * Device pointers, updated in place so an episode can continue in chunks:
+ *   fidx [B]; q, vel [B][n][3]; P [B][n] (a permutation); flush [B] u8;
+ *   est [B] acl_episode_status_t; ring_u [B][bufflen][n] f64 and
+ *   ring_ca [B][bufflen][n] u8 (zeroed with est before step 0).
+ * Optional histories (NULL = not stored), k = local step:
+ *   q_hist, vel_hist [steps][B][n][3] (state after step k), u_hist [steps][B][n][3]
+ *   (DistCntrl output), ca_hist [steps][B][n], P_hist [steps][B][n]
+ *   (assignment used by step k's controller).
+ * workspace: acl_episode_workspace_bytes(n, B) bytes. */
+typedef struct {
+  double control_dt;       /* 0.01 s (coordination.launch:25, safety.cpp:38) */
+  int32_t auction_every;   /* autoauction_dt / control_dt = 1.2 / 0.01 = 120
+                              (coordination.launch:6,24) */
+  int32_t sample_every;    /* control steps per supervisor tick: 100 Hz / 50 Hz
+                              = 2 (supervisor.py:121) */
+  int32_t bufflen;         /* BUFFER_SECONDS * tick_rate = 50 (supervisor.py:
+                              47,126) */
+  int32_t reserved;
+  double max_accel_xy;     /* 0.5 (safety.cpp:45) */
+  double max_accel_z;      /* 0.8 (safety.cpp:46) */
+  double bounds_min[3];    /* room bounds: trial.sh:96 {-100, -100, 0} */
+  double bounds_max[3];    /*              {100, 100, 30} */
+  double orig_zero_vel_thr;  /* 1.00 m/s (supervisor.py:61) */
+  double avg_active_ca_thr;  /* 0.95 (supervisor.py:62) */
+} acl_episode_params_t;
+
+void acl_default_episode_params(acl_episode_params_t* e);
+
+typedef struct {
+  int32_t converged_step;  /* first global step whose tick found has_converged, -1 */
+  int32_t gridlock_step;   /* first global step whose tick found has_gridlocked, -1 */
+  int32_t converged;       /* has_converged at the last tick */
+  int32_t gridlocked;      /* has_gridlocked at the last tick */
+  uint16_t n_auctions;     /* auctions run */
+  uint16_t n_invalid;      /* auctions that converged on an invalid assignment */
+  uint16_t n_skipped;      /* auctions skipped by the flush rule */
+  uint16_t n_disagree;     /* valid auctions whose vehicles ended on different
+                              tables (P kept: the per-vehicle divergent state of
+                              the reference is not carried) */
+  uint32_t n_samples;      /* supervisor ticks taken */
+  uint32_t n_ca_steps;     /* vehicle-steps with collision avoidance active */
+} acl_episode_status_t; /* 32 bytes */
+
+typedef struct {
+  int32_t B;
+  const int32_t* fidx;
+  double* q;
+  double* vel;
+  uint16_t* P;
+  uint8_t* flush;
+  acl_episode_status_t* est;
+  double* ring_u;
+  uint8_t* ring_ca;
+  int32_t step0;
+  int32_t steps;
+  double* q_hist;
+  double* vel_hist;
+  double* u_hist;
+  uint8_t* ca_hist;
+  uint16_t* P_hist;
+  void* workspace;
+  acl_cntrl_gains_t cntrl;
+  acl_safety_params_t safety;
+  acl_episode_params_t ep;
+} acl_episode_args_t;
+
+size_t acl_episode_workspace_bytes(int32_t n, int32_t B);
+acl_status_t acl_episode_batch(const acl_formations_t* formations,
+                               const acl_episode_args_t* args, void* stream);
+
 /* ---- ADMM formation-gain design (admm::Solver::solve, solver.cpp:28-79) -
  * F formations of n points: pts [F][3][n] column-major 3 x n per formation
  * (Eigen::Matrix<double,3,Dynamic>), adj [F][n][n] f64 (symmetric 0/1),

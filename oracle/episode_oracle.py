@@ -1,0 +1,174 @@
+"""CPU restatement of the closed-loop episode.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/ as the checker of
+acl_episode_batch; never by the product path.
+
+What it restates, in the order one lockstep control period applies it:
+  * CoordinationROS::autoauctionCb (aclswarm/src/coordination_ros.cpp:322-359):
+    every `auction_every` steps, a swarm whose last auction converged on an
+    invalid assignment flushes and skips (:339-345); otherwise CBAA from the
+    current q (pyoracle.solve, the restatement of auctioneer.cpp) and
+    adoption of a valid agreed result (auctioneer.cpp:283-292);
+  * DistCntrl::compute + Safety::cmdinCb + collisionAvoidance for every
+    vehicle (pyoracle.control / saturate / collision_avoidance, i.e.
+    distcntrl.cpp:46-102, safety.cpp:172-197,412-541);
+  * Safety::makeSafeTraj (safety.cpp:330-408) with utils::rateLimit and
+    utils::clamp (aclswarm/include/aclswarm/utils.h:213-264); the vehicle
+    tracks its goal exactly (the outer loop / simulator are out of scope);
+  * the supervisor's has_converged / has_gridlocked
+    (aclswarm_sim/nodes/supervisor.py:297-337) at every `sample_every`-th
+    step over a window of `bufflen` ticks (deque(maxlen=BUFFLEN), mean over
+    the window as a sequential sum oldest -> newest, then / BUFFLEN).
+
+Parity: pinned only through its parts -- the CBAA/control/safety restatement
+is oracle/aclswarm_oracle.c; makeSafeTraj and the
+supervisor predicates are restated here from the reference text and are
+"parity unpinned" (no reference test or fixture covers them; the ROS nodes
+do not build here).
+"""
+import numpy as np
+
+import pyoracle as O
+
+
+def default_params():
+    """acl_default_episode_params: coordination.launch:6,24-25,
+    safety.cpp:45-46, trial.sh:96, supervisor.py:47,61-62,121."""
+    return dict(control_dt=0.01, auction_every=120, sample_every=2, bufflen=50,
+                max_accel_xy=0.5, max_accel_z=0.8,
+                bounds_min=(-100.0, -100.0, 0.0), bounds_max=(100.0, 100.0, 30.0),
+                orig_zero_vel_thr=1.0, avg_active_ca_thr=0.95)
+
+
+def params_from_struct(e):
+    return dict(control_dt=e.control_dt, auction_every=e.auction_every,
+                sample_every=e.sample_every, bufflen=e.bufflen,
+                max_accel_xy=e.max_accel_xy, max_accel_z=e.max_accel_z,
+                bounds_min=tuple(e.bounds_min), bounds_max=tuple(e.bounds_max),
+                orig_zero_vel_thr=e.orig_zero_vel_thr, avg_active_ca_thr=e.avg_active_ca_thr)
+
+
+def _rate_limit(dt, lo, hi, v0, v1):
+    """utils::rateLimit (utils.h:254-264), elementwise."""
+    upper = v0 + hi * dt
+    lower = v0 + lo * dt
+    v1 = np.where(v1 > upper, upper, v1)
+    return np.where(v1 < lower, lower, v1)
+
+
+def make_safe_traj(pos, vel, cmd, ep):
+    """Safety::makeSafeTraj (safety.cpp:330-408) for arrays [..., 3] of goal
+    positions, goal velocities and velocity goals. Returns (pos, vel)."""
+    dt = ep["control_dt"]
+    amax = np.array([ep["max_accel_xy"], ep["max_accel_xy"], ep["max_accel_z"]])
+    bmin = np.array(ep["bounds_min"], dtype=np.float64)
+    bmax = np.array(ep["bounds_max"], dtype=np.float64)
+    pos = np.asarray(pos, np.float64)
+    vel = np.asarray(vel, np.float64)
+    c = _rate_limit(dt, -amax, amax, vel, np.asarray(cmd, np.float64))
+    nxt = pos + c * dt
+    lo = np.where(pos < bmin, pos, bmin)         # std::min(bounds_min, pos)
+    hi = np.where(bmax < pos, pos, bmax)         # std::max(bounds_max, pos)
+    below = nxt < lo
+    above = ~below & (nxt > hi)
+    clamped = below | above
+    newpos = np.where(below, lo, np.where(above, hi, nxt))
+    c = np.where(clamped, _rate_limit(dt, -amax, amax, vel, np.zeros_like(c)), c)
+    return newpos, c
+
+
+class Supervisor:
+    """supervisor.py:297-337 for one swarm of n vehicles."""
+
+    def __init__(self, n, ep):
+        self.L = ep["bufflen"]
+        self.ep = ep
+        self.speed = []
+        self.ca = []
+        self.n_samples = 0
+        self.converged = False
+        self.gridlocked = False
+
+    def tick(self, u, ca):
+        """u [n][3] DistCntrl commands (voriggoal), ca [n] flags."""
+        u = np.asarray(u, np.float64)
+        sp = np.sqrt((u[:, 0] * u[:, 0] + u[:, 1] * u[:, 1]) + u[:, 2] * u[:, 2])
+        self.speed.append(sp)
+        self.ca.append(np.asarray(ca).astype(np.float64))
+        self.speed = self.speed[-self.L:]
+        self.ca = self.ca[-self.L:]
+        self.n_samples += 1
+        if self.n_samples < self.L:
+            return None
+        su = np.zeros_like(sp)
+        sc = np.zeros_like(sp)
+        for a, b in zip(self.speed, self.ca):   # oldest -> newest
+            su = su + a
+            sc = sc + b
+        mu = su / float(self.L)
+        mc = sc / float(self.L)
+        self.converged = bool((mu < self.ep["orig_zero_vel_thr"]).all())
+        self.gridlocked = bool((mc > self.ep["avg_active_ca_thr"]).any())
+        return self.converged, self.gridlocked
+
+
+def control_step(q, vel, p, adj, gains, P, g=None, s=None):
+    """DistCntrl::compute + cmdinCb + collisionAvoidance for every vehicle of
+    one swarm with assignment P (vehicle -> point). Returns u, u_safe, ca."""
+    n = q.shape[0]
+    Pt = np.zeros(n, np.uint16)
+    Pt[np.asarray(P, np.int64)] = np.arange(n, dtype=np.uint16)
+    u = np.zeros((n, 3))
+    us = np.zeros((n, 3))
+    ca = np.zeros(n, np.uint8)
+    for v in range(n):
+        u[v] = O.control(v, q, vel[v], Pt, adj, gains, p, g)
+        c = O.saturate(u[v], s)
+        us[v], mod = O.collision_avoidance(v, q, c, s)
+        ca[v] = mod
+    return u, us, ca
+
+
+def adopt(P, flush, res):
+    """autoauctionCb's flush rule + adoption for one swarm after an auction
+    result `res` (pyoracle.solve). Returns (P, flush, event) with event one
+    of 'skipped', 'adopted', 'invalid', 'disagree'."""
+    if flush:
+        return P, 0, "skipped"
+    fl = res["status"]["flags"]
+    valid, agree = bool(fl & 0x01), bool(fl & 0x02)
+    if agree and valid:
+        return res["P_out"].astype(np.uint16).copy(), 0, "adopted"
+    if agree:
+        return P, 1, "invalid"
+    return P, 0, "disagree"
+
+
+def run_episode(q, vel, P, p, adj, gains, steps, ep, step0=0, g=None, s=None):
+    """The whole closed loop for one swarm on the CPU (small cases only)."""
+    q = np.array(q, np.float64)
+    vel = np.array(vel, np.float64)
+    P = np.array(P, np.uint16)
+    flush = 0
+    sup = Supervisor(q.shape[0], ep)
+    counts = dict(skipped=0, adopted=0, invalid=0, disagree=0)
+    conv_step = grid_step = -1
+    qs = []
+    for k in range(steps):
+        step = step0 + k
+        if step % ep["auction_every"] == 0:
+            res = O.solve(q, vel, p, adj, gains, P, g, s)
+            P, flush, ev = adopt(P, flush, res)
+            counts[ev] += 1
+        u, us, ca = control_step(q, vel, p, adj, gains, P, g, s)
+        q, vel = make_safe_traj(q, vel, us, ep)
+        if step % ep["sample_every"] == 0:
+            r = sup.tick(u, ca)
+            if r is not None:
+                if r[0] and conv_step < 0:
+                    conv_step = step
+                if r[1] and grid_step < 0:
+                    grid_step = step
+        qs.append(q.copy())
+    return dict(q=q, vel=vel, P=P, flush=flush, counts=counts, converged_step=conv_step,
+                gridlock_step=grid_step, q_hist=np.array(qs))

@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Closed-loop episode benchmark (acl_episode_batch).
+
+B swarms of n = 100 vehicles (config C3 shape: noncomplete formations, a
+unique formation per swarm, ADMM-structured gain records) flown for `steps`
+control periods of 10 ms: auto-auctions every 120 steps (1.2 s), DistCntrl +
+Safety + makeSafeTraj every step, supervisor ticks every 2 steps. Reports
+swarm-steps/s (one swarm advanced one control period) with the state
+resident in HBM, per-kernel times from HIP events are not used here (the
+step is a sequence of small launches; rocprofv3 --stats gives the split).
+The CPU baseline runs oracle/episode_oracle.py's loop on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from aclswarm_amd import _lib as L  # noqa: E402
+from aclswarm_amd import engine, workload  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=16384)
+    ap.add_argument("--n", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=240)
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(99)
+    w = workload.simform_workload(args.B, args.n, gen, dev, F=None, complete=False, planes=5)
+    T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"], w["planes"])
+    # warm-up: a short episode (first launches, workspace)
+    e0 = engine.Episode(T, w["fidx"], w["q"], w["vel"], w["P_in"])
+    e0.run(2)
+    torch.cuda.synchronize()
+    e = engine.Episode(T, w["fidx"], w["q"], w["vel"], w["P_in"])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e.run(args.steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = e.status()
+    ep = e.ep
+    line = {
+        "metric": "closed-loop episode swarm-steps/sec (N=100)",
+        "value": args.B * args.steps / dt, "unit": "swarm-steps/s",
+        "B": args.B, "n": args.n, "steps": args.steps, "seconds": dt,
+        "ms_per_step": dt / args.steps * 1e3,
+        "auctions_per_swarm": int(st["n_auctions"][0] + st["n_skipped"][0]),
+        "control_dt": ep.control_dt, "auction_every": ep.auction_every,
+        "dtype": "f64", "data": "synthetic (simform_workload, C3 shape)",
+        "episode": {"converged": int((st["converged_step"] >= 0).sum()),
+                    "gridlocked": int((st["gridlock_step"] >= 0).sum()),
+                    "invalid_auctions": int(st["n_invalid"].sum()),
+                    "disagree_auctions": int(st["n_disagree"].sum()),
+                    "ca_vehicle_steps": int(st["n_ca_steps"].sum())},
+    }
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import episode_oracle as E
+        epd = E.params_from_struct(ep)
+        b = 0
+        f = int(w["fidx"][b])
+        p = w["p"][f].cpu().numpy()
+        adj = w["adj"][f].cpu().numpy().astype(np.uint8)
+        G = workload.dense_gains_host(w, f)
+        q = w["q"][b].cpu().numpy()
+        vel = w["vel"][b].cpu().numpy()
+        P = w["P_in"][b].cpu().numpy().view(np.uint16)
+        t0 = time.perf_counter()
+        k = 0
+        while True:
+            E.run_episode(q, vel, P, p, adj, G, 1, epd, step0=k)
+            k += 1
+            if time.perf_counter() - t0 > args.cpu_budget:
+                break
+        tc = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": k / tc, "unit": "swarm-steps/s", "cores": 1,
+                                "kind": "port",
+                                "sample": f"{k} control steps of one n={args.n} swarm through "
+                                          "oracle/episode_oracle.py (C restatement of "
+                                          "DistCntrl/Safety/CBAA per vehicle), 1 thread"}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,158 @@
+"""GPU parity of closed-loop batched episodes (acl_episode_batch, SURVEY.md
+§8f row 1) against oracle/episode_oracle.py.
+
+Teacher-forced: every recorded step of the GPU episode is re-derived on the
+CPU from the GPU's own state before that step -- the auction and adoption
+(assignments bit-exact), DistCntrl + Safety (u within 1e-5 relative, CA flags
+exact), makeSafeTraj (state within 1e-9 absolute), and the supervisor's
+window predicates from the recorded commands (tick for tick exact). Then the
+whole closed loop once more, untouched, against the CPU's own episode, and
+chunked calls against one call (bit-identical).
+"""
+import numpy as np
+import pytest
+
+import episode_oracle as E
+import helpers as H
+import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+U_RTOL = 1e-5      # control commands: fp64, within 1e-5 relative (north_star)
+Q_ATOL = 1e-9      # one makeSafeTraj step from commands within U_RTOL * dt
+
+
+def _cases():
+    rng = np.random.RandomState(11)
+    pts, adj, gains, q0 = H.swarm6()
+    B = 6
+    q = np.stack([q0 + (rng.normal(0, 0.4, q0.shape) if b else 0) for b in range(B)])
+    q[..., 2] = 1.0
+    a = dict(name="swarm6_3d", pts=list(pts), adj=list(adj), gains=list(gains),
+             fidx=np.arange(B) % 3, q=q, vel=np.zeros((B, 6, 3)),
+             P=np.stack([H.random_perm(rng, 6) for _ in range(B)]),
+             steps=250, ep=dict())
+    P20, A20 = H.simform("simform20_nc")
+    p20 = [P20[0, 0], P20[1, 1]]
+    a20 = [A20[0], A20[1]]
+    g20 = [H.synth_gains(rng, x) for x in a20]
+    B = 8
+    q = np.stack([H.dense_positions(rng, 20, 7.0 + b) for b in range(B)])
+    b_ = dict(name="simform20_dense", pts=p20, adj=a20, gains=g20, fidx=np.arange(B) % 2,
+              q=q, vel=rng.normal(0, 0.2, (B, 20, 3)),
+              P=np.stack([H.random_perm(rng, 20) for _ in range(B)]),
+              steps=160, ep=dict(auction_every=40, bufflen=20))
+    return [a, b_]
+
+
+def _episode(case, dev):
+    import torch
+    from aclswarm_amd import _lib as L
+    from aclswarm_amd import engine
+    T = engine.FormationTable.from_host(case["pts"], case["adj"], case["gains"], device=dev)
+    ep = L.default_episode_params()
+    for k, v in case["ep"].items():
+        setattr(ep, k, v)
+    e = engine.Episode(T, torch.from_numpy(case["fidx"].astype(np.int32)).to(dev),
+                       torch.from_numpy(case["q"]).to(dev), torch.from_numpy(case["vel"]).to(dev),
+                       torch.from_numpy(case["P"].astype(np.uint16).view(np.int16)).to(dev),
+                       params=ep)
+    return e, ep
+
+
+@pytest.mark.parametrize("ci", [0, 1])
+def test_episode_teacher_forced_parity(cuda, ci):
+    import torch
+    case = _cases()[ci]
+    e, eps = _episode(case, cuda)
+    hist = e.run(case["steps"], history=True)
+    torch.cuda.synchronize()
+    h = {k: v.cpu().numpy() for k, v in hist.items()}
+    h["P"] = h["P"].view(np.uint16)
+    est = e.status()
+    ep = E.params_from_struct(eps)
+    B, n = case["q"].shape[:2]
+    n_adopt = n_ca = 0
+    for b in range(B):
+        f = case["fidx"][b]
+        p, adj, G = case["pts"][f], case["adj"][f], case["gains"][f]
+        qprev, vprev = case["q"][b], case["vel"][b]
+        P, flush = case["P"][b].astype(np.uint16), 0
+        sup = E.Supervisor(n, ep)
+        counts = dict(skipped=0, adopted=0, invalid=0, disagree=0)
+        conv = grid = -1
+        for k in range(case["steps"]):
+            if k % ep["auction_every"] == 0:
+                res = O.solve(qprev, vprev, p, adj, G, P)
+                P, flush, ev = E.adopt(P, flush, res)
+                counts[ev] += 1
+            assert (h["P"][k, b] == P).all(), (b, k)
+            u, us, ca = E.control_step(qprev, vprev, p, adj, G, P)
+            np.testing.assert_allclose(h["u"][k, b], u, rtol=U_RTOL, atol=U_RTOL)
+            assert (h["ca"][k, b] == ca).all(), (b, k)
+            qn, vn = E.make_safe_traj(qprev, vprev, us, ep)
+            np.testing.assert_allclose(h["q"][k, b], qn, rtol=0, atol=Q_ATOL)
+            np.testing.assert_allclose(h["vel"][k, b], vn, rtol=0, atol=Q_ATOL)
+            if k % ep["sample_every"] == 0:
+                r = sup.tick(h["u"][k, b], h["ca"][k, b])
+                if r is not None:
+                    conv = k if (r[0] and conv < 0) else conv
+                    grid = k if (r[1] and grid < 0) else grid
+            qprev, vprev = h["q"][k, b], h["vel"][k, b]
+            n_ca += int(ca.sum())
+        st = est[b]
+        assert st["n_auctions"] == counts["adopted"] + counts["invalid"] + counts["disagree"]
+        assert (st["n_skipped"], st["n_invalid"], st["n_disagree"]) == \
+            (counts["skipped"], counts["invalid"], counts["disagree"])
+        assert (st["converged_step"], st["gridlock_step"]) == (conv, grid), b
+        assert st["converged"] == int(sup.converged) and st["gridlocked"] == int(sup.gridlocked)
+        assert st["n_samples"] == sup.n_samples
+        assert st["n_ca_steps"] == int(h["ca"][:, b].sum())
+        n_adopt += counts["adopted"]
+    assert n_adopt > 0
+    if ci == 1:
+        assert n_ca > 0          # the dense starts exercise collision avoidance
+
+
+def test_episode_closed_loop_matches_cpu_episode(cuda):
+    """The untouched GPU loop against the CPU's own loop, in the smooth regime
+    (start grid spread 3x: no collision avoidance in 250 steps). With vehicles
+    in contact the loop is not smooth -- collision avoidance snaps headings to
+    sector edges -- and ulp-level differences of the atan2/asin edges can pick
+    a different edge some steps later; the teacher-forced test is the per-step
+    gate for those cases."""
+    import torch
+    case = dict(_cases()[0])
+    rng = np.random.RandomState(5)
+    _, _, _, q0 = H.swarm6()
+    q = np.stack([3.0 * q0 + (rng.normal(0, 0.4, q0.shape) if b else 0) for b in range(6)])
+    q[..., 2] = 1.0
+    case["q"] = q
+    e, eps = _episode(case, cuda)
+    e.run(case["steps"])
+    torch.cuda.synchronize()
+    ep = E.params_from_struct(eps)
+    qg = e.q.cpu().numpy()
+    Pg = e.P.cpu().numpy().view(np.uint16)
+    est = e.status()
+    assert int(est["n_ca_steps"].sum()) == 0
+    for b in range(case["q"].shape[0]):
+        f = case["fidx"][b]
+        r = E.run_episode(case["q"][b], case["vel"][b], case["P"][b], case["pts"][f],
+                          case["adj"][f], case["gains"][f], case["steps"], ep)
+        np.testing.assert_allclose(qg[b], r["q"], rtol=0, atol=1e-9)
+        assert (Pg[b] == r["P"]).all()
+        assert est[b]["converged_step"] == r["converged_step"]
+
+
+def test_episode_chunks_equal_one_call(cuda):
+    import torch
+    case = _cases()[1]
+    e1, _ = _episode(case, cuda)
+    e1.run(case["steps"])
+    e2, _ = _episode(case, cuda)
+    e2.run(57)
+    e2.run(case["steps"] - 57)
+    torch.cuda.synchronize()
+    for k in ("q", "vel", "P", "flush", "est", "ring_u", "ring_ca"):
+        assert torch.equal(getattr(e1, k), getattr(e2, k)), k
