@@ -187,157 +187,135 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
   // assignment (vehicle v = Pt[i] of row i): consecutive rows are consecutive
   // edge ranges, so the gain stream is read nearly sequentially.
   // Otherwise groups walk vehicles, each with its own adopted point.
-  // The wave's (group, pass) steps form one flat sequence so that the gain
-  // loads of the next step -- the next group's first pass included -- are in
-  // flight while the current step computes and while a finished group's
-  // segment sums are reduced.
-  struct Slot {
-    int act, vv, i;
-  };
-  auto slot_of = [&](int grp) -> Slot {
+  for (int grp = wave; grp < ngroups; grp += kCtlWaves) {
     const int r = grp * GV + seg;
     const bool act = seg < GV && r < n;
     const int rr = act ? r : 0;
-    Slot o;
-    o.act = act;
-    o.vv = uniform ? (int)Pt[rr] : rr;
-    o.i = uniform ? rr : (int)myi[o.vv];
-    return o;
-  };
-  auto edge_of = [&](const Slot& sl, int t) -> int {
-    const int j = s + S * t;
-    const int jw = j >> 6, jb = j & 63;
-    const unsigned long long word = (sl.act && j < n) ? adjF[sl.i * NW + jw] : 0ull;
-    if (!((word >> jb) & 1ull)) return -1;
-    return rowpre[sl.i * NW + jw] + __popcll(word & ((1ull << jb) - 1ull));
-  };
-  auto load_planes = [&](int e, double (&Lg)[NP]) {
-    if constexpr (NP == 9) {
-      const int voff = e >= 0 ? e * 8 : 0x40000000;  // past num_records -> 0
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const auto raw = __builtin_amdgcn_raw_buffer_load_b64(grs, voff, k * E * 8, 0);
-        __builtin_memcpy(&Lg[k], &raw, 8);
-      }
-    } else {
-      // one 40-byte record per edge: two 16-byte loads and one 8-byte load
-      const int voff = e >= 0 ? e * 40 : 0x40000000;
-      const auto r0 = __builtin_amdgcn_raw_buffer_load_b128(grs, voff, 0, 0);
-      const auto r1 = __builtin_amdgcn_raw_buffer_load_b128(grs, voff, 16, 0);
-      const auto r2 = __builtin_amdgcn_raw_buffer_load_b64(grs, voff, 32, 0);
-      __builtin_memcpy(&Lg[0], &r0, 16);
-      __builtin_memcpy(&Lg[2], &r1, 16);
-      __builtin_memcpy(&Lg[4], &r2, 8);
-    }
-  };
-  const int ng_w = wave < ngroups ? (ngroups - wave + kCtlWaves - 1) / kCtlWaves : 0;
-  const int K = ng_w * IT;
-  int grp = wave, t = 0;
-  Slot cur = slot_of(grp);
-  int e_cur = K > 0 ? edge_of(cur, 0) : -1;
-  double Lc[NP];
-  load_planes(e_cur, Lc);
-  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-  int nedge = 0;  // the damping term kd (-vel) is added once per edge, below
-#pragma unroll 1
-  for (int k = 0; k < K; ++k) {
-    // the vehicle's values are re-read from LDS every step (short live
-    // ranges: fewer VGPRs, more waves per SIMD)
-    asm volatile("" ::: "memory");
-    const int vv = cur.vv, i = cur.i;
-    const double qv0 = q[3 * vv], qv1 = q[3 * vv + 1], qv2 = q[3 * vv + 2];
-    const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
-    const double Ni = pn[2 * i], Nzi = pn[2 * i + 1];
-    // next step: the same group's next pass, or the next group's first
-    const bool last = t + 1 == IT;
-    const int grp_n = last ? grp + kCtlWaves : grp;
-    const int t_n = last ? 0 : t + 1;
-    Slot nxt = last ? slot_of(grp_n < ngroups ? grp_n : grp) : cur;
-    const int e_nxt = k + 1 < K ? edge_of(nxt, t_n) : -1;
-    double Ln[NP];
-    load_planes(e_nxt, Ln);
-    if (e_cur >= 0) {
-      // tolerance-based parity (1e-5 relative): fused multiply-adds and the
-      // refined fast sqrt / quotient (common.h) are allowed here
-#pragma clang fp contract(fast)
+    const int vv = uniform ? (int)Pt[rr] : rr;
+    const int v = vv;
+    const int i = uniform ? rr : (int)myi[vv];
+    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+    int nedge = 0;  // the damping term kd (-vel) is added once per edge, below
+    // edge of pass t for this lane (-1: none); the gain loads of pass t + 1
+    // are issued before pass t's math so that each wave keeps one pass of
+    // the gain stream in flight while it computes
+    auto edge_of = [&](int t) -> int {
       const int j = s + S * t;
-      double A[9];
+      const int jw = j >> 6, jb = j & 63;
+      const unsigned long long word = (act && j < n) ? adjF[i * NW + jw] : 0ull;
+      if (!((word >> jb) & 1ull)) return -1;
+      return rowpre[i * NW + jw] + __popcll(word & ((1ull << jb) - 1ull));
+    };
+    auto load_planes = [&](int e, double (&Lg)[NP]) {
       if constexpr (NP == 9) {
+        const int voff = e >= 0 ? e * 8 : 0x40000000;  // past num_records -> 0
 #pragma unroll
-        for (int kk = 0; kk < 9; ++kk) A[kk] = Lc[kk];
+        for (int k = 0; k < 9; ++k) {
+          const auto raw = __builtin_amdgcn_raw_buffer_load_b64(grs, voff, k * E * 8, 0);
+          __builtin_memcpy(&Lg[k], &raw, 8);
+        }
       } else {
-        // (0,0) (0,1) (1,0) (1,1) (2,2) stored; +0.0 elsewhere (solver.cpp:49-77).
-        // The zeros still multiply q below, as in the 9-plane layout.
-        A[0] = Lc[0]; A[1] = Lc[1]; A[2] = 0.0;
-        A[3] = Lc[2]; A[4] = Lc[3]; A[5] = 0.0;
-        A[6] = 0.0;   A[7] = 0.0;   A[8] = Lc[4];
+        // one 40-byte record per edge: two 16-byte loads and one 8-byte load
+        const int voff = e >= 0 ? e * 40 : 0x40000000;
+        const auto r0 = __builtin_amdgcn_raw_buffer_load_b128(grs, voff, 0, 0);
+        const auto r1 = __builtin_amdgcn_raw_buffer_load_b128(grs, voff, 16, 0);
+        const auto r2 = __builtin_amdgcn_raw_buffer_load_b64(grs, voff, 32, 0);
+        __builtin_memcpy(&Lg[0], &r0, 16);
+        __builtin_memcpy(&Lg[2], &r1, 16);
+        __builtin_memcpy(&Lg[4], &r2, 8);
       }
-      const int uu = uniform ? Pt[j] : rows[(size_t)vv * n + j];
-      const double q0 = q[3 * uu] - qv0, q1 = q[3 * uu + 1] - qv1, q2 = q[3 * uu + 2] - qv2;
-      const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
-      const double dxy = sqrt_nr((Ni + pn[2 * j]) - 2.0 * (pix * pjx + piy * pjy));
-      const double dz = sqrt_nr((Nzi + pn[2 * j + 1]) - 2.0 * (piz * pjz));
-      const double e_xy = sqrt_nr(q0 * q0 + q1 * q1) - dxy;
-      const double e_z = fabs(q2) - dz;  // |q_ij.z| = sqrt(q2^2) (no over/underflow)
-      // the two gated atan terms, one after the other (register pressure)
-      double Fxy = 0.0, Fz = 0.0;
-      const bool gxy = fabs(e_xy) > g.e_xy_thr, gz = fabs(e_z) > g.e_z_thr;
+    };
+    int e_cur = edge_of(0);
+    double Lc[NP];
+    load_planes(e_cur, Lc);
 #pragma unroll 1
-      for (int kk = 0; kk < 2; ++kk) {
-        const bool on = kk ? gz : gxy;
-        if (on) {
-          const double fa = kk ? g.K1_z * acl_atan_tab(g.K2_z * e_z, atab)
-                               : g.K1_xy * acl_atan_tab(g.K2_xy * e_xy, atab);
-          if (kk) Fz = fa; else Fxy = fa;
-        }
-      }
-      const double up0 = ((A[0] * q0 + A[1] * q1) + A[2] * q2) + Fxy * q0;
-      const double up1 = ((A[3] * q0 + A[4] * q1) + A[5] * q2) + Fxy * q1;
-      const double up2 = ((A[6] * q0 + A[7] * q1) + A[8] * q2) + Fz * q2;
-#ifdef ACL_EXP_GAIN_STREAM_ONLY
-      acc0 += A[0] + A[1]; acc1 += A[3] + A[4]; acc2 += A[8];
-      (void)up0; (void)up1; (void)up2;
-#else
-      acc0 += g.kp * up0;
-      acc1 += g.kp * up1;
-      acc2 += g.kp * up2;
-      ++nedge;
-#endif
-    }
-    if (last) {
-      // + kd (-vel) for each of the lane's edges (distcntrl.cpp:85-95 adds it
-      // per neighbour)
-      if (nedge) {
-        const double* gv = P.vel + ((size_t)b * n + vv) * 3;
-        const double cn = (double)nedge;
-        acc0 += cn * (g.kd * (-gv[0]));
-        acc1 += cn * (g.kd * (-gv[1]));
-        acc2 += cn * (g.kd * (-gv[2]));
-      }
-      // segment sums: each vehicle's S lane partials, in lane order
-      red[3 * lane] = acc0; red[3 * lane + 1] = acc1; red[3 * lane + 2] = acc2;
-      __builtin_amdgcn_wave_barrier();
+    for (int t = 0; t < IT; ++t) {
+      // the vehicle's values are re-read from LDS every pass (short live
+      // ranges: fewer VGPRs, more waves per SIMD)
       asm volatile("" ::: "memory");
-      if (lane < GV && grp * GV + lane < n) {
-        const double* r = red + 3 * S * lane;
-        double c0 = r[0], c1 = r[1], c2 = r[2];
-        for (int kk = 1; kk < S; ++kk) {
-          c0 += r[3 * kk]; c1 += r[3 * kk + 1]; c2 += r[3 * kk + 2];
-        }
-        const int w = uniform ? (int)Pt[grp * GV + lane] : grp * GV + lane;
-        uo[3 * w] = c0; uo[3 * w + 1] = c1; uo[3 * w + 2] = c2;
-      }
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("" ::: "memory");
-      acc0 = acc1 = acc2 = 0.0;
-      nedge = 0;
-    }
-    grp = grp_n;
-    t = t_n;
-    cur = nxt;
-    e_cur = e_nxt;
+      const double qv0 = q[3 * vv], qv1 = q[3 * vv + 1], qv2 = q[3 * vv + 2];
+      const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
+      const double Ni = pn[2 * i], Nzi = pn[2 * i + 1];
+      int e_nxt = -1;
+      double Ln[NP];
+      if (t + 1 < IT) e_nxt = edge_of(t + 1);
+      load_planes(e_nxt, Ln);
+      if (e_cur >= 0) {
+        // tolerance-based parity (1e-5 relative): fused multiply-adds and the
+        // refined fast sqrt / quotient (common.h) are allowed here
+#pragma clang fp contract(fast)
+        const int j = s + S * t;
+        double A[9];
+        if constexpr (NP == 9) {
 #pragma unroll
-    for (int kk = 0; kk < NP; ++kk) Lc[kk] = Ln[kk];
+          for (int k = 0; k < 9; ++k) A[k] = Lc[k];
+        } else {
+          // (0,0) (0,1) (1,0) (1,1) (2,2) stored; +0.0 elsewhere (solver.cpp:49-77).
+          // The zeros still multiply q below, as in the 9-plane layout.
+          A[0] = Lc[0]; A[1] = Lc[1]; A[2] = 0.0;
+          A[3] = Lc[2]; A[4] = Lc[3]; A[5] = 0.0;
+          A[6] = 0.0;   A[7] = 0.0;   A[8] = Lc[4];
+        }
+        const int uu = uniform ? Pt[j] : rows[(size_t)v * n + j];
+        const double q0 = q[3 * uu] - qv0, q1 = q[3 * uu + 1] - qv1, q2 = q[3 * uu + 2] - qv2;
+        const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
+        const double dxy = sqrt_nr((Ni + pn[2 * j]) - 2.0 * (pix * pjx + piy * pjy));
+        const double dz = sqrt_nr((Nzi + pn[2 * j + 1]) - 2.0 * (piz * pjz));
+        const double e_xy = sqrt_nr(q0 * q0 + q1 * q1) - dxy;
+        const double e_z = fabs(q2) - dz;  // |q_ij.z| = sqrt(q2^2) (no over/underflow)
+        // the two gated atan terms, one after the other (register pressure)
+        double Fxy = 0.0, Fz = 0.0;
+        const bool gxy = fabs(e_xy) > g.e_xy_thr, gz = fabs(e_z) > g.e_z_thr;
+#pragma unroll 1
+        for (int kk = 0; kk < 2; ++kk) {
+          const bool on = kk ? gz : gxy;
+          if (on) {
+            const double fa = kk ? g.K1_z * acl_atan_tab(g.K2_z * e_z, atab)
+                                 : g.K1_xy * acl_atan_tab(g.K2_xy * e_xy, atab);
+            if (kk) Fz = fa; else Fxy = fa;
+          }
+        }
+        const double up0 = ((A[0] * q0 + A[1] * q1) + A[2] * q2) + Fxy * q0;
+        const double up1 = ((A[3] * q0 + A[4] * q1) + A[5] * q2) + Fxy * q1;
+        const double up2 = ((A[6] * q0 + A[7] * q1) + A[8] * q2) + Fz * q2;
+#ifdef ACL_EXP_GAIN_STREAM_ONLY
+        acc0 += A[0] + A[1]; acc1 += A[3] + A[4]; acc2 += A[8];
+        (void)up0; (void)up1; (void)up2;
+#else
+        acc0 += g.kp * up0;
+        acc1 += g.kp * up1;
+        acc2 += g.kp * up2;
+        ++nedge;
+#endif
+      }
+      e_cur = e_nxt;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) Lc[k] = Ln[k];
+    }
+    // + kd (-vel) for each of the lane's edges (distcntrl.cpp:85-95 adds it
+    // per neighbour)
+    if (nedge) {
+      const double* gv = P.vel + ((size_t)b * n + vv) * 3;
+      const double cn = (double)nedge;
+      acc0 += cn * (g.kd * (-gv[0]));
+      acc1 += cn * (g.kd * (-gv[1]));
+      acc2 += cn * (g.kd * (-gv[2]));
+    }
+    // segment sums: each vehicle's S lane partials, in lane order
+    red[3 * lane] = acc0; red[3 * lane + 1] = acc1; red[3 * lane + 2] = acc2;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (lane < GV && grp * GV + lane < n) {
+      const double* r = red + 3 * S * lane;
+      double c0 = r[0], c1 = r[1], c2 = r[2];
+      for (int k = 1; k < S; ++k) {
+        c0 += r[3 * k]; c1 += r[3 * k + 1]; c2 += r[3 * k + 2];
+      }
+      const int w = uniform ? (int)Pt[grp * GV + lane] : grp * GV + lane;
+      uo[3 * w] = c0; uo[3 * w + 1] = c1; uo[3 * w + 2] = c2;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
   }
   __syncthreads();
   // per vehicle (lanes over vehicles): Safety::cmdinCb saturation and the
