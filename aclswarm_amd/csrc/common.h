@@ -215,6 +215,70 @@ __device__ __forceinline__ double acl_atan_tab(double x, const double* tab) {
   return (ax == __builtin_inf()) ? copysign(1.57079632679489655800e+00, x) : copysign(r, x);
 }
 
+// Square root with one Goldschmidt step from v_rsq_f64 (relative error
+// ~2^-46): the distances of the control law's gated terms, where the parity
+// bar is 1e-5 relative on u. sqrt(negative) and NaN give NaN, +-0 and +inf
+// themselves, as std::sqrt.
+__device__ __forceinline__ double sqrt_nr1(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  const double g = x * y, h = 0.5 * y;
+  const double r = __builtin_fma(-g, h, 0.5);
+  const double s = __builtin_fma(g, r, g);
+  return (x == 0.0 || __builtin_isinf(x)) ? x : s;
+}
+
+// Rows k = 0..16 of {na, nb, da, db, a_k} for acl_atan_k32:
+// atan(|x|) = a_k + atan(t), t = (na |x| + nb) / (da |x| + db), i.e.
+// t = (|x| - c_k) / (1 + c_k |x|) with c_k = tan(k pi / 32), a_k = atan(c_k);
+// k = 16: t = -1 / |x|, a = pi / 2. Callers stage it in LDS.
+__device__ constexpr double kAtan32Tab[17][5] = {
+    {1.0, 0.0, 0.0, 1.0, 0.0},
+    {1.0, -0.09849140335716425, 0.09849140335716425, 1.0, 0.09817477042468103},
+    {1.0, -0.198912367379658, 0.198912367379658, 1.0, 0.19634954084936207},
+    {1.0, -0.3033466836073424, 0.3033466836073424, 1.0, 0.2945243112740431},
+    {1.0, -0.41421356237309503, 0.41421356237309503, 1.0, 0.39269908169872414},
+    {1.0, -0.5345111359507916, 0.5345111359507916, 1.0, 0.4908738521234052},
+    {1.0, -0.6681786379192989, 0.6681786379192989, 1.0, 0.5890486225480862},
+    {1.0, -0.8206787908286602, 0.8206787908286602, 1.0, 0.6872233929727672},
+    {1.0, -0.9999999999999999, 0.9999999999999999, 1.0, 0.7853981633974483},
+    {1.0, -1.2185035255879764, 1.2185035255879764, 1.0, 0.8835729338221293},
+    {1.0, -1.496605762665489, 1.496605762665489, 1.0, 0.9817477042468103},
+    {1.0, -1.8708684117893888, 1.8708684117893888, 1.0, 1.0799224746714913},
+    {1.0, -2.414213562373095, 2.414213562373095, 1.0, 1.1780972450961724},
+    {1.0, -3.296558208938321, 3.296558208938321, 1.0, 1.2762720155208536},
+    {1.0, -5.027339492125846, 5.027339492125846, 1.0, 1.3744467859455345},
+    {1.0, -10.153170387608842, 10.153170387608842, 1.0, 1.4726215563702154},
+    {0.0, -1.0, 1.0, 0.0, 1.5707963267948966}};
+
+// atan for the control law's gated terms (parity bar 1e-5 relative on u). An
+// fp32 estimate of atan(|x|) (pi/4 y - y (y - 1)(0.2447 + 0.0663 y) on
+// y = min(|x|, 1/|x|), |error| < 2e-3 rad) picks the nearest table point, so
+// |t| <= tan(pi/64 + 2e-3) < 0.052, and atan(t) = t + t z (-1/3 + z/5 - z^2/7
+// + z^3/9), z = t^2, is within z^5 / 11 < 1.3e-14 relative. One reciprocal
+// with one Newton step for the quotient.
+__device__ __forceinline__ double acl_atan_k32(double x, const double* tab) {
+  const double ax = fabs(x);
+  const float xf = (float)ax;
+  const bool big = xf > 1.0f;
+  const float yf = big ? __builtin_amdgcn_rcpf(xf) : xf;
+  const float t0 = yf * (0.78539816f - (yf - 1.0f) * (0.2447f + 0.0663f * yf));
+  const float th = big ? 1.57079633f - t0 : t0;
+  int k = (int)(th * 10.18591636f + 0.5f);  // round(th * 32 / pi)
+  k = k < 0 ? 0 : (k > 16 ? 16 : k);
+  const double* rw = tab + 5 * k;
+  const double num = __builtin_fma(rw[0], ax, rw[1]);
+  const double den = __builtin_fma(rw[2], ax, rw[3]);
+  double r = __builtin_amdgcn_rcp(den);
+  r = __builtin_fma(__builtin_fma(-den, r, 1.0), r, r);
+  const double t = num * r;
+  const double z = t * t;
+  double p = __builtin_fma(z, 1.0 / 9.0, -1.0 / 7.0);
+  p = ACL_FMA_K(z, p, 1.0 / 5.0);
+  p = ACL_FMA_K(z, p, -1.0 / 3.0);
+  const double res = rw[4] + __builtin_fma(t * z, p, t);
+  return (ax == __builtin_inf()) ? copysign(1.57079632679489655800e+00, x) : copysign(res, x);
+}
+
 __device__ __forceinline__ double wrap_to_pi(double a) {  // utils.h:275-280
   if (a > kPi) return a - 2 * kPi;
   if (a < -kPi) return a + 2 * kPi;

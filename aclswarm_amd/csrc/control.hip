@@ -34,7 +34,19 @@ namespace acl_amd {
 
 constexpr int kCtlBlock = 256;
 #ifndef ACL_GAIN_WAVES
-#define ACL_GAIN_WAVES 5  // waves per SIMD the record-layout gain kernel is built for
+#define ACL_GAIN_WAVES 6  // waves per SIMD the record-layout gain kernel is built for
+#endif
+#ifndef ACL_GAIN_FASTMATH
+#define ACL_GAIN_FASTMATH 1  // 17-point atan reduction and one-step sqrt (1e-14 relative)
+#endif
+#if ACL_GAIN_FASTMATH
+#define ACL_GAIN_SQRT sqrt_nr1
+#define ACL_GAIN_ATAN acl_atan_k32
+#define ACL_ATAB_N 85
+#else
+#define ACL_GAIN_SQRT sqrt_nr
+#define ACL_GAIN_ATAN acl_atan_tab
+#define ACL_ATAB_N 30
 #endif
 constexpr int kCtlWaves = kCtlBlock / 64;
 
@@ -81,7 +93,7 @@ __host__ __device__ inline GainLayout make_gain_layout(int n) {
   L.myi = o;    o = cal16(o + n * 2);
   L.out = o;    o = cal16(o + n * 3 * 8);       // u (DistCntrl)
   L.red = o;    o = cal16(o + kCtlWaves * 64 * 3 * 8);  // per-lane partial sums
-  L.atab = o;   o = cal16(o + 30 * 8);          // atan range-reduction table
+  L.atab = o;   o = cal16(o + ACL_ATAB_N * 8);  // atan range-reduction table
   L.total = o;
   return L;
 }
@@ -122,7 +134,11 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
   double* uo = reinterpret_cast<double*>(smem + L.out);
   double* red = reinterpret_cast<double*>(smem + L.red) + wave * 64 * 3;
   double* atab = reinterpret_cast<double*>(smem + L.atab);
-  if (tid < 30) atab[tid] = kAtanTab[tid / 6][tid % 6];
+#if ACL_GAIN_FASTMATH
+  if (tid < ACL_ATAB_N) atab[tid] = kAtan32Tab[tid / 5][tid % 5];
+#else
+  if (tid < ACL_ATAB_N) atab[tid] = kAtanTab[tid / 6][tid % 6];
+#endif
 
   const int f = P.fidx[b];
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
@@ -259,9 +275,9 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
         const int uu = uniform ? Pt[j] : rows[(size_t)v * n + j];
         const double q0 = q[3 * uu] - qv0, q1 = q[3 * uu + 1] - qv1, q2 = q[3 * uu + 2] - qv2;
         const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
-        const double dxy = sqrt_nr((Ni + pn[2 * j]) - 2.0 * (pix * pjx + piy * pjy));
-        const double dz = sqrt_nr((Nzi + pn[2 * j + 1]) - 2.0 * (piz * pjz));
-        const double e_xy = sqrt_nr(q0 * q0 + q1 * q1) - dxy;
+        const double dxy = ACL_GAIN_SQRT((Ni + pn[2 * j]) - 2.0 * (pix * pjx + piy * pjy));
+        const double dz = ACL_GAIN_SQRT((Nzi + pn[2 * j + 1]) - 2.0 * (piz * pjz));
+        const double e_xy = ACL_GAIN_SQRT(q0 * q0 + q1 * q1) - dxy;
         const double e_z = fabs(q2) - dz;  // |q_ij.z| = sqrt(q2^2) (no over/underflow)
         // the two gated atan terms, one after the other (register pressure)
         double Fxy = 0.0, Fz = 0.0;
@@ -270,8 +286,8 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
         for (int kk = 0; kk < 2; ++kk) {
           const bool on = kk ? gz : gxy;
           if (on) {
-            const double fa = kk ? g.K1_z * acl_atan_tab(g.K2_z * e_z, atab)
-                                 : g.K1_xy * acl_atan_tab(g.K2_xy * e_xy, atab);
+            const double fa = kk ? g.K1_z * ACL_GAIN_ATAN(g.K2_z * e_z, atab)
+                                 : g.K1_xy * ACL_GAIN_ATAN(g.K2_xy * e_xy, atab);
             if (kk) Fz = fa; else Fxy = fa;
           }
         }

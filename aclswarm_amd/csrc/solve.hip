@@ -35,6 +35,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/aclswarm_amd.h"
 #include "common.h"
 #include "umeyama_dev.h"
@@ -288,17 +290,26 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
     // lazy scaling multiplies by oon, the other form by 1.0 (exact)
     const double scale = lazy ? oon : 1.0;
     double acc = lazy ? -0.0 : 0.0;
-    for (int jb = 0; jb < n; jb += 32) {
-      const unsigned m = (unsigned)((jb < 64 ? r0 : r1) >> (jb & 63));
+    // 1.0 * x == x exactly: a wave with no lazy-product vehicle skips the
+    // scaling multiply (every vehicle with k + 4 >= 20, e.g. all at n = 100)
+    auto pass2 = [&](auto scaled) {
+      for (int jb = 0; jb < n; jb += 32) {
+        const unsigned m = (unsigned)((jb < 64 ? r0 : r1) >> (jb & 63));
 #pragma unroll
-      for (int x = 0; x < 32; ++x) {
-        const int j = jb + x < n ? jb + x : n - 1;
-        const double s0 = p[3 * j + sj] - smj;
-        const double d0 = scale * (qf[3 * j + di] - dmi);
-        const double pr = d0 * s0;
-        acc += ((m >> x) & 1u) ? pr : -0.0;
+        for (int x = 0; x < 32; ++x) {
+          const int j = jb + x < n ? jb + x : n - 1;
+          const double s0 = p[3 * j + sj] - smj;
+          const double dd = qf[3 * j + di] - dmi;
+          const double d0 = decltype(scaled)::value ? scale * dd : dd;
+          const double pr = d0 * s0;
+          acc += ((m >> x) & 1u) ? pr : -0.0;
+        }
       }
-    }
+    };
+    if (__ballot(act && lazy) != 0ull)
+      pass2(std::true_type{});
+    else
+      pass2(std::false_type{});
     if (act) sums[8 * v + 4 + c] = lazy ? acc : acc * oon;
   }
   __syncthreads();
