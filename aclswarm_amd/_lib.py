@@ -35,6 +35,7 @@ EXPORTS = (
     "acl_control_batch", "acl_write_assignment_log", "acl_read_assignment_log",
     "acl_hungarian_batch",
     "acl_default_episode_params", "acl_episode_workspace_bytes", "acl_episode_batch",
+    "acl_generate_formation_groups",
     "acl_malloc", "acl_free", "acl_memcpy_h2d", "acl_memcpy_d2h", "acl_memset",
     "acl_stream_synchronize", "acl_last_error",
 )
@@ -166,6 +167,10 @@ def lib():
     L.acl_episode_workspace_bytes.restype = SZ
     L.acl_episode_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(EpisodeArgs), VP]
     L.acl_episode_batch.restype = ct.c_int
+    L.acl_generate_formation_groups.argtypes = [I32, I32, VP, I32, ct.c_double, ct.c_double,
+                                                ct.c_double, ct.c_double, I64, VP, VP, VP,
+                                                VP, VP]
+    L.acl_generate_formation_groups.restype = ct.c_int
     L.acl_hungarian_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(HungarianArgs), VP]
     L.acl_hungarian_batch.restype = ct.c_int
     L.acl_write_assignment_log.argtypes = [ct.c_char_p, I32, VP, VP, VP, VP, VP, VP]

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(HERE)
 DRIVER_SRC = os.path.join(ROOT, "tests", "facade_driver.cpp")
 DRIVER = os.path.join(HERE, "lib", "libfacade_driver.so")
 SOURCES = ["solve.hip", "solve_wide.hip", "control.hip", "admm.hip", "hungarian.hip", "episode.hip",
-           "api.cpp"]
+           "formation_gen.hip", "api.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
          "-fPIC", "-shared", "-Wall", "-Wno-unused-function"]

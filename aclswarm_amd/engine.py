@@ -356,3 +356,31 @@ class Episode:
         """Episode counters as a structured numpy array [B]."""
         arr = np.ascontiguousarray(self.est.cpu().numpy())
         return arr.view(L.EPISODE_STATUS_DTYPE).reshape(-1)
+
+
+def generate_formation_groups(seeds, n, fc, l, w, h, min_dist=2.0, max_candidates=0,
+                              stream=None):
+    """acl_generate_formation_groups: the reference's
+    generate_formation_group (generate_random_formation.py:59-80) after
+    np.random.seed(seed), for every seed at once on the device.
+
+    seeds: [F] int tensor on the device (taken as uint32). Returns a dict of
+    device tensors: points [F][2][n][3] f64, adj [F][n][n] u8, status [F]
+    int32, drawn [F] int64 (32-bit outputs consumed)."""
+    dev = seeds.device
+    F = int(seeds.shape[0])
+    s32 = (seeds.to(torch.int64) & 0xFFFFFFFF).to(torch.int32).contiguous()  # uint32 bits
+    out = {
+        "points": torch.empty((F, 2, n, 3), dtype=torch.float64, device=dev),
+        "adj": torch.empty((F, n, n), dtype=torch.uint8, device=dev),
+        "status": torch.empty(F, dtype=torch.int32, device=dev),
+        "drawn": torch.empty(F, dtype=torch.int64, device=dev),
+    }
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    L.check(L.lib().acl_generate_formation_groups(
+        F, n, s32.data_ptr(), int(bool(fc)), float(l), float(w), float(h), float(min_dist),
+        int(max_candidates), out["points"].data_ptr(), out["adj"].data_ptr(),
+        out["status"].data_ptr(), out["drawn"].data_ptr(), ct.c_void_p(stream)),
+        "acl_generate_formation_groups")
+    return out

@@ -423,6 +423,28 @@ size_t acl_episode_workspace_bytes(int32_t n, int32_t B);
 acl_status_t acl_episode_batch(const acl_formations_t* formations,
                                const acl_episode_args_t* args, void* stream);
 
+/* ---- random formation groups on the device -----------
+ * Replaces aclswarm_sim/nodes/generate_random_formation.py:59-80
+ * generate_formation_group(n, fc, l, w, h, min_dist) after
+ * np.random.seed(seeds[g]) (trial.sh:60): numpy's legacy MT19937 stream,
+ * reproduced output for output, so the C2-C5 inputs are the reference
+ * generator's own formations without a host round trip. One wavefront per
+ * group. Device pointers:
+ *   seeds   [F] u32
+ *   points  [F][2][n][3] f64  formations 'A' and 'B', xyz per point
+ *   adj     [F][n][n] u8      adjmat (ones - eye, minus the random pairs
+ *                             unless fc)
+ *   status  [F]               0, or bit k set: formation k needed more than
+ *                             max_candidates samples (the reference gives up
+ *                             after 5 s of wall clock, :35-53, and returns {})
+ *   drawn   [F] i64           32-bit outputs consumed (NULL ok)
+ * n in [1, 512]; a noncomplete group needs n >= 5 (randint(1, n - 3)). */
+acl_status_t acl_generate_formation_groups(int32_t F, int32_t n, const uint32_t* seeds,
+                                           int32_t fc, double l, double w, double h,
+                                           double min_dist, int64_t max_candidates,
+                                           double* points, uint8_t* adj, int32_t* status,
+                                           int64_t* drawn, void* stream);
+
 /* ---- ADMM formation-gain design (admm::Solver::solve, solver.cpp:28-79) -
  * F formations of n points: pts [F][3][n] column-major 3 x n per formation
  * (Eigen::Matrix<double,3,Dynamic>), adj [F][n][n] f64 (symmetric 0/1),

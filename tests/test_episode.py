@@ -204,3 +204,14 @@ def test_episode_defaults_and_argument_errors_without_gpu():
     a.steps = 1
     assert lib.acl_episode_batch(ct.byref(F), ct.byref(a), None) != 0
     assert math.isfinite(e.control_dt)
+
+
+def test_formation_generator_argument_errors_without_gpu():
+    from aclswarm_amd import _lib as L
+    lib = L.lib()
+    z = None
+    assert lib.acl_generate_formation_groups(4, 4, z, 0, 1.0, 1.0, 1.0, 2.0, 0, z, z, z, z, z) != 0
+    assert b"n >= 5" in lib.acl_last_error()
+    assert lib.acl_generate_formation_groups(4, 600, z, 1, 1.0, 1.0, 1.0, 2.0, 0, z, z, z, z, z) != 0
+    assert lib.acl_generate_formation_groups(0, 20, z, 1, 1.0, 1.0, 1.0, 2.0, 0, z, z, z, z, z) == 0
+    assert lib.acl_generate_formation_groups(2, 20, z, 1, 1.0, 1.0, 1.0, 2.0, 0, z, z, z, z, z) != 0
