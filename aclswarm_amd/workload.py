@@ -1,13 +1,12 @@
 """Synthetic batched workloads generated on the device (no host round trip).
 
-Formation groups follow the reference generator's recipe
-(aclswarm_sim/nodes/generate_random_formation.py:20-96): points uniform in an
-l x w x h box, rejection of any point closer than `min_dist` (in xy) to an
-accepted one; noncomplete graphs remove m ~ U[1, n-4] random vertex pairs
-from the complete graph. Start positions follow start.sh:19-61 (discs of
-radius 0.75 in a square, z = takeoff altitude). The random streams are torch
-Philox streams, not the reference's MT19937: bit-exact reproductions of the
-reference generator are the committed fixtures in tests/golden/.
+Formations come from the reference generator itself
+(aclswarm_sim/nodes/generate_random_formation.py:20-96, numpy MT19937 seeded
+per group) run on the device by acl_generate_formation_groups, bit-exact; a
+torch-Philox version of the same recipe is kept for other shapes. Start
+positions follow start.sh:19-61 (discs of radius 0.75 in a square, z =
+takeoff altitude) on torch Philox streams (the reference draws them from the
+shell's $RANDOM).
 
 Gains are synthetic (random values with the reference's block structure is
 not needed for throughput): formation gain design for 65536 unique
@@ -77,8 +76,22 @@ def pack_bits(adj):
     return (pad.view(B, n, W, 64) << shifts).sum(dim=-1)
 
 
+def reference_formations(nf, n, L, complete, seed0, device, h=2.0, min_dist=2.0):
+    """nf formations from the reference's own generator on the device
+    (acl_generate_formation_groups = generate_formation_group after
+    np.random.seed(seed0 + f), generate_random_formation.py:59-80): formation
+    'A' of each group and the group's graph. Returns (p [nf][n][3] f64,
+    adj [nf][n][n] bool)."""
+    from . import engine
+    seeds = torch.arange(seed0, seed0 + nf, dtype=torch.int64, device=device)
+    g = engine.generate_formation_groups(seeds, n, complete, L, L, h, min_dist)
+    if int((g["status"] != 0).sum().item()):
+        raise RuntimeError("reference_formations: a formation did not fit the box")
+    return g["points"][:, 0].contiguous(), g["adj"].bool()
+
+
 def simform_workload(B, n, gen, device, F=None, L=None, complete=False, gains_scale=0.05,
-                     planes=5):
+                     planes=5, formations="reference", seed0=0):
     """Config C3 (n=100, noncomplete, L=40) style batch.
 
     F=None: every swarm has its own formation (points, graph, gains): the
@@ -87,13 +100,19 @@ def simform_workload(B, n, gen, device, F=None, L=None, complete=False, gains_sc
     planes=5: gain blocks with the structure admm::Solver::solve produces
     ([a b 0; c d 0; 0 0 e], solver.cpp:49-77), 5-entry records per edge;
     planes=9: unstructured random 3x3 blocks as 9 planes.
+    formations="reference": points and graphs from the reference generator
+    itself (seeds seed0 .. seed0 + F - 1, bit-exact, on the device);
+    "philox": the same recipe on torch Philox streams.
     Returns dict of device tensors (formation table + swarm inputs).
     """
     if L is None:
         L = 15.0 if n <= 20 else 40.0 * (n / 100.0) ** 0.5
     nf = B if F is None else F
-    p = nonoverlapping_points(nf, n, L, L, 0.0, 2.0, 2.0, gen, device)
-    adj = random_adjacency(nf, n, complete, gen, device)
+    if formations == "reference":
+        p, adj = reference_formations(nf, n, L, complete, seed0, device)
+    else:  # torch Philox streams with the same recipe
+        p = nonoverlapping_points(nf, n, L, L, 0.0, 2.0, 2.0, gen, device)
+        adj = random_adjacency(nf, n, complete, gen, device)
     bits = pack_bits(adj)
     E = adj.sum(dim=(1, 2)).to(torch.int64)
     goff = torch.zeros(nf, dtype=torch.int64, device=device)

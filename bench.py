@@ -158,7 +158,7 @@ def main():
     t0 = time.time()
     w = workload.simform_workload(args.B, args.n, gen, dev,
                                   F=(args.formations or None), complete=False,
-                                  planes=args.gain_planes)
+                                  planes=args.gain_planes, seed0=rank * args.B)
     torch.cuda.synchronize()
     t_gen = time.time() - t0
     T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"],
@@ -251,6 +251,10 @@ def main():
             "workload": "simform100_nc (config C3): noncomplete random formation graphs, "
                         + ("a unique formation (points, graph, gain blocks) per swarm"
                            if not args.formations else f"{args.formations} shared formations"),
+            "formations": "the reference generator (generate_random_formation.py:59-80, "
+                          "L=40, h=2, min_dist=2) after np.random.seed(s), "
+                          f"s = {rank * args.B}..{rank * args.B + (args.formations or args.B) - 1}, "
+                          "reproduced bit-exact on the device",
             "n": n, "B_per_gpu": B, "B_total": world * B,
             "edges_per_formation_avg": e_avg,
             "cbaa": "all 2N rounds" if args.full_rounds else "exact fixed-point exit",
