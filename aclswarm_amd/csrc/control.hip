@@ -25,6 +25,7 @@
 //                  picks the closest safe edge exactly as the reference.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/aclswarm_amd.h"
 #include "common.h"
@@ -110,6 +111,47 @@ __device__ __forceinline__ void saturate(const acl_safety_params_t& sp, double& 
   if (velz > sp.max_vel_z) c2 = c2 / velz * sp.max_vel_z;
 }
 
+// per vehicle (lanes over vehicles): Safety::cmdinCb saturation and the
+// first test of collisionAvoidance -- any other vehicle with
+// !(|dq_xy| > d_avoid_thresh)? |dq_xy|^2 above (thr (1 + 2^-40))^2 is far
+// for certain, so the sqrt is taken only near the threshold. q: the swarm's
+// positions in vehicle order (LDS), uo: DistCntrl's u per vehicle (LDS).
+__device__ void gain_epilogue(const CtlParams& P, int b, int n, const double* q, const double* uo,
+                              int tid) {
+  const acl_safety_params_t sp = P.s;
+  const double thr_hi = sp.d_avoid_thresh * (1.0 + 0x1p-40);
+  const double thr2hi = thr_hi * thr_hi;
+  for (int v = tid; v < n; v += kCtlBlock) {
+    double cmd0 = uo[3 * v], cmd1 = uo[3 * v + 1], cmd2 = uo[3 * v + 2];
+    double* gu = P.u + ((size_t)b * n + v) * 3;
+    gu[0] = cmd0; gu[1] = cmd1; gu[2] = cmd2;
+    saturate(sp, cmd0, cmd1, cmd2);
+    const double qv0 = q[3 * v], qv1 = q[3 * v + 1];
+    bool near = false;  // any j != v with !(s2 > thr2hi) (NaN included)
+    for (int j = 0; j < n; ++j) {
+      const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
+      near |= (j != v) && !(dx * dx + dy * dy > thr2hi);
+    }
+    bool close = false;
+    if (near) {
+      for (int j = 0; j < n; ++j) {
+        const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
+        const double s2 = dx * dx + dy * dy;
+        if (j != v && !(s2 > thr2hi)) close |= !(sqrt(s2) > sp.d_avoid_thresh);
+      }
+    }
+    if (P.u_safe) {
+      double* o = P.u_safe + ((size_t)b * n + v) * 3;
+      o[0] = cmd0; o[1] = cmd1; o[2] = cmd2;
+    }
+    if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 0;
+    if (close) {  // the rest of collisionAvoidance runs in ca_kernel
+      const unsigned slot = atomicAdd(P.ca_count, 1u);
+      P.ca_list[slot] = (unsigned)(b * n + v);
+    }
+  }
+}
+
 // NP = 9: general 3x3 gain blocks; NP = 5: the ADMM block structure, the four
 // structural zeros supplied as constants (acl_formations_t::gain_planes)
 template <int NP>
@@ -123,6 +165,7 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
   const int lane = tid & 63;
   const int wave = tid >> 6;
   if (P.status[b].flags & ACL_SWARM_BAD_INPUT) return;  // auction kernel zeroed outputs
+  if (P.only_nonuniform && P.wsMode[b] == 0) return;    // gain_pair_kernel's swarms
 
   double* q = reinterpret_cast<double*>(smem + L.q);
   double* p = reinterpret_cast<double*>(smem + L.p);
@@ -334,42 +377,283 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
     asm volatile("" ::: "memory");
   }
   __syncthreads();
-  // per vehicle (lanes over vehicles): Safety::cmdinCb saturation and the
-  // first test of collisionAvoidance -- any other vehicle with
-  // !(|dq_xy| > d_avoid_thresh)? |dq_xy|^2 above (thr (1 + 2^-40))^2 is far
-  // for certain, so the sqrt is taken only near the threshold.
-  const acl_safety_params_t sp = P.s;
-  const double thr_hi = sp.d_avoid_thresh * (1.0 + 0x1p-40);
-  const double thr2hi = thr_hi * thr_hi;
-  for (int v = tid; v < n; v += kCtlBlock) {
-    double cmd0 = uo[3 * v], cmd1 = uo[3 * v + 1], cmd2 = uo[3 * v + 2];
-    double* gu = P.u + ((size_t)b * n + v) * 3;
-    gu[0] = cmd0; gu[1] = cmd1; gu[2] = cmd2;
-    saturate(sp, cmd0, cmd1, cmd2);
-    const double qv0 = q[3 * v], qv1 = q[3 * v + 1];
-    bool near = false;  // any j != v with !(s2 > thr2hi) (NaN included)
-    for (int j = 0; j < n; ++j) {
-      const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
-      near |= (j != v) && !(dx * dx + dy * dy > thr2hi);
+  gain_epilogue(P, b, n, q, uo, tid);
+}
+
+// ---- gain_pair_kernel: DistCntrl::compute once per undirected edge ----------
+//
+// The scale terms of distcntrl.cpp:67-83 are symmetric: q_ji = q_i - q_j is
+// -q_ij exactly (IEEE subtraction), so |q_ij.xy|, |q_ij.z|, pdistmat's
+// Gram-formula distances (sums and products commute) and hence e_xy, e_z and
+// the gated atan terms of edge (j, i) equal those of (i, j) bit for bit. This
+// kernel evaluates them once per pair {i, j} and applies both blocks: A_ij
+// q_ij + F q_ij to u_i and A_ji q_ji + F q_ji to u_j -- about 60% of the fp64
+// work of the directed walk. For swarms whose vehicles all adopted the same
+// assignment (wsMode 0: formation row i is vehicle Pt[i]); the others run in
+// gain_kernel.
+//
+// A wave takes 8 x 8 tiles (rows I-block x columns J-block, J >= I; lane =
+// 8 r + c, pair (8I + r, 8J + c); in diagonal tiles r < c, and r == c for a
+// diagonal edge), loading the next tile's two 40-byte records per lane before
+// the current tile's math. Row sums (over c) and column sums (over r) are
+// butterfly shuffles; each wave accumulates into its own u array in LDS in a
+// fixed tile order, and the four arrays are added in wave order: the result
+// is deterministic (tolerance-based parity, 1e-5 relative).
+#ifndef ACL_GAIN_PAIR_WAVES
+#define ACL_GAIN_PAIR_WAVES 5
+#endif
+
+struct PairLayout {
+  int q, qf, p, pn, adjF, rowpre, Pt, acc, out, atab, total;
+};
+
+__host__ __device__ inline PairLayout make_pair_layout(int n) {
+  const int NW = (n + 63) >> 6;
+  PairLayout L;
+  int o = 0;
+  L.q = o;      o = cal16(o + n * 3 * 8);            // vehicle order
+  L.qf = o;     o = cal16(o + n * 3 * 8);            // formation order: qf[i] = q[Pt[i]]
+  L.p = o;      o = cal16(o + n * 3 * 8);
+  L.pn = o;     o = cal16(o + n * 2 * 8);
+  L.adjF = o;   o = cal16(o + n * NW * 8);
+  L.rowpre = o; o = cal16(o + (n * NW + 1) * 4);
+  L.Pt = o;     o = cal16(o + n * 2);
+  L.acc = o;    o = cal16(o + kCtlWaves * n * 3 * 8);  // per-wave u partial sums (row order)
+  L.out = o;    o = cal16(o + n * 3 * 8);            // u per vehicle
+  L.atab = o;   o = cal16(o + ACL_ATAB_N * 8);
+  L.total = o;
+  return L;
+}
+
+__global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kernel(const CtlParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = P.n;
+  const int NW = (n + 63) >> 6;
+  const PairLayout L = make_pair_layout(n);
+  const int b = P.b0 + blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  if (P.status[b].flags & ACL_SWARM_BAD_INPUT) return;
+  if (P.wsMode[b] != 0) return;  // per-vehicle assignments: gain_kernel
+
+  double* q = reinterpret_cast<double*>(smem + L.q);
+  double* qf = reinterpret_cast<double*>(smem + L.qf);
+  double* p = reinterpret_cast<double*>(smem + L.p);
+  double* pn = reinterpret_cast<double*>(smem + L.pn);
+  unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
+  int* rowpre = reinterpret_cast<int*>(smem + L.rowpre);
+  uint16_t* Pt = reinterpret_cast<uint16_t*>(smem + L.Pt);
+  double* acc = reinterpret_cast<double*>(smem + L.acc);
+  double* uo = reinterpret_cast<double*>(smem + L.out);
+  double* atab = reinterpret_cast<double*>(smem + L.atab);
+#if ACL_GAIN_FASTMATH
+  if (tid < ACL_ATAB_N) atab[tid] = kAtan32Tab[tid / 5][tid % 5];
+#else
+  if (tid < ACL_ATAB_N) atab[tid] = kAtanTab[tid / 6][tid % 6];
+#endif
+  const int f = P.fidx[b];
+  const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+  {
+    const double* gq = P.q + (size_t)b * n * 3;
+    const double* gp = P.p + (size_t)f * n * 3;
+    for (int k = tid; k < 3 * n; k += kCtlBlock) {
+      q[k] = gq[k];
+      p[k] = gp[k];
     }
-    bool close = false;
-    if (near) {
-      for (int j = 0; j < n; ++j) {
-        const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
-        const double s2 = dx * dx + dy * dy;
-        if (j != v && !(s2 > thr2hi)) close |= !(sqrt(s2) > sp.d_avoid_thresh);
+    for (int j = tid; j < n; j += kCtlBlock) {
+      const double x = gp[3 * j], y = gp[3 * j + 1], z = gp[3 * j + 2];
+      pn[2 * j] = x * x + y * y;
+      pn[2 * j + 1] = z * z;
+      Pt[j] = P.wsPt[(size_t)b * n + j];
+    }
+    const uint64_t* ga = P.adj + (size_t)f * n * NW;
+    for (int k = tid; k < n * NW; k += kCtlBlock) {
+      unsigned long long x = ga[k];
+      if (k % NW == NW - 1) x &= lastmask;
+      adjF[k] = x;
+    }
+    for (int k = tid; k < kCtlWaves * n * 3; k += kCtlBlock) acc[k] = 0.0;
+  }
+  __syncthreads();
+  for (int k = tid; k < 3 * n; k += kCtlBlock) {
+    const int i = k / 3, c = k - 3 * i;
+    qf[k] = q[3 * Pt[i] + c];
+  }
+  if (wave == 0) {  // edge index of the first bit of every row word (row-major edges)
+    int base = 0;
+    for (int w = 0; w < NW * n; w += 64) {
+      const int k = w + lane;
+      const int cnt = (k < n * NW) ? __popcll(adjF[k]) : 0;
+      int x = cnt;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (k < n * NW) rowpre[k] = base + x - cnt;
+      base += __shfl(x, 63, 64);
+    }
+    if (lane == 0) rowpre[n * NW] = base;
+  }
+  __syncthreads();
+
+  const int E = __builtin_amdgcn_readfirstlane(rowpre[n * NW]);
+  const double* G = P.gains + 5 * P.gain_off[f];
+  const __amdgpu_buffer_rsrc_t grs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 5 * E * 8, 0x00020000);
+  const acl_cntrl_gains_t g = P.g;
+  const int r = lane >> 3, c = lane & 7;
+  const int nb = (n + 7) >> 3;
+  const int NT = nb * (nb + 1) / 2;
+  double* myacc = acc + wave * n * 3;
+
+  // edge index of (i, j), -1 if adjmat(i, j) == 0
+  auto edge_idx = [&](int i, int j) -> int {
+    const int jw = j >> 6, jb = j & 63;
+    const unsigned long long word = adjF[i * NW + jw];
+    if (!((word >> jb) & 1ull)) return -1;
+    return rowpre[i * NW + jw] + __popcll(word & ((1ull << jb) - 1ull));
+  };
+  auto load_rec = [&](int e, double (&Lg)[5]) {
+    const int voff = e >= 0 ? e * 40 : 0x40000000;  // past num_records -> 0
+    const auto r0 = __builtin_amdgcn_raw_buffer_load_b128(grs, voff, 0, 0);
+    const auto r1 = __builtin_amdgcn_raw_buffer_load_b128(grs, voff, 16, 0);
+    const auto r2 = __builtin_amdgcn_raw_buffer_load_b64(grs, voff, 32, 0);
+    __builtin_memcpy(&Lg[0], &r0, 16);
+    __builtin_memcpy(&Lg[2], &r1, 16);
+    __builtin_memcpy(&Lg[4], &r2, 8);
+  };
+  // tile t -> (I, J), J >= I, enumerated row block by row block
+  auto tile_of = [&](int t, int& I, int& J) {
+    int rem = t, ii = 0;
+    while (rem >= nb - ii) {
+      rem -= nb - ii;
+      ++ii;
+    }
+    I = ii;
+    J = ii + rem;
+  };
+  auto lane_pair = [&](int t, int& i, int& j, int& eij, int& eji) {
+    eij = eji = -1;
+    i = j = 0;
+    if (t >= NT) return;
+    int I, J;
+    tile_of(t, I, J);
+    i = 8 * I + r;
+    j = 8 * J + c;
+    if (i >= n || j >= n || (I == J && r > c)) {
+      i = j = 0;
+      return;
+    }
+    eij = edge_idx(i, j);
+    if (i != j) eji = edge_idx(j, i);
+  };
+
+  int i_c, j_c, eij_c, eji_c;
+  lane_pair(wave, i_c, j_c, eij_c, eji_c);
+  double Aij[5], Aji[5];
+  load_rec(eij_c, Aij);
+  load_rec(eji_c, Aji);
+#pragma unroll 1
+  for (int t = wave; t < NT; t += kCtlWaves) {
+    int i_n, j_n, eij_n, eji_n;
+    lane_pair(t + kCtlWaves, i_n, j_n, eij_n, eji_n);
+    double Bij[5], Bji[5];
+    load_rec(eij_n, Bij);
+    load_rec(eji_n, Bji);
+    double rs0 = 0.0, rs1 = 0.0, rs2 = 0.0, cs0 = 0.0, cs1 = 0.0, cs2 = 0.0;
+    if (eij_c >= 0 || eji_c >= 0) {
+#pragma clang fp contract(fast)
+      const int i = i_c, j = j_c;
+      const double q0 = qf[3 * j] - qf[3 * i], q1 = qf[3 * j + 1] - qf[3 * i + 1],
+                   q2 = qf[3 * j + 2] - qf[3 * i + 2];
+      const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
+      const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
+      const double dxy = ACL_GAIN_SQRT((pn[2 * i] + pn[2 * j]) - 2.0 * (pix * pjx + piy * pjy));
+      const double dz = ACL_GAIN_SQRT((pn[2 * i + 1] + pn[2 * j + 1]) - 2.0 * (piz * pjz));
+      const double e_xy = ACL_GAIN_SQRT(q0 * q0 + q1 * q1) - dxy;
+      const double e_z = fabs(q2) - dz;
+      double Fxy = 0.0, Fz = 0.0;
+      const bool gxy = fabs(e_xy) > g.e_xy_thr, gz = fabs(e_z) > g.e_z_thr;
+#pragma unroll 1
+      for (int kk = 0; kk < 2; ++kk) {
+        const bool on = kk ? gz : gxy;
+        if (on) {
+          const double fa = kk ? g.K1_z * ACL_GAIN_ATAN(g.K2_z * e_z, atab)
+                               : g.K1_xy * ACL_GAIN_ATAN(g.K2_xy * e_xy, atab);
+          if (kk) Fz = fa; else Fxy = fa;
+        }
+      }
+      // (0,0) (0,1) (1,0) (1,1) (2,2) stored; the structural zeros still
+      // multiply q (solver.cpp:49-77, NaN propagation as the 3x3 product)
+      if (eij_c >= 0) {
+        const double up0 = ((Aij[0] * q0 + Aij[1] * q1) + 0.0 * q2) + Fxy * q0;
+        const double up1 = ((Aij[2] * q0 + Aij[3] * q1) + 0.0 * q2) + Fxy * q1;
+        const double up2 = ((0.0 * q0 + 0.0 * q1) + Aij[4] * q2) + Fz * q2;
+        rs0 = g.kp * up0; rs1 = g.kp * up1; rs2 = g.kp * up2;
+      }
+      if (eji_c >= 0) {
+        const double m0 = -q0, m1 = -q1, m2 = -q2;  // q_ji
+        const double up0 = ((Aji[0] * m0 + Aji[1] * m1) + 0.0 * m2) + Fxy * m0;
+        const double up1 = ((Aji[2] * m0 + Aji[3] * m1) + 0.0 * m2) + Fxy * m1;
+        const double up2 = ((0.0 * m0 + 0.0 * m1) + Aji[4] * m2) + Fz * m2;
+        cs0 = g.kp * up0; cs1 = g.kp * up1; cs2 = g.kp * up2;
       }
     }
-    if (P.u_safe) {
-      double* o = P.u_safe + ((size_t)b * n + v) * 3;
-      o[0] = cmd0; o[1] = cmd1; o[2] = cmd2;
+    // row sums over c (lanes 8r .. 8r + 7), column sums over r (stride 8)
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      rs0 += __shfl_xor(rs0, o, 64); rs1 += __shfl_xor(rs1, o, 64); rs2 += __shfl_xor(rs2, o, 64);
     }
-    if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 0;
-    if (close) {  // the rest of collisionAvoidance runs in ca_kernel
-      const unsigned slot = atomicAdd(P.ca_count, 1u);
-      P.ca_list[slot] = (unsigned)(b * n + v);
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+      cs0 += __shfl_xor(cs0, o, 64); cs1 += __shfl_xor(cs1, o, 64); cs2 += __shfl_xor(cs2, o, 64);
+    }
+    {
+      int I, J;
+      tile_of(t, I, J);
+      const int ri = 8 * I + r, cj = 8 * J + c;
+      if (c == 0 && ri < n) {
+        myacc[3 * ri] += rs0; myacc[3 * ri + 1] += rs1; myacc[3 * ri + 2] += rs2;
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      if (r == 0 && cj < n) {
+        myacc[3 * cj] += cs0; myacc[3 * cj + 1] += cs1; myacc[3 * cj + 2] += cs2;
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+    i_c = i_n; j_c = j_n; eij_c = eij_n; eji_c = eji_n;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      Aij[k] = Bij[k];
+      Aji[k] = Bji[k];
     }
   }
+  __syncthreads();
+  // u of the vehicle at row i: the four waves' sums in wave order, plus
+  // kd (-vel) once per edge of row i (distcntrl.cpp:85-95)
+  for (int i = tid; i < n; i += kCtlBlock) {
+    const int v = Pt[i];
+    int deg = 0;
+    for (int w = 0; w < NW; ++w) deg += __popcll(adjF[i * NW + w]);
+    double u0 = 0.0, u1 = 0.0, u2 = 0.0;
+    for (int w = 0; w < kCtlWaves; ++w) {
+      const double* a = acc + w * n * 3 + 3 * i;
+      u0 += a[0]; u1 += a[1]; u2 += a[2];
+    }
+    if (deg) {
+      const double* gv = P.vel + ((size_t)b * n + v) * 3;
+      const double cn = (double)deg;
+      u0 += cn * (g.kd * (-gv[0]));
+      u1 += cn * (g.kd * (-gv[1]));
+      u2 += cn * (g.kd * (-gv[2]));
+    }
+    uo[3 * v] = u0; uo[3 * v + 1] = u1; uo[3 * v + 2] = u2;
+  }
+  __syncthreads();
+  gain_epilogue(P, b, n, q, uo, tid);
 }
 
 // collisionAvoidance (safety.cpp:412-541) for the vehicles gain_kernel
@@ -580,16 +864,39 @@ hipError_t launch_control_prep(const CtlParams& P, const uint16_t* Pgiven, int n
   return hipGetLastError();
 }
 
+// ACLSWARM_AMD_GAIN_PAIR=0 selects the directed walk (gain_kernel) for every
+// swarm (diagnostic A/B switch; read once).
+static bool gain_pair_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("ACLSWARM_AMD_GAIN_PAIR");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  return on != 0;
+}
+
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream) {
   if (which == 0) {
+    CtlParams Q = P;
+    Q.only_nonuniform = 0;
+    if (P.gain_planes == 5 && gain_pair_enabled()) {
+      // uniform swarms: one evaluation per undirected edge; then gain_kernel
+      // for the swarms whose vehicles hold different assignments
+      const PairLayout PL = make_pair_layout(P.n);
+      if (PL.total > 64 * 1024)
+        (void)hipFuncSetAttribute((const void*)gain_pair_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, PL.total);
+      hipLaunchKernelGGL(gain_pair_kernel, dim3(nb), dim3(kCtlBlock), PL.total, stream, Q);
+      Q.only_nonuniform = 1;
+    }
     const GainLayout L = make_gain_layout(P.n);
     const void* k = P.gain_planes == 5 ? (const void*)gain_kernel<5> : (const void*)gain_kernel<9>;
     if (L.total > 64 * 1024)
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, L.total);
     if (P.gain_planes == 5)
-      hipLaunchKernelGGL(gain_kernel<5>, dim3(nb), dim3(kCtlBlock), L.total, stream, P);
+      hipLaunchKernelGGL(gain_kernel<5>, dim3(nb), dim3(kCtlBlock), L.total, stream, Q);
     else
-      hipLaunchKernelGGL(gain_kernel<9>, dim3(nb), dim3(kCtlBlock), L.total, stream, P);
+      hipLaunchKernelGGL(gain_kernel<9>, dim3(nb), dim3(kCtlBlock), L.total, stream, Q);
   } else {
     // a fixed grid striding over the device-side count of listed vehicles
     const int lds = kCaWaves * ca_wave_bytes(P.n);

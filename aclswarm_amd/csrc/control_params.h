@@ -94,6 +94,7 @@ struct CtlParams {
   unsigned* ca_count;
   acl_cntrl_gains_t g;
   acl_safety_params_t s;
+  int only_nonuniform;  // set by launch_control: gain_kernel skips uniform swarms
 };
 
 // misc int slots of the auction kernels' LDS

@@ -221,7 +221,9 @@ def main():
     per_launch = {"auction": a_all / nlaunch, "gain": g_all / nlaunch, "ca": s_all / nlaunch}
     kern = {}
     for k, (name, sym) in enumerate((("auction", "acl_amd::solve_kernel"),
-                                     ("gain", f"acl_amd::gain_kernel<{w['planes']}>"),
+                                     ("gain", "acl_amd::gain_pair_kernel" if w["planes"] == 5
+                                      and os.environ.get("ACLSWARM_AMD_GAIN_PAIR", "1") != "0"
+                                      else f"acl_amd::gain_kernel<{w['planes']}>"),
                                      ("ca", "acl_amd::ca_kernel"))):
         avg = kms[k] / max(kcnt[k], 1)
         ach = per_launch[name] / (avg * 1e-3) / 1e9

@@ -342,9 +342,9 @@ def test_align_rt_output(cuda):
 
 
 def test_gain_layouts_5_and_9_planes(cuda):
-    """ADMM-structured gains: the 5-entry record table gives bit-identical commands to
-    the 9-plane table of the same GainMat; unstructured blocks (9 planes
-    only) match the oracle."""
+    """ADMM-structured gains: the 5-entry record table gives the commands of
+    the 9-plane table of the same GainMat (to summation order); unstructured
+    blocks (9 planes only) match the oracle."""
     import torch
     from aclswarm_amd import engine
     P20, A20 = H.simform("simform20_nc")
@@ -371,8 +371,13 @@ def test_gain_layouts_5_and_9_planes(cuda):
     r5, np5 = run(structured, None)
     r9, np9 = run(structured, 9)
     assert (np5, np9) == (5, 9)
-    for k in ("u", "u_safe", "ca_flag", "P_out"):
+    # the 5-entry table runs gain_pair_kernel (one evaluation per undirected
+    # edge), the 9-plane table the directed walk: same terms, different
+    # summation order
+    for k in ("ca_flag", "P_out"):
         np.testing.assert_array_equal(r5[k], r9[k], err_msg=k)
+    for k in ("u", "u_safe"):
+        np.testing.assert_allclose(r5[k], r9[k], rtol=1e-12, atol=1e-12, err_msg=k)
     general = [H.random_block_gains(rng, a, scale=1.0) for a in adjs]
     gpu = _gpu_solve(pts, adjs, general, fidx, q, vel, P_in)
     ref = _oracle(pts, adjs, general, fidx, q, vel, P_in)
