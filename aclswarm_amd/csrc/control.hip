@@ -887,6 +887,7 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
         (void)hipFuncSetAttribute((const void*)gain_pair_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, PL.total);
       hipLaunchKernelGGL(gain_pair_kernel, dim3(nb), dim3(kCtlBlock), PL.total, stream, Q);
+      if (P.all_uniform) return hipGetLastError();
       Q.only_nonuniform = 1;
     }
     const GainLayout L = make_gain_layout(P.n);

@@ -95,6 +95,7 @@ struct CtlParams {
   acl_cntrl_gains_t g;
   acl_safety_params_t s;
   int only_nonuniform;  // set by launch_control: gain_kernel skips uniform swarms
+  int all_uniform;      // every swarm has one assignment (given P): no gain_kernel pass
 };
 
 // misc int slots of the auction kernels' LDS
@@ -109,6 +110,14 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
 // permutation check, inverse assignment, status.
 hipError_t launch_control_prep(const CtlParams& P, const uint16_t* Pgiven, int nb,
                                hipStream_t stream);
+
+// acl_control_batch's stages (solve.hip): flags CTL_PREP runs the hand-off
+// kernel (permutation check, inverse assignment, status), CTL_RESET zeroes
+// the collision-avoidance count first; without them the hand-off of the
+// previous call with the same P and workspace is reused (acl_episode_batch).
+enum { CTL_PREP = 1, CTL_RESET = 2 };
+acl_status_t run_control(const acl_formations_t* F, const acl_control_args_t* a, hipStream_t s,
+                         int flags);
 
 // The n > 128 auction kernel (solve_wide.hip).
 hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream);

@@ -99,6 +99,7 @@ struct TrajParams {
   double* u_hist;
   uint8_t* ca_hist;
   uint16_t* P_hist;
+  unsigned* ca_count;  // the control stage's collision-avoidance count
   acl_episode_params_t ep;
 };
 
@@ -126,6 +127,8 @@ __global__ void __launch_bounds__(kEpBlock) traj_kernel(const TrajParams T) {
     s_all_conv = 1;
     s_any_grid = 0;
     s_nca = 0;
+    // ca_kernel has consumed the list (stream order): reset for the next step
+    if (b == 0) *T.ca_count = 0u;
   }
   __syncthreads();
   const uint32_t m0 = T.est[b].n_samples;  // ticks before this one
@@ -274,16 +277,22 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
   T.est = a->est; T.ring_u = a->ring_u; T.ring_ca = a->ring_ca;
   T.q_hist = a->q_hist; T.vel_hist = a->vel_hist; T.u_hist = a->u_hist; T.ca_hist = a->ca_hist; T.P_hist = a->P_hist;
   T.ep = ep;
+  // the control hand-off (inverse assignment) depends only on P: it is
+  // rebuilt on the first step of a call and after every auction (which also
+  // overwrites it); the collision-avoidance count is zeroed by traj_kernel
+  T.ca_count = reinterpret_cast<unsigned*>(ws + W.solve + ws_layout(n, B).cacount);
   for (int k = 0; k < a->steps; ++k) {
     const int step = a->step0 + k;
+    int flags = k == 0 ? (CTL_PREP | CTL_RESET) : 0;
     if (step % ep.auction_every == 0) {
       const acl_status_t r = acl_solve_batch(F, &sa, stream);
       if (r != ACL_OK) return r;
       hipLaunchKernelGGL(adopt_kernel, dim3(B), dim3(64), 0, s, n, a->P, Pnew, st, a->flush,
                          a->est);
       if (hipGetLastError() != hipSuccess) return acl__set_error("adopt_kernel launch failed");
+      flags |= CTL_PREP | CTL_RESET;
     }
-    const acl_status_t r = acl_control_batch(F, &cs, stream);
+    const acl_status_t r = run_control(F, &cs, s, flags);
     if (r != ACL_OK) return r;
     T.step = step;
     T.k = k;

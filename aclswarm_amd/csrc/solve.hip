@@ -763,6 +763,8 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   C.ca_list = reinterpret_cast<unsigned*>(P.ws + P.W.calist);
   C.ca_count = reinterpret_cast<unsigned*>(P.ws + P.W.cacount);
   C.g = a->cntrl; C.s = a->safety;
+  C.only_nonuniform = 0;
+  C.all_uniform = 0;
   if (hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
     return acl__set_error("hipMemsetAsync failed");
   for (int which = 0; which < 2; ++which) {
@@ -774,8 +776,8 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   return ACL_OK;
 }
 
-extern "C" acl_status_t acl_control_batch(const acl_formations_t* F, const acl_control_args_t* a,
-                                          void* stream) {
+acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_args_t* a,
+                                  hipStream_t s, int flags) {
   using namespace acl_amd;
   if (!F || !a) return acl__set_error("acl_control_batch: null argument");
   const int n = F->n;
@@ -803,14 +805,23 @@ extern "C" acl_status_t acl_control_batch(const acl_formations_t* F, const acl_c
   C.ca_list = reinterpret_cast<unsigned*>(ws + W.calist);
   C.ca_count = reinterpret_cast<unsigned*>(ws + W.cacount);
   C.g = a->cntrl; C.s = a->safety;
-  hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
+  C.only_nonuniform = 0;
+  C.all_uniform = 1;  // the hand-off of a given P is one assignment per swarm
+  if ((flags & CTL_RESET) && hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
     return acl__set_error("hipMemsetAsync failed");
-  hipError_t e = launch_control_prep(C, a->P, a->B, s);
-  if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+  hipError_t e = hipSuccess;
+  if (flags & CTL_PREP) {
+    e = launch_control_prep(C, a->P, a->B, s);
+    if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+  }
   for (int which = 0; which < 2; ++which) {
     e = launch_control(C, a->B, which, s);
     if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
   }
   return ACL_OK;
+}
+
+extern "C" acl_status_t acl_control_batch(const acl_formations_t* F, const acl_control_args_t* a,
+                                          void* stream) {
+  return acl_amd::run_control(F, a, (hipStream_t)stream, acl_amd::CTL_PREP | acl_amd::CTL_RESET);
 }

@@ -52,7 +52,7 @@ def main():
     st = e.status()
     ep = e.ep
     line = {
-        "metric": "closed-loop episode swarm-steps/sec (N=100)",
+        "metric": f"closed-loop episode swarm-steps/sec (N={args.n})",
         "value": args.B * args.steps / dt, "unit": "swarm-steps/s",
         "B": args.B, "n": args.n, "steps": args.steps, "seconds": dt,
         "ms_per_step": dt / args.steps * 1e3,
