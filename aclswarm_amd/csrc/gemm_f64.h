@@ -5,8 +5,8 @@
 // live in device memory, so a setup kernel may fill them and converged
 // problems drop out without a host round trip).
 //
-// Tiling: 64 x 64 output tile per 256-thread workgroup, four waves in a 2 x 2
-// arrangement, each wave 2 x 2 MFMA 16x16 tiles; K staged through LDS in
+// Tiling: a 64 x 64 (or 32 x 32) output tile per 256-thread workgroup, four
+// waves in a 2 x 2 arrangement, each wave 2 x 2 (1 x 1) MFMA 16x16 tiles; K staged through LDS in
 // steps of 16 with a register-prefetched double buffer (one barrier per step).
 // The MFMA is issued with the operands swapped (it computes the tile of D^T),
 // so the accumulator's lane index runs along D's rows and every epilogue
@@ -14,6 +14,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 namespace acl_amd {
 
@@ -30,42 +31,55 @@ struct GemmJob {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kGemmTile = 64;
 constexpr int kGemmKStep = 16;
-constexpr int kGemmPad = 80;  // LDS row stride in doubles: 160 words = 32 banks shift
+#ifndef ACL_GEMM_TILE_DEFAULT
+#define ACL_GEMM_TILE_DEFAULT 64
+#endif
 
 // op(A)[i][kk]: TA ? A[kk + i*lda] : A[i + kk*lda]
 // op(B)[kk][j]: TB ? B[j + kk*ldb] : B[kk + j*ldb]
-template <bool TA, bool TB>
+// TW = MFMA 16x16 tiles per wave per dimension: TW = 2 -> 64 x 64 output
+// tile per workgroup, TW = 1 -> 32 x 32 (less padding on the ADMM's 392- and
+// 196-sized products, but one accumulator per wave).
+template <bool TA, bool TB, int TW>
 __global__ void __launch_bounds__(256) gemm_f64_kernel(const GemmJob* __restrict__ jobs,
                                                           unsigned long long* flops) {
+  constexpr int TILE = 32 * TW;
+  constexpr int EPT = TILE / 16;  // operand elements each thread stages per K step
   const GemmJob J = jobs[blockIdx.z];
   if (J.skip && *J.skip) return;
-  const int m0 = blockIdx.x * kGemmTile, n0 = blockIdx.y * kGemmTile;
+  const int m0 = blockIdx.x * TILE, n0 = blockIdx.y * TILE;
   if (m0 >= J.m || n0 >= J.n) return;
   if (flops && threadIdx.x == 0)  // algorithmic flops of this tile (diagnostics)
-    atomicAdd(flops, 2ull * (unsigned long long)min(kGemmTile, J.m - m0) *
-                         (unsigned long long)min(kGemmTile, J.n - n0) * (unsigned long long)J.k);
-  __shared__ double As[2][kGemmKStep][kGemmPad];
-  __shared__ double Bs[2][kGemmKStep][kGemmPad];
+    atomicAdd(flops, 2ull * (unsigned long long)min(TILE, J.m - m0) *
+                         (unsigned long long)min(TILE, J.n - n0) * (unsigned long long)J.k);
+  constexpr int PAD = TILE + 16;  // LDS row stride in doubles (bank shift)
+  __shared__ double As[2][kGemmKStep][PAD];
+  __shared__ double Bs[2][kGemmKStep][PAD];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
 
-  double ra[4], rb[4];
+  double ra[EPT], rb[EPT];
+  auto a_idx = [&](int r, int& i, int& kk) {
+    if (!TA) { i = tid % TILE; kk = tid / TILE + (256 / TILE) * r; }
+    else     { kk = tid & 15; i = (tid >> 4) + 16 * r; }
+  };
+  auto b_idx = [&](int r, int& j, int& kb) {
+    if (TB) { j = tid % TILE; kb = tid / TILE + (256 / TILE) * r; }
+    else    { kb = tid & 15; j = (tid >> 4) + 16 * r; }
+  };
   auto load = [&](int k0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < EPT; ++r) {
       int i, kk;
-      if (!TA) { i = tid & 63; kk = (tid >> 6) + 4 * r; }
-      else     { kk = tid & 15; i = (tid >> 4) + 16 * r; }
+      a_idx(r, i, kk);
       const int gi = m0 + i, gk = k0 + kk;
       ra[r] = (gi < J.m && gk < J.k)
                   ? (TA ? J.A[gk + (size_t)gi * J.lda] : J.A[gi + (size_t)gk * J.lda])
                   : 0.0;
       int j, kb;
-      if (TB) { j = tid & 63; kb = (tid >> 6) + 4 * r; }
-      else    { kb = tid & 15; j = (tid >> 4) + 16 * r; }
+      b_idx(r, j, kb);
       const int gj = n0 + j, gkb = k0 + kb;
       rb[r] = (gj < J.n && gkb < J.k)
                   ? (TB ? J.B[gj + (size_t)gkb * J.ldb] : J.B[gkb + (size_t)gj * J.ldb])
@@ -74,23 +88,21 @@ __global__ void __launch_bounds__(256) gemm_f64_kernel(const GemmJob* __restrict
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < EPT; ++r) {
       int i, kk;
-      if (!TA) { i = tid & 63; kk = (tid >> 6) + 4 * r; }
-      else     { kk = tid & 15; i = (tid >> 4) + 16 * r; }
+      a_idx(r, i, kk);
       As[buf][kk][i] = ra[r];
       int j, kb;
-      if (TB) { j = tid & 63; kb = (tid >> 6) + 4 * r; }
-      else    { kb = tid & 15; j = (tid >> 4) + 16 * r; }
+      b_idx(r, j, kb);
       Bs[buf][kb][j] = rb[r];
     }
   };
 
-  f64x4 acc[2][2];
+  f64x4 acc[TW][TW];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TW; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int b = 0; b < TW; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
 
   const int nk = (J.k + kGemmKStep - 1) / kGemmKStep;
   if (nk > 0) {
@@ -104,16 +116,16 @@ __global__ void __launch_bounds__(256) gemm_f64_kernel(const GemmJob* __restrict
 #pragma unroll
     for (int k4 = 0; k4 < kGemmKStep; k4 += 4) {
       const int kr = k4 + (lane >> 4);
-      double av[2], bv[2];
+      double av[TW], bv[TW];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        av[t] = As[cur][kr][wm * 32 + t * 16 + (lane & 15)];
-        bv[t] = Bs[cur][kr][wn * 32 + t * 16 + (lane & 15)];
+      for (int t = 0; t < TW; ++t) {
+        av[t] = As[cur][kr][wm * 16 * TW + t * 16 + (lane & 15)];
+        bv[t] = Bs[cur][kr][wn * 16 * TW + t * 16 + (lane & 15)];
       }
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < TW; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < TW; ++b)
           // swapped operands: the MFMA tile is D^T, lane&15 runs along D's rows
           acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(bv[b], av[a], acc[a][b], 0, 0, 0);
     }
@@ -123,13 +135,13 @@ __global__ void __launch_bounds__(256) gemm_f64_kernel(const GemmJob* __restrict
 
   const double alpha = J.alpha, beta = J.beta;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TW; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < TW; ++b)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int gi = m0 + wm * 32 + a * 16 + (lane & 15);
-        const int gj = n0 + wn * 32 + b * 16 + (lane >> 4) + 4 * r;
+        const int gi = m0 + wm * 16 * TW + a * 16 + (lane & 15);
+        const int gj = n0 + wn * 16 * TW + b * 16 + (lane >> 4) + 4 * r;
         if (gi < J.m && gj < J.n) {
           double v = alpha * acc[a][b][r];
           if (beta != 0.0) v += beta * J.C[gi + (size_t)gj * J.ldc];
@@ -138,16 +150,37 @@ __global__ void __launch_bounds__(256) gemm_f64_kernel(const GemmJob* __restrict
       }
 }
 
+// Output tile per workgroup: 64 (default) or 32 (ACLSWARM_AMD_GEMM_TILE=32).
+// Measured on C5 (N=100, F=1024): 548 ms per batch with 64, 684 ms with 32
+// (the 32-tile wave holds one accumulator: less padding, but dependent MFMAs).
+inline int gemm_tile() {
+  static int t = 0;
+  if (!t) {
+    const char* e = getenv("ACLSWARM_AMD_GEMM_TILE");
+    t = e ? (e[0] == '3' ? 32 : 64) : ACL_GEMM_TILE_DEFAULT;
+  }
+  return t;
+}
+
 // Host launcher: `jobs` is a device array of `njobs` descriptors whose m, n
 // are bounded by mmax, nmax.
 inline hipError_t gemm_f64(bool ta, bool tb, const GemmJob* jobs, int njobs, int mmax, int nmax,
                            hipStream_t s, unsigned long long* flops = nullptr) {
   if (njobs <= 0 || mmax <= 0 || nmax <= 0) return hipSuccess;
-  const dim3 grid((mmax + kGemmTile - 1) / kGemmTile, (nmax + kGemmTile - 1) / kGemmTile, njobs);
-  if (!ta && !tb) hipLaunchKernelGGL((gemm_f64_kernel<false, false>), grid, dim3(256), 0, s, jobs, flops);
-  else if (!ta && tb) hipLaunchKernelGGL((gemm_f64_kernel<false, true>), grid, dim3(256), 0, s, jobs, flops);
-  else if (ta && !tb) hipLaunchKernelGGL((gemm_f64_kernel<true, false>), grid, dim3(256), 0, s, jobs, flops);
-  else hipLaunchKernelGGL((gemm_f64_kernel<true, true>), grid, dim3(256), 0, s, jobs, flops);
+  const int T = gemm_tile();
+  const dim3 grid((mmax + T - 1) / T, (nmax + T - 1) / T, njobs);
+#define ACL_GEMM_LAUNCH(TA_, TB_)                                                            \
+  do {                                                                                       \
+    if (T == 64)                                                                             \
+      hipLaunchKernelGGL((gemm_f64_kernel<TA_, TB_, 2>), grid, dim3(256), 0, s, jobs, flops); \
+    else                                                                                     \
+      hipLaunchKernelGGL((gemm_f64_kernel<TA_, TB_, 1>), grid, dim3(256), 0, s, jobs, flops); \
+  } while (0)
+  if (!ta && !tb) ACL_GEMM_LAUNCH(false, false);
+  else if (!ta && tb) ACL_GEMM_LAUNCH(false, true);
+  else if (ta && !tb) ACL_GEMM_LAUNCH(true, false);
+  else ACL_GEMM_LAUNCH(true, true);
+#undef ACL_GEMM_LAUNCH
   return hipGetLastError();
 }
 
