@@ -31,7 +31,7 @@ STATUS_DTYPE = np.dtype([("flags", "<u4"), ("eff_rounds", "<u2"),
 EXPORTS = (
     "acl_default_cntrl_gains", "acl_default_safety_params", "acl_default_admm_params",
     "acl_max_vehicles", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
-    "acl_pack_gains", "acl_gain_planes", "acl_pack_gains_planes", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
+    "acl_pack_gains", "acl_gain_planes", "acl_pack_gains_planes", "acl_tile_gains", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
     "acl_control_batch", "acl_write_assignment_log", "acl_read_assignment_log",
     "acl_hungarian_batch",
     "acl_default_episode_params", "acl_episode_workspace_bytes", "acl_episode_batch",
@@ -64,7 +64,8 @@ class AdmmParams(ct.Structure):
 class Formations(ct.Structure):
     _fields_ = [("n", ct.c_int32), ("n_formations", ct.c_int32),
                 ("p", ct.c_void_p), ("adj", ct.c_void_p), ("gains", ct.c_void_p),
-                ("gain_off", ct.c_void_p), ("gain_planes", ct.c_int32)]
+                ("gain_off", ct.c_void_p), ("gain_planes", ct.c_int32),
+                ("gains_tiled", ct.c_void_p)]
 
 
 class SolveArgs(ct.Structure):
@@ -157,6 +158,8 @@ def lib():
     L.acl_gain_planes.restype = I32
     L.acl_pack_gains_planes.argtypes = [I32, VP, VP, I32, VP]
     L.acl_pack_gains_planes.restype = ct.c_int
+    L.acl_tile_gains.argtypes = [ct.POINTER(Formations), VP, VP]
+    L.acl_tile_gains.restype = ct.c_int
     L.acl_admm_solve_batch.argtypes = [I32, I32, VP, VP, VP, VP, ct.POINTER(AdmmParams), VP]
     L.acl_admm_solve_batch.restype = ct.c_int
     L.acl_control_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(ControlArgs), VP]

@@ -403,8 +403,89 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
 #define ACL_GAIN_PAIR_WAVES 5
 #endif
 
+// ---- tiled gain records (acl_formations_t::gains_tiled, acl_tile_gains) ----
+// Tile t = (I, J), J >= I, row block by row block, is what one wave of
+// gain_pair_kernel evaluates: lane = 8r + c takes the pair (8I + r, 8J + c).
+// Its records are two runs in lane order: first edge (i, j) of every lane
+// (run 1, mask tmask[2t]), then edge (j, i) of every lane (run 2, mask
+// tmask[2t + 1]); on a diagonal tile run 1 holds the lanes r <= c and run 2
+// the lanes r < c. A lane's record index is then its run's first record
+// plus the mask bits below the lane (v_mbcnt).
+__host__ __device__ inline int pair_tiles(int n) {
+  const int nb = (n + 7) >> 3;
+  return nb * (nb + 1) / 2;
+}
+
+__device__ __forceinline__ void tile_ij(int t, int nb, int& I, int& J) {
+  int rem = t, ii = 0;
+  while (rem >= nb - ii) {
+    rem -= nb - ii;
+    ++ii;
+  }
+  I = ii;
+  J = ii + rem;
+}
+
+// block (I, J) of the adjacency, bit 8r + c = adjmat(8I + r, 8J + c); adjF
+// rows are masked past n
+__device__ __forceinline__ unsigned long long block_mask(const unsigned long long* adjF, int NW,
+                                                         int n, int I, int J) {
+  unsigned long long m = 0ull;
+  const int cw = (8 * J) >> 6, cb = (8 * J) & 63;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int i = 8 * I + r;
+    if (i < n) m |= ((adjF[i * NW + cw] >> cb) & 0xFFull) << (8 * r);
+  }
+  return m;
+}
+
+// 8 x 8 bit-matrix transpose (bit 8r + c -> bit 8c + r)
+__device__ __forceinline__ unsigned long long transpose8(unsigned long long x) {
+  unsigned long long t;
+  t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;  x ^= t ^ (t << 7);
+  t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull; x ^= t ^ (t << 14);
+  t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull; x ^= t ^ (t << 28);
+  return x;
+}
+
+constexpr unsigned long long kUpperIncl = 0x80C0E0F0F8FCFEFFull;  // bits 8r + c, r <= c
+
+// one wave: tile masks and run offsets (exclusive scan in tile order)
+__device__ void build_tiles(const unsigned long long* adjF, int NW, int n, int lane,
+                            unsigned long long* tm, int* ts) {
+  const int nb = (n + 7) >> 3, NT = pair_tiles(n);
+  int base = 0;
+  for (int t0 = 0; t0 < NT; t0 += 64) {
+    const int t = t0 + lane;
+    int cnt = 0, ca = 0;
+    if (t < NT) {
+      int I, J;
+      tile_ij(t, nb, I, J);
+      const unsigned long long b = block_mask(adjF, NW, n, I, J);
+      const unsigned long long a = I == J ? (b & kUpperIncl) : b;
+      const unsigned long long m2 = I == J ? (transpose8(b) & kUpperIncl & ~0x8040201008040201ull)
+                                           : transpose8(block_mask(adjF, NW, n, J, I));
+      tm[2 * t] = a;
+      tm[2 * t + 1] = m2;
+      ca = __popcll(a);
+      cnt = ca + __popcll(m2);
+    }
+    int x = cnt;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (t < NT) {
+      ts[2 * t] = base + x - cnt;
+      ts[2 * t + 1] = base + x - cnt + ca;
+    }
+    base += __shfl(x, 63, 64);
+  }
+}
+
 struct PairLayout {
-  int q, qf, p, pn, adjF, rowpre, Pt, acc, out, atab, total;
+  int q, qf, p, pn, adjF, rowpre, Pt, acc, out, atab, tmask, tstart, total;
 };
 
 __host__ __device__ inline PairLayout make_pair_layout(int n) {
@@ -421,10 +502,14 @@ __host__ __device__ inline PairLayout make_pair_layout(int n) {
   L.acc = o;    o = cal16(o + kCtlWaves * n * 3 * 8);  // per-wave u partial sums (row order)
   L.out = o;    o = cal16(o + n * 3 * 8);            // u per vehicle
   L.atab = o;   o = cal16(o + ACL_ATAB_N * 8);
+  const int NT = n <= kMaxN ? pair_tiles(n) : 0;   // tiled records: n <= 128 only
+  L.tmask = o;  o = cal16(o + 2 * NT * 8);
+  L.tstart = o; o = cal16(o + 2 * NT * 4);
   L.total = o;
   return L;
 }
 
+template <bool kTiled>
 __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
@@ -495,10 +580,14 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
     }
     if (lane == 0) rowpre[n * NW] = base;
   }
+  constexpr bool tiled = kTiled;  // P.gains_tiled != NULL
+  unsigned long long* tmask = reinterpret_cast<unsigned long long*>(smem + L.tmask);
+  int* tstart = reinterpret_cast<int*>(smem + L.tstart);
+  if (tiled && wave == 1) build_tiles(adjF, NW, n, lane, tmask, tstart);
   __syncthreads();
 
   const int E = __builtin_amdgcn_readfirstlane(rowpre[n * NW]);
-  const double* G = P.gains + 5 * P.gain_off[f];
+  const double* G = (tiled ? P.gains_tiled : P.gains) + 5 * P.gain_off[f];
   const __amdgpu_buffer_rsrc_t grs =
       __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 5 * E * 8, 0x00020000);
   const acl_cntrl_gains_t g = P.g;
@@ -543,6 +632,24 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
     j = 8 * J + c;
     if (i >= n || j >= n || (I == J && r > c)) {
       i = j = 0;
+      return;
+    }
+    if (tiled) {  // record index within the tile's contiguous run
+      // t is wave-uniform: the masks and offsets live in SGPRs
+      auto uni64 = [](unsigned long long x) -> unsigned long long {
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)x);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(x >> 32));
+        return ((unsigned long long)hi << 32) | lo;
+      };
+      const unsigned long long a = uni64(tmask[2 * t]), m2 = uni64(tmask[2 * t + 1]);
+      const int s1 = __builtin_amdgcn_readfirstlane(tstart[2 * t]);
+      const int s2 = __builtin_amdgcn_readfirstlane(tstart[2 * t + 1]);
+      if ((a >> lane) & 1ull)
+        eij = s1 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(a >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((unsigned)a, 0u));
+      if ((m2 >> lane) & 1ull)
+        eji = s2 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m2 >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((unsigned)m2, 0u));
       return;
     }
     eij = edge_idx(i, j);
@@ -654,6 +761,73 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
   }
   __syncthreads();
   gain_epilogue(P, b, n, q, uo, tid);
+}
+
+// acl_tile_gains: one workgroup per formation copies every 40-byte record
+// from its row-major position to its tile position (formation setup).
+__global__ void __launch_bounds__(kCtlBlock) tile_gains_kernel(int n, const uint64_t* adj,
+                                                               const double* gains,
+                                                               const int64_t* gain_off,
+                                                               double* out) {
+  constexpr int kNW = (kMaxN + 63) / 64;
+  constexpr int kNT = (kMaxN / 8) * (kMaxN / 8 + 1) / 2;
+  __shared__ unsigned long long adjF[kMaxN * kNW];
+  __shared__ int rowpre[kMaxN * kNW + 1];
+  __shared__ unsigned long long tm[2 * kNT];
+  __shared__ int ts[2 * kNT];
+  const int NW = (n + 63) >> 6, nb = (n + 7) >> 3;
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+  for (int k = tid; k < n * NW; k += kCtlBlock) {
+    unsigned long long x = adj[(size_t)f * n * NW + k];
+    if (k % NW == NW - 1) x &= lastmask;
+    adjF[k] = x;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    int base = 0;
+    for (int w = 0; w < NW * n; w += 64) {
+      const int k = w + lane;
+      const int cnt = (k < n * NW) ? __popcll(adjF[k]) : 0;
+      int x = cnt;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (k < n * NW) rowpre[k] = base + x - cnt;
+      base += __shfl(x, 63, 64);
+    }
+  } else if (wave == 1) {
+    build_tiles(adjF, NW, n, lane, tm, ts);
+  }
+  __syncthreads();
+  const double* src = gains + 5 * gain_off[f];
+  double* dst = out + 5 * gain_off[f];
+  for (int k = tid; k < n * n; k += kCtlBlock) {
+    const int i = k / n, j = k - i * n;
+    const int jw = j >> 6, jb = j & 63;
+    const unsigned long long word = adjF[i * NW + jw];
+    if (!((word >> jb) & 1ull)) continue;
+    const int e = rowpre[i * NW + jw] + __popcll(word & ((1ull << jb) - 1ull));
+    // run 1 of tile (I, J) at lane 8r + c, or run 2 of tile (J, I) at the
+    // lane 8c + r whose pair this edge reverses
+    const int I = i >> 3, J = j >> 3, r = i & 7, c = j & 7;
+    const bool run1 = I < J || (I == J && r <= c);
+    const int lo = I <= J ? I : J, hi = I <= J ? J : I;
+    const int t = lo * nb - lo * (lo - 1) / 2 + (hi - lo);
+    const int s = run1 ? 2 * t : 2 * t + 1;
+    const int bit = run1 ? 8 * r + c : 8 * c + r;
+    const int pos = ts[s] + __popcll(tm[s] & ((1ull << bit) - 1ull));
+#pragma unroll
+    for (int c = 0; c < 5; ++c) dst[5 * (size_t)pos + c] = src[5 * (size_t)e + c];
+  }
+}
+
+hipError_t launch_tile_gains(int n, int F, const uint64_t* adj, const double* gains,
+                             const int64_t* gain_off, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(tile_gains_kernel, dim3(F), dim3(kCtlBlock), 0, stream, n, adj, gains,
+                     gain_off, out);
+  return hipGetLastError();
 }
 
 // collisionAvoidance (safety.cpp:412-541) for the vehicles gain_kernel
@@ -883,10 +1057,15 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
       // uniform swarms: one evaluation per undirected edge; then gain_kernel
       // for the swarms whose vehicles hold different assignments
       const PairLayout PL = make_pair_layout(P.n);
+      const bool tiled = P.gains_tiled != nullptr && P.n <= kMaxN;
+      const void* kp = tiled ? (const void*)gain_pair_kernel<true>
+                             : (const void*)gain_pair_kernel<false>;
       if (PL.total > 64 * 1024)
-        (void)hipFuncSetAttribute((const void*)gain_pair_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, PL.total);
-      hipLaunchKernelGGL(gain_pair_kernel, dim3(nb), dim3(kCtlBlock), PL.total, stream, Q);
+        (void)hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, PL.total);
+      if (tiled)
+        hipLaunchKernelGGL(gain_pair_kernel<true>, dim3(nb), dim3(kCtlBlock), PL.total, stream, Q);
+      else
+        hipLaunchKernelGGL(gain_pair_kernel<false>, dim3(nb), dim3(kCtlBlock), PL.total, stream, Q);
       if (P.all_uniform) return hipGetLastError();
       Q.only_nonuniform = 1;
     }

@@ -79,6 +79,7 @@ struct CtlParams {
   const double* gains;
   const int64_t* gain_off;
   int gain_planes;  // 9 or 5 (acl_formations_t::gain_planes)
+  const double* gains_tiled;  // acl_formations_t::gains_tiled (NULL: row-major records)
   const int32_t* fidx;
   const double* q;
   const double* vel;
@@ -105,6 +106,8 @@ enum { M_BAD = 0, M_NONFIN = 1, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 
 // [P.b0, P.b0 + nb) (DistCntrl::compute, saturation, the collision test),
 // 1 the collisionAvoidance kernel over the listed vehicles.
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream);
+hipError_t launch_tile_gains(int n, int F, const uint64_t* adj, const double* gains,
+                             const int64_t* gain_off, double* out, hipStream_t stream);
 
 // Hand-off of given assignments to the control kernels (acl_control_batch):
 // permutation check, inverse assignment, status.

@@ -753,6 +753,7 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   C.n = n; C.B = a->B; C.b0 = 0;
   C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
   C.gain_planes = F->gain_planes == 5 ? 5 : 9;
+  C.gains_tiled = (C.gain_planes == 5 && n <= kMaxN) ? F->gains_tiled : nullptr;
   C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P_out;
   C.status = a->status;
   C.u = a->u ? a->u : reinterpret_cast<double*>(P.ws + P.W.u);
@@ -795,6 +796,7 @@ acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_a
   C.n = n; C.B = a->B; C.b0 = 0;
   C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
   C.gain_planes = F->gain_planes == 5 ? 5 : 9;
+  C.gains_tiled = (C.gain_planes == 5 && n <= kMaxN) ? F->gains_tiled : nullptr;
   C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P;
   C.status = a->status;
   C.u = a->u ? a->u : reinterpret_cast<double*>(ws + W.u);
@@ -824,4 +826,20 @@ acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_a
 extern "C" acl_status_t acl_control_batch(const acl_formations_t* F, const acl_control_args_t* a,
                                           void* stream) {
   return acl_amd::run_control(F, a, (hipStream_t)stream, acl_amd::CTL_PREP | acl_amd::CTL_RESET);
+}
+
+extern "C" acl_status_t acl_tile_gains(const acl_formations_t* F, double* out, void* stream) {
+  using namespace acl_amd;
+  if (!F || !out) return acl__set_error("acl_tile_gains: null argument");
+  if (F->gain_planes != 5) return acl__set_error("acl_tile_gains: gain_planes must be 5");
+  if (F->n < 1 || F->n > kMaxN) return acl__set_error("acl_tile_gains: n out of range [1, 128]");
+  if (F->n_formations < 0) return acl__set_error("acl_tile_gains: n_formations < 0");
+  if (F->n_formations == 0) return ACL_OK;
+  if (!F->adj || !F->gains || !F->gain_off)
+    return acl__set_error("acl_tile_gains: required pointer is NULL");
+  if (out == F->gains) return acl__set_error("acl_tile_gains: out aliases gains");
+  const hipError_t e = launch_tile_gains(F->n, F->n_formations, F->adj, F->gains, F->gain_off,
+                                         out, (hipStream_t)stream);
+  if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+  return ACL_OK;
 }

@@ -64,6 +64,21 @@ class FormationTable:
         self.gain_off = gain_off
         self.gain_planes = int(gain_planes)
         self.F = int(p.shape[0])
+        self.gains_tiled = None
+
+    def tile_gains(self, stream=None):
+        """Formation-setup step: keep a tile-ordered copy of the 5-plane gain
+        records (acl_tile_gains) for the pair kernel's contiguous tile reads."""
+        if self.gain_planes != 5 or self.n > 128:
+            return self
+        out = torch.empty_like(self.gains)
+        f = self.struct()
+        if stream is None:
+            stream = torch.cuda.current_stream(self.gains.device).cuda_stream
+        L.check(L.lib().acl_tile_gains(ct.byref(f), out.data_ptr(), ct.c_void_p(stream)),
+                "acl_tile_gains")
+        self.gains_tiled = out
+        return self
 
     @classmethod
     def from_host(cls, points, adjs, gains=None, device="cuda", planes=None):
@@ -94,7 +109,8 @@ class FormationTable:
 
     def struct(self):
         return L.Formations(self.n, self.F, self.p.data_ptr(), self.adj.data_ptr(),
-                            self.gains.data_ptr(), self.gain_off.data_ptr(), self.gain_planes)
+                            self.gains.data_ptr(), self.gain_off.data_ptr(), self.gain_planes,
+                            self.gains_tiled.data_ptr() if self.gains_tiled is not None else None)
 
 
 _WS = {}

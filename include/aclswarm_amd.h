@@ -139,6 +139,12 @@ typedef struct {
  *            propagation included; the record stream is 40 B per edge
  *            instead of 72. acl_gain_planes tells which layout a GainMat
  *            admits.
+ *   gains_tiled  optional (NULL = unused): the gain_planes == 5 records of
+ *            every formation re-ordered by acl_tile_gains into 8 x 8 edge
+ *            tiles (same per-formation offsets 5*gain_off[f]). The kernel that
+ *            applies each undirected edge once reads it instead of `gains`
+ *            when n <= 128, so that every tile it processes is one contiguous
+ *            run of records. Same values, same commands, bit for bit.
  */
 typedef struct {
   int32_t n;
@@ -148,7 +154,18 @@ typedef struct {
   const double* gains;
   const int64_t* gain_off;
   int32_t gain_planes;
+  const double* gains_tiled;
 } acl_formations_t;
+
+/* Formation-setup step (once per formation table, like acl_pack_gains; not
+ * part of a solve): writes the tiled copy of F->gains (gain_planes must be 5,
+ * n <= 128) to `out` (device, 5 * sum(E_f) doubles, not aliasing F->gains).
+ * Tile order: tiles (I, J) with J >= I, row block by row block; a tile is
+ * the 64 vertex pairs (8I + r, 8J + c), lane = 8r + c (on a diagonal tile
+ * the lanes r <= c). Its records are two runs in lane order: edge (i, j) of
+ * every lane that has one, then edge (j, i) of every lane that has one
+ * (diagonal tile: lanes r < c). Stream-ordered. */
+acl_status_t acl_tile_gains(const acl_formations_t* F, double* out, void* stream);
 
 /* ---- the batched solve --------------------------------------------------
  * One "solve" = for one swarm of n vehicles:

@@ -155,6 +155,7 @@ struct DeviceFormation {
     F.gains = has_gains ? gains.as<const double>() : nullptr;
     F.gain_off = off.as<const int64_t>();
     F.gain_planes = planes;
+    F.gains_tiled = nullptr;
     return F;
   }
 };

@@ -382,3 +382,81 @@ def test_gain_layouts_5_and_9_planes(cuda):
     gpu = _gpu_solve(pts, adjs, general, fidx, q, vel, P_in)
     ref = _oracle(pts, adjs, general, fidx, q, vel, P_in)
     _compare(gpu, ref)
+
+
+def _tile_order(adj):
+    """Row-major edge index of every record in acl_tile_gains order (the
+    layout include/aclswarm_amd.h documents), restated on the host."""
+    n = adj.shape[0]
+    eidx = -np.ones((n, n), np.int64)
+    ii, jj = np.nonzero(adj)
+    eidx[ii, jj] = np.arange(ii.size)
+    nb = (n + 7) // 8
+    order = []
+    for I in range(nb):
+        for J in range(I, nb):
+            for run in (1, 2):  # lane order: edge (i, j), then edge (j, i)
+                for r in range(8):
+                    for c in range(8):
+                        i, j = 8 * I + r, 8 * J + c
+                        if I == J and (r > c or (run == 2 and r == c)):
+                            continue
+                        if run == 2:
+                            i, j = j, i
+                        if i < n and j < n and adj[i, j]:
+                            order.append(eidx[i, j])
+    return np.array(order, np.int64)
+
+
+@pytest.mark.parametrize("n,complete", [(1, True), (7, True), (20, False), (37, False),
+                                        (100, False), (128, False)])
+def test_tiled_gain_records(cuda, n, complete):
+    """acl_tile_gains writes the records in the documented tile order, and the
+    pair kernel reading the tiled copy gives the same commands, bit for bit,
+    as reading the row-major records (same terms, same summation order)."""
+    import torch
+    from aclswarm_amd import engine
+    rng = np.random.RandomState(1000 + n)
+    F, B = 3, 24
+    pts, adjs = [], []
+    for f in range(F):
+        p = np.c_[rng.uniform(-n, n, (n, 2)), rng.uniform(0, 2, n)]
+        a = np.ones((n, n), np.uint8) - np.eye(n, dtype=np.uint8)
+        if not complete:
+            for _ in range(max(1, n // 3)):
+                i, j = rng.randint(0, n, 2)
+                if i != j:
+                    a[i, j] = a[j, i] = 0
+        if f == 1 and n > 1:
+            a[0, 0] = 1  # a diagonal edge is an edge of the control law too
+        pts.append(p)
+        adjs.append(a)
+    gains = [H.synth_gains(rng, a, scale=1.0) for a in adjs]
+    for G in gains:  # the diagonal row sums carry -0.0 at the structural zeros
+        for i in range(n):
+            G[3 * i + np.array([0, 1, 2, 2]), 3 * i + np.array([2, 2, 0, 1])] = 0.0
+    dev = torch.device("cuda:0")
+    T = engine.FormationTable.from_host(pts, adjs, gains, device=dev, planes=5)
+    assert T.gain_planes == 5
+    T.tile_gains()
+    torch.cuda.synchronize()
+    assert T.gains_tiled is not None
+    rows = T.gains.cpu().numpy()
+    tiled = T.gains_tiled.cpu().numpy()
+    off = 0
+    for f in range(F):
+        order = _tile_order(adjs[f])
+        E = order.size
+        want = rows[5 * off:5 * (off + E)].reshape(E, 5)[order]
+        np.testing.assert_array_equal(tiled[5 * off:5 * (off + E)].reshape(E, 5), want)
+        off += E
+    fidx = torch.from_numpy((np.arange(B) % F).astype(np.int32)).to(dev)
+    q = torch.from_numpy(np.stack([H.dense_positions(rng, n, 2.0 * n) for _ in range(B)])).to(dev)
+    vel = torch.from_numpy(rng.normal(0, 0.3, (B, n, 3))).to(dev)
+    P_in = torch.from_numpy(np.stack([H.random_perm(rng, n) for _ in range(B)])
+                            .astype(np.uint16).view(np.int16)).to(dev)
+    r_t = {k: v.cpu().numpy() for k, v in engine.solve(T, fidx, q, vel, P_in).items()}
+    T.gains_tiled = None
+    r_r = {k: v.cpu().numpy() for k, v in engine.solve(T, fidx, q, vel, P_in).items()}
+    for k in ("P_out", "ca_flag", "u", "u_safe"):
+        np.testing.assert_array_equal(r_t[k], r_r[k], err_msg=k)
