@@ -708,12 +708,16 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
       }
     }
     // row sums over c (lanes 8r .. 8r + 7), column sums over r (stride 8)
+    // (DPP for the steps inside a 16-lane row: quad_perm xor 1, xor 2, then
+    // row_half_mirror -- after the quad sums lane 8r + c reads the other
+    // quad's sum -- and row_ror:8 = xor 8; the same additions in the same
+    // order as the xor butterfly)
+    rs0 += dpp_f64_z<0xB1, 0xF>(rs0); rs1 += dpp_f64_z<0xB1, 0xF>(rs1); rs2 += dpp_f64_z<0xB1, 0xF>(rs2);
+    rs0 += dpp_f64_z<0x4E, 0xF>(rs0); rs1 += dpp_f64_z<0x4E, 0xF>(rs1); rs2 += dpp_f64_z<0x4E, 0xF>(rs2);
+    rs0 += dpp_f64_z<0x141, 0xF>(rs0); rs1 += dpp_f64_z<0x141, 0xF>(rs1); rs2 += dpp_f64_z<0x141, 0xF>(rs2);
+    cs0 += dpp_f64_z<0x128, 0xF>(cs0); cs1 += dpp_f64_z<0x128, 0xF>(cs1); cs2 += dpp_f64_z<0x128, 0xF>(cs2);
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) {
-      rs0 += __shfl_xor(rs0, o, 64); rs1 += __shfl_xor(rs1, o, 64); rs2 += __shfl_xor(rs2, o, 64);
-    }
-#pragma unroll
-    for (int o = 8; o < 64; o <<= 1) {
+    for (int o = 16; o < 64; o <<= 1) {
       cs0 += __shfl_xor(cs0, o, 64); cs1 += __shfl_xor(cs1, o, 64); cs2 += __shfl_xor(cs2, o, 64);
     }
     {

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /root/repo
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread -k "tiled or layouts" > gpurun_out/pytest_tiled.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_tiled.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_tiled.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_tiled.log; exit 1; }
 grep -cE "PASSED" gpurun_out/pytest_tiled.log; tail -2 gpurun_out/pytest_tiled.log
 timeout -k 10 300 python bench.py --no-cpu > gpurun_out/bench_tiled.json 2> gpurun_out/bench_tiled.err || { echo "bench failed"; tail -30 gpurun_out/bench_tiled.err; exit 1; }
 timeout -k 10 300 python bench.py --no-cpu --no-tile-gains > gpurun_out/bench_rows.json 2> gpurun_out/bench_rows.err || { echo "bench failed"; tail -30 gpurun_out/bench_rows.err; exit 1; }
