@@ -484,6 +484,29 @@ __device__ void build_tiles(const unsigned long long* adjF, int NW, int n, int l
   }
 }
 
+// x + (x of lane ^ W), W = 16 or 32, with gfx950's v_permlane{16,32}_swap:
+// swapping a copy of x with itself leaves {x[l], x[l ^ W]} in the two
+// registers of lane l; their sum is the xor-butterfly step exactly (IEEE
+// addition commutes).
+template <int W>
+__device__ __forceinline__ double swap_sum(double x) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  unsigned a0, a1, b0, b1;
+  if constexpr (W == 16) {
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a0 = l[0]; b0 = l[1]; a1 = h[0]; b1 = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a0 = l[0]; b0 = l[1]; a1 = h[0]; b1 = h[1];
+  }
+  const double a = __longlong_as_double((long long)(((unsigned long long)a1 << 32) | a0));
+  const double b = __longlong_as_double((long long)(((unsigned long long)b1 << 32) | b0));
+  return a + b;
+}
+
 struct PairLayout {
   int q, qf, p, pn, adjF, rowpre, Pt, acc, out, atab, tmask, tstart, total;
 };
@@ -716,10 +739,8 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
     rs0 += dpp_f64_z<0x4E, 0xF>(rs0); rs1 += dpp_f64_z<0x4E, 0xF>(rs1); rs2 += dpp_f64_z<0x4E, 0xF>(rs2);
     rs0 += dpp_f64_z<0x141, 0xF>(rs0); rs1 += dpp_f64_z<0x141, 0xF>(rs1); rs2 += dpp_f64_z<0x141, 0xF>(rs2);
     cs0 += dpp_f64_z<0x128, 0xF>(cs0); cs1 += dpp_f64_z<0x128, 0xF>(cs1); cs2 += dpp_f64_z<0x128, 0xF>(cs2);
-#pragma unroll
-    for (int o = 16; o < 64; o <<= 1) {
-      cs0 += __shfl_xor(cs0, o, 64); cs1 += __shfl_xor(cs1, o, 64); cs2 += __shfl_xor(cs2, o, 64);
-    }
+    cs0 = swap_sum<16>(cs0); cs1 = swap_sum<16>(cs1); cs2 = swap_sum<16>(cs2);
+    cs0 = swap_sum<32>(cs0); cs1 = swap_sum<32>(cs1); cs2 = swap_sum<32>(cs2);
     {
       int I, J;
       tile_of(t, I, J);
