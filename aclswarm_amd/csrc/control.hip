@@ -484,6 +484,16 @@ __device__ void build_tiles(const unsigned long long* adjF, int NW, int n, int l
   }
 }
 
+// DPP move of a double for patterns whose every lane has a source lane
+// (quad_perm, row_half_mirror, row_ror): no `old` operand to initialise.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64_all(double x) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  const int lo = __builtin_amdgcn_mov_dpp((int)u, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
 // x + (x of lane ^ W), W = 16 or 32, with gfx950's v_permlane{16,32}_swap:
 // swapping a copy of x with itself leaves {x[l], x[l ^ W]} in the two
 // registers of lane l; their sum is the xor-butterfly step exactly (IEEE
@@ -735,10 +745,10 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
     // row_half_mirror -- after the quad sums lane 8r + c reads the other
     // quad's sum -- and row_ror:8 = xor 8; the same additions in the same
     // order as the xor butterfly)
-    rs0 += dpp_f64_z<0xB1, 0xF>(rs0); rs1 += dpp_f64_z<0xB1, 0xF>(rs1); rs2 += dpp_f64_z<0xB1, 0xF>(rs2);
-    rs0 += dpp_f64_z<0x4E, 0xF>(rs0); rs1 += dpp_f64_z<0x4E, 0xF>(rs1); rs2 += dpp_f64_z<0x4E, 0xF>(rs2);
-    rs0 += dpp_f64_z<0x141, 0xF>(rs0); rs1 += dpp_f64_z<0x141, 0xF>(rs1); rs2 += dpp_f64_z<0x141, 0xF>(rs2);
-    cs0 += dpp_f64_z<0x128, 0xF>(cs0); cs1 += dpp_f64_z<0x128, 0xF>(cs1); cs2 += dpp_f64_z<0x128, 0xF>(cs2);
+    rs0 += dpp_f64_all<0xB1>(rs0); rs1 += dpp_f64_all<0xB1>(rs1); rs2 += dpp_f64_all<0xB1>(rs2);
+    rs0 += dpp_f64_all<0x4E>(rs0); rs1 += dpp_f64_all<0x4E>(rs1); rs2 += dpp_f64_all<0x4E>(rs2);
+    rs0 += dpp_f64_all<0x141>(rs0); rs1 += dpp_f64_all<0x141>(rs1); rs2 += dpp_f64_all<0x141>(rs2);
+    cs0 += dpp_f64_all<0x128>(cs0); cs1 += dpp_f64_all<0x128>(cs1); cs2 += dpp_f64_all<0x128>(cs2);
     cs0 = swap_sum<16>(cs0); cs1 = swap_sum<16>(cs1); cs2 = swap_sum<16>(cs2);
     cs0 = swap_sum<32>(cs0); cs1 = swap_sum<32>(cs1); cs2 = swap_sum<32>(cs2);
     {
