@@ -838,23 +838,27 @@ __global__ void __launch_bounds__(kCtlBlock) tile_gains_kernel(int n, const uint
   __syncthreads();
   const double* src = gains + 5 * gain_off[f];
   double* dst = out + 5 * gain_off[f];
-  for (int k = tid; k < n * n; k += kCtlBlock) {
-    const int i = k / n, j = k - i * n;
+  // one wave per run (s = 2t + run), lane = 8r + c: the run's records are
+  // written contiguously, in lane order
+  const int r = lane >> 3, c = lane & 7;
+  for (int s = wave; s < 2 * pair_tiles(n); s += kCtlWaves) {
+    const unsigned long long m = tm[s];
+    if (!((m >> lane) & 1ull)) continue;
+    int I, J;
+    tile_ij(s >> 1, nb, I, J);
+    int i = 8 * I + r, j = 8 * J + c;
+    if (s & 1) {  // run 2: edge (j, i)
+      const int x = i;
+      i = j;
+      j = x;
+    }
     const int jw = j >> 6, jb = j & 63;
     const unsigned long long word = adjF[i * NW + jw];
-    if (!((word >> jb) & 1ull)) continue;
     const int e = rowpre[i * NW + jw] + __popcll(word & ((1ull << jb) - 1ull));
-    // run 1 of tile (I, J) at lane 8r + c, or run 2 of tile (J, I) at the
-    // lane 8c + r whose pair this edge reverses
-    const int I = i >> 3, J = j >> 3, r = i & 7, c = j & 7;
-    const bool run1 = I < J || (I == J && r <= c);
-    const int lo = I <= J ? I : J, hi = I <= J ? J : I;
-    const int t = lo * nb - lo * (lo - 1) / 2 + (hi - lo);
-    const int s = run1 ? 2 * t : 2 * t + 1;
-    const int bit = run1 ? 8 * r + c : 8 * c + r;
-    const int pos = ts[s] + __popcll(tm[s] & ((1ull << bit) - 1ull));
+    const int pos = ts[s] + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 #pragma unroll
-    for (int c = 0; c < 5; ++c) dst[5 * (size_t)pos + c] = src[5 * (size_t)e + c];
+    for (int k = 0; k < 5; ++k) dst[5 * (size_t)pos + k] = src[5 * (size_t)e + k];
   }
 }
 
