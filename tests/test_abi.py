@@ -92,6 +92,27 @@ def test_solve_batch_argument_errors_without_gpu():
     assert lib.acl_solve_batch(None, ct.byref(a), None) == 1
 
 
+def test_tile_gains_argument_errors_without_gpu():
+    from aclswarm_amd import _lib as L
+    lib = L.lib()
+    out = ct.c_void_p(0x1000)  # never dereferenced: every call below fails its checks
+    F = L.Formations(100, 1, None, None, None, None, 9)
+    assert lib.acl_tile_gains(ct.byref(F), out, None) == 1
+    assert b"gain_planes must be 5" in lib.acl_last_error()
+    F.gain_planes = 5
+    F.n = 129
+    assert lib.acl_tile_gains(ct.byref(F), out, None) == 1
+    assert b"n out of range" in lib.acl_last_error()
+    F.n = 100
+    assert lib.acl_tile_gains(ct.byref(F), out, None) == 1
+    assert b"NULL" in lib.acl_last_error()
+    F.n_formations = 0
+    assert lib.acl_tile_gains(ct.byref(F), out, None) == 0  # nothing to do
+    assert lib.acl_tile_gains(None, out, None) == 1
+    assert lib.acl_tile_gains(ct.byref(F), None, None) == 1
+    assert ct.sizeof(L.Formations) == 56  # gains_tiled appended after gain_planes
+
+
 def test_status_record_is_16_bytes():
     from aclswarm_amd import _lib as L
     assert L.STATUS_DTYPE.itemsize == 16
