@@ -33,12 +33,15 @@ def main():
     ap.add_argument("--steps", type=int, default=240)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-tile-gains", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     gen = torch.Generator(device=dev)
     gen.manual_seed(99)
     w = workload.simform_workload(args.B, args.n, gen, dev, F=None, complete=False, planes=5)
     T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"], w["planes"])
+    if not args.no_tile_gains:
+        T.tile_gains()  # formation setup: tile-ordered gain records (acl_tile_gains)
     # warm-up: a short episode (first launches, workspace)
     e0 = engine.Episode(T, w["fidx"], w["q"], w["vel"], w["P_in"])
     e0.run(2)
