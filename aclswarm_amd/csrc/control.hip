@@ -715,7 +715,7 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
       const double e_z = fabs(q2) - dz;
       double Fxy = 0.0, Fz = 0.0;
       const bool gxy = fabs(e_xy) > g.e_xy_thr, gz = fabs(e_z) > g.e_z_thr;
-#pragma unroll 1
+#pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const bool on = kk ? gz : gxy;
         if (on) {
