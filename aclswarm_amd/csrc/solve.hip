@@ -63,7 +63,10 @@ struct Layout {
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
-constexpr int kLevels = 3;  // price levels resolved per dirty column before the exact scan
+#ifndef ACL_CBAA_LEVELS
+#define ACL_CBAA_LEVELS 3
+#endif
+constexpr int kLevels = ACL_CBAA_LEVELS;  // price levels resolved per dirty column before the exact scan
 
 __host__ __device__ inline Layout make_layout(int n) {
   Layout L;
