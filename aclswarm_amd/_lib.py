@@ -22,15 +22,17 @@ FLAG_CHANGED = 0x04
 FLAG_NONFINITE = 0x08
 FLAG_BAD_INPUT = 0x10
 FLAG_CA_ACTIVE = 0x20
+FLAG_FRAGILE = 0x40
+FRAGILE_MARGIN = 1e-6
 
 STATUS_DTYPE = np.dtype([("flags", "<u4"), ("eff_rounds", "<u2"),
                          ("rounds", "<u2"), ("n_invalid", "<u2"),
-                         ("n_ca", "<u2"), ("reserved", "<u4")])
+                         ("n_ca", "<u2"), ("margin", "<f4")])
 
 # every symbol include/aclswarm_amd.h declares
 EXPORTS = (
     "acl_default_cntrl_gains", "acl_default_safety_params", "acl_default_admm_params",
-    "acl_max_vehicles", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
+    "acl_formations_init", "acl_max_vehicles", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
     "acl_pack_gains", "acl_gain_planes", "acl_pack_gains_planes", "acl_tile_gains", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
     "acl_control_batch", "acl_write_assignment_log", "acl_read_assignment_log",
     "acl_hungarian_batch",
@@ -75,7 +77,7 @@ class SolveArgs(ct.Structure):
                 ("ca_flag", ct.c_void_p), ("who", ct.c_void_p), ("workspace", ct.c_void_p),
                 ("cntrl", CntrlGains), ("safety", SafetyParams),
                 ("early_exit", ct.c_int32), ("do_control", ct.c_int32),
-                ("align_Rt", ct.c_void_p)]
+                ("align_Rt", ct.c_void_p), ("gate_margin", ct.c_void_p)]
 
 
 class ControlArgs(ct.Structure):
@@ -83,7 +85,8 @@ class ControlArgs(ct.Structure):
     _fields_ = [("B", ct.c_int32), ("fidx", ct.c_void_p), ("q", ct.c_void_p),
                 ("vel", ct.c_void_p), ("P", ct.c_void_p), ("u", ct.c_void_p),
                 ("u_safe", ct.c_void_p), ("ca_flag", ct.c_void_p), ("status", ct.c_void_p),
-                ("workspace", ct.c_void_p), ("cntrl", CntrlGains), ("safety", SafetyParams)]
+                ("workspace", ct.c_void_p), ("cntrl", CntrlGains), ("safety", SafetyParams),
+                ("gate_margin", ct.c_void_p)]
 
 
 class HungarianArgs(ct.Structure):
@@ -143,6 +146,8 @@ def lib():
     L.acl_default_cntrl_gains.argtypes = [ct.POINTER(CntrlGains)]
     L.acl_default_safety_params.argtypes = [ct.POINTER(SafetyParams)]
     L.acl_default_admm_params.argtypes = [ct.POINTER(AdmmParams)]
+    L.acl_formations_init.argtypes = [ct.POINTER(Formations), I32, I32]
+    L.acl_formations_init.restype = None
     L.acl_max_vehicles.restype = I32
     L.acl_solve_workspace_bytes.argtypes = [I32, I32]
     L.acl_solve_workspace_bytes.restype = ct.c_size_t

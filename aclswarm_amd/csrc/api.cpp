@@ -43,6 +43,14 @@ extern "C" void acl_default_admm_params(acl_admm_params_t* a) {
   a->mu = 1.0; a->thresh = 1e-4; a->threshTr = 0.10; a->maxItr = 10;
 }
 
+extern "C" void acl_formations_init(acl_formations_t* F, int32_t n, int32_t n_formations) {
+  if (!F) return;
+  std::memset(F, 0, sizeof(*F));
+  F->n = n;
+  F->n_formations = n_formations;
+  F->gain_planes = 9;
+}
+
 // ---- packing -------------------------------------------------------------
 
 extern "C" int64_t acl_count_edges(int32_t n, const uint8_t* adj) {

@@ -286,3 +286,64 @@ __device__ __forceinline__ double wrap_to_pi(double a) {  // utils.h:275-280
 }
 
 }  // namespace acl_amd
+
+namespace acl_amd {
+
+// ---- decision margin (include/aclswarm_amd.h, acl_swarm_status_t::margin) --
+// A thread tracks the compared f32 pair (hi, lo), hi >= lo >= 0, with the
+// largest ratio lo / hi: products of two floats are exact in double, so the
+// ranking is exact and order-independent; a tie (lo == hi) is ratio 1. The
+// oracle (oracle/aclswarm_oracle.c, orc_margin_track) is the same function.
+struct MarginPair {
+  float hi, lo;
+};
+
+__device__ __forceinline__ void margin_init(MarginPair& m) {
+  m.hi = 1.0f;
+  m.lo = 0.0f;
+}
+
+__device__ __forceinline__ void margin_track(MarginPair& m, float hi, float lo) {
+  if (!(lo < hi)) {
+    if (lo == hi) {
+      m.hi = 1.0f;
+      m.lo = 1.0f;
+    }
+    return;  // NaN: the swarm is NONFINITE (margin 0)
+  }
+  if ((double)lo * (double)m.hi > (double)m.lo * (double)hi) {
+    m.hi = hi;
+    m.lo = lo;
+  }
+}
+
+// gap of a tracked pair: (hi - lo) / hi in double (hi - lo exact there), 1
+// when lo < 2^-28 hi; monotone in the ratio, so min over gaps = gap of the
+// max-ratio pair
+__device__ __forceinline__ double margin_gap(const MarginPair& m) {
+  const double hi = m.hi, lo = m.lo;
+  if (lo * 268435456.0 < hi) return 1.0;
+  return (hi - lo) / hi;
+}
+
+// Decision gap of the alignment's determinant-sign and rank tests
+// (Eigen::umeyama 3.3.x, auctioneer.cpp:397), as orc_umeyama2_gap.
+__device__ __forceinline__ double align_gap(const double S[4], double det, const double sv[2]) {
+  const double den = fabs(S[0] * S[3]) + fabs(S[2] * S[1]);
+  double g = (den > 0.0) ? fabs(det) / den : 0.0;
+  if (!(g <= 1.0)) g = (g > 1.0) ? 1.0 : 0.0;
+  const double th = fabs(sv[0]) * 1e-12, a = fabs(sv[1]);
+  const double mx = (a > th) ? a : th;
+  const double gr = (mx > 0.0) ? fabs(a - th) / mx : 0.0;
+  return (gr < g) ? gr : g;
+}
+
+// non-negative doubles order like their bit patterns: block minimum through
+// one LDS word (initialised to 1.0)
+__device__ __forceinline__ void block_min_gap(unsigned long long* word, double g) {
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(g);
+  const unsigned long long m = ~wave_max_u64(~bits);  // wave minimum
+  if ((threadIdx.x & 63) == 0) atomicMin(word, m);
+}
+
+}  // namespace acl_amd

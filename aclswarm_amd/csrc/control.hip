@@ -152,6 +152,41 @@ __device__ void gain_epilogue(const CtlParams& P, int b, int n, const double* q,
   }
 }
 
+// The discrete gates |e| > thr of distcntrl.cpp:75,80 decide whether an
+// atan term is added at all, so they are decided on the oracle's arithmetic:
+// the fast e (fused multiply-adds, one-step sqrt; error far below 1e-9 at the
+// configs' distances) is recomputed with correctly rounded square roots and
+// no contraction whenever it lies within 1e-9 of a threshold. Returns the
+// two gate decisions; gm takes the gate margin min(| |e| - thr | / thr).
+#define ACL_GATE_WINDOW 1e-9
+__device__ __forceinline__ void gate_decide(const acl_cntrl_gains_t& g, double e_xy, double e_z,
+                                            double q0, double q1, double q2, double Ni, double Nj,
+                                            double Nzi, double Nzj, double pix, double piy,
+                                            double piz, double pjx, double pjy, double pjz,
+                                            bool& gxy, bool& gz, double& gm) {
+  double axy = fabs(e_xy), az = fabs(e_z);
+  const double dxy = fabs(axy - g.e_xy_thr), dz = fabs(az - g.e_z_thr);
+  if (dxy < ACL_GATE_WINDOW || dz < ACL_GATE_WINDOW) {
+#pragma clang fp contract(off)
+    const double xy = sqrt(q0 * q0 + q1 * q1) - sqrt((Ni + Nj) - 2.0 * (pix * pjx + piy * pjy));
+    const double zz = sqrt(q2 * q2) - sqrt((Nzi + Nzj) - 2.0 * (piz * pjz));
+    axy = fabs(xy);
+    az = fabs(zz);
+  }
+  gxy = axy > g.e_xy_thr;
+  gz = az > g.e_z_thr;
+  const double mxy = fabs(axy - g.e_xy_thr) / g.e_xy_thr, mz = fabs(az - g.e_z_thr) / g.e_z_thr;
+  gm = fmin(gm, fmin(mxy, mz));
+}
+
+// per-swarm gate margin: wave minimum, then the block's minimum through LDS
+// (non-negative doubles order like their bits); all lanes active
+__device__ __forceinline__ void gate_margin_reduce(unsigned long long* word, double gm) {
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(gm);
+  const unsigned long long m = ~wave_max_u64(~bits);
+  if ((threadIdx.x & 63) == 0) atomicMin(word, m);
+}
+
 // NP = 9: general 3x3 gain blocks; NP = 5: the ADMM block structure, the four
 // structural zeros supplied as constants (acl_formations_t::gain_planes)
 template <int NP>
@@ -231,6 +266,9 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
   __syncthreads();
 
   const int E = __builtin_amdgcn_readfirstlane(rowpre[n * NW]);
+  __shared__ unsigned long long gmw;
+  if (tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
+  double gmin = __builtin_inf();
   const double* G = P.gains + NP * P.gain_off[f];
   // the formation's gains through one buffer resource (9 planes: plane k at
   // SGPR offset 8kE, one VGPR offset per lane; 5: one 40-byte record per
@@ -324,7 +362,9 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
         const double e_z = fabs(q2) - dz;  // |q_ij.z| = sqrt(q2^2) (no over/underflow)
         // the two gated atan terms, one after the other (register pressure)
         double Fxy = 0.0, Fz = 0.0;
-        const bool gxy = fabs(e_xy) > g.e_xy_thr, gz = fabs(e_z) > g.e_z_thr;
+        bool gxy, gz;
+        gate_decide(g, e_xy, e_z, q0, q1, q2, Ni, pn[2 * j], Nzi, pn[2 * j + 1], pix, piy, piz,
+                    pjx, pjy, pjz, gxy, gz, gmin);
 #pragma unroll 1
         for (int kk = 0; kk < 2; ++kk) {
           const bool on = kk ? gz : gxy;
@@ -376,7 +416,9 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }
+  if (P.gate_margin) gate_margin_reduce(&gmw, gmin);
   __syncthreads();
+  if (P.gate_margin && tid == 0) P.gate_margin[b] = __longlong_as_double((long long)gmw);
   gain_epilogue(P, b, n, q, uo, tid);
 }
 
@@ -620,6 +662,9 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
   __syncthreads();
 
   const int E = __builtin_amdgcn_readfirstlane(rowpre[n * NW]);
+  __shared__ unsigned long long gmw;
+  if (tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
+  double gmin = __builtin_inf();
   const double* G = (tiled ? P.gains_tiled : P.gains) + 5 * P.gain_off[f];
   const __amdgpu_buffer_rsrc_t grs =
       __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 5 * E * 8, 0x00020000);
@@ -714,7 +759,9 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
       const double e_xy = ACL_GAIN_SQRT(q0 * q0 + q1 * q1) - dxy;
       const double e_z = fabs(q2) - dz;
       double Fxy = 0.0, Fz = 0.0;
-      const bool gxy = fabs(e_xy) > g.e_xy_thr, gz = fabs(e_z) > g.e_z_thr;
+      bool gxy, gz;
+      gate_decide(g, e_xy, e_z, q0, q1, q2, pn[2 * i], pn[2 * j], pn[2 * i + 1], pn[2 * j + 1],
+                  pix, piy, piz, pjx, pjy, pjz, gxy, gz, gmin);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const bool on = kk ? gz : gxy;
@@ -773,7 +820,9 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
       Aji[k] = Bji[k];
     }
   }
+  if (P.gate_margin) gate_margin_reduce(&gmw, gmin);
   __syncthreads();
+  if (P.gate_margin && tid == 0) P.gate_margin[b] = __longlong_as_double((long long)gmw);
   // u of the vehicle at row i: the four waves' sums in wave order, plus
   // kd (-vel) once per edge of row i (distcntrl.cpp:85-95)
   for (int i = tid; i < n; i += kCtlBlock) {
@@ -1044,6 +1093,8 @@ __global__ void __launch_bounds__(256) control_prep_kernel(const CtlParams P,
   if (tid == 0) bad = 0;
   __syncthreads();
   uint16_t* wsPt = const_cast<uint16_t*>(P.wsPt) + (size_t)b * n;
+  const int f = P.fidx[b];
+  if (tid == 0 && (f < 0 || f >= P.F)) bad = 1;  // formation index out of range
   for (int v = tid; v < n; v += 256) {
     const unsigned pv = Pg[(size_t)b * n + v];
     if (pv >= (unsigned)n) {
@@ -1062,6 +1113,7 @@ __global__ void __launch_bounds__(256) control_prep_kernel(const CtlParams P,
     P.status[b] = st;
   }
   if (bad) {
+    if (P.gate_margin && tid == 0) P.gate_margin[b] = __builtin_inf();
     for (int k = tid; k < 3 * n; k += 256) {
       P.u[(size_t)b * n * 3 + k] = 0.0;
       if (P.u_safe) P.u_safe[(size_t)b * n * 3 + k] = 0.0;

@@ -70,6 +70,7 @@ struct SolveParams {
   unsigned char* ws;  // workspace base (WsLayout)
   WsLayout W;
   unsigned long long* stamps;  // diagnostic: [B][16] s_memtime at phase ends (NULL = off)
+  double* gate_margin;         // acl_solve_args_t::gate_margin (+inf for BAD_INPUT swarms)
 };
 
 struct CtlParams {
@@ -97,10 +98,13 @@ struct CtlParams {
   acl_safety_params_t s;
   int only_nonuniform;  // set by launch_control: gain_kernel skips uniform swarms
   int all_uniform;      // every swarm has one assignment (given P): no gain_kernel pass
+  int F;                // formations in the table (fidx range check of the hand-off)
+  double* gate_margin;  // [B] optional: min | |e| - thr | / thr of the swarm's gates
 };
 
 // misc int slots of the auction kernels' LDS
-enum { M_BAD = 0, M_NONFIN = 1, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 8 };
+enum { M_BAD = 0, M_NONFIN = 1, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 8,
+       M_MARG = 10 /* u64: bits of the swarm's minimum decision gap (misc[10..11]) */ };
 
 // Control stage: which = 0 launches the gain kernel for swarms
 // [P.b0, P.b0 + nb) (DistCntrl::compute, saturation, the collision test),

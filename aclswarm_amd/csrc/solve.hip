@@ -110,22 +110,40 @@ __device__ __forceinline__ float entry_price(const float* C, int n, int w, int j
 // C[v][j] > 0 and C[v][j] > price_j (price_j = C[who_j][j]); nw[c] is this
 // lane's entry for task lane+64c. Returns the selected task (wave-uniform) or -1.
 __device__ __forceinline__ int wave_select(int n, int v, int lane, const float* C,
-                                           const int (&nw)[2]) {
+                                           const int (&nw)[2], MarginPair& m) {
   unsigned key[2];
+  float cvs[2], prs[2];
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const int j = lane + 64 * c;
     key[c] = 0u;
+    cvs[c] = prs[c] = 0.0f;
     if (j < n) {
       const float cv = C[v * n + j];
       const float pr = entry_price(C, n, nw[c], j);
       if (cv > 0.0f && cv > pr) key[c] = __float_as_uint(cv);
+      cvs[c] = cv;
+      prs[c] = pr;
     }
   }
   const unsigned M = wave_max_u32(key[0] > key[1] ? key[0] : key[1]);
-  if (M == 0u) return -1;
-  const unsigned long long e0 = __ballot(key[0] == M), e1 = __ballot(key[1] == M);
-  return e0 ? __ffsll((long long)e0) - 1 : 64 + __ffsll((long long)e1) - 1;
+  int js = -1;
+  if (M != 0u) {
+    const unsigned long long e0 = __ballot(key[0] == M), e1 = __ballot(key[1] == M);
+    js = e0 ? __ffsll((long long)e0) - 1 : 64 + __ffsll((long long)e1) - 1;
+  }
+  // margin of the decisive comparisons (include/aclswarm_amd.h)
+  const float cmax = __uint_as_float(M);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int j = lane + 64 * c;
+    if (j >= n || nw[c] == v) continue;
+    if (j == js) margin_track(m, cvs[c], prs[c]);
+    else if (key[c] != 0u) margin_track(m, cmax, cvs[c]);
+    else if (cvs[c] > 0.0f && (js < 0 || cvs[c] > cmax || (cvs[c] == cmax && j < js)))
+      margin_track(m, prs[c], cvs[c]);
+  }
+  return js;
 }
 
 __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const SolveParams P) {
@@ -151,7 +169,13 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
   unsigned char* validv = smem + L.valid;
   int* misc = reinterpret_cast<int*>(smem + L.misc);
 
-  const int f = P.fidx[b];
+  // a formation index out of range is a bad input like a bad P_in
+  const int f_in = P.fidx[b];
+  const bool fbad = f_in < 0 || f_in >= P.F;
+  const int f = fbad ? 0 : f_in;
+  MarginPair mp;
+  margin_init(mp);
+  double galign = 1.0;
   const int gw = (n + 63) >> 6;  // words per row in the global table
   const unsigned long long lastmask =
       (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
@@ -172,8 +196,14 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
       adjF[k] = x;
     }
     if (tid < 16) misc[tid] = 0;
-    if (tid == 0) misc[M_AGREE] = 1;
     if (tid < 2) H[tid] = 0ull;  // "seen" mask for the permutation check
+  }
+  __syncthreads();
+  if (tid == 0) {
+    misc[M_AGREE] = 1;
+    if (fbad) misc[M_BAD] = 1;
+    *reinterpret_cast<unsigned long long*>(misc + M_MARG) =
+        (unsigned long long)__double_as_longlong(1.0);
   }
   __syncthreads();
   for (int v = tid; v < n; v += kBlock) {
@@ -202,10 +232,12 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
     }
     if (P.who)
       for (int k = tid; k < n * n; k += kBlock) P.who[(size_t)b * n * n + k] = 0xFFFF;
+    if (P.gate_margin && tid == 0) P.gate_margin[b] = __builtin_inf();
     if (tid == 0) {
       acl_swarm_status_t st = {};
       st.flags = ACL_SWARM_BAD_INPUT;
       st.rounds = (uint16_t)(2 * n);
+      st.margin = 1.0f;
       P.status[b] = st;
     }
     return;
@@ -327,8 +359,9 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
     const double dm[2] = {sums[8 * v + 2] * oon, sums[8 * v + 3] * oon};
     // column-major sigma: S(di, sj) = a_(di, sj)
     const double S[4] = {sums[8 * v + 4], sums[8 * v + 6], sums[8 * v + 5], sums[8 * v + 7]};
-    double R[4], t[2];
-    umeyama_finish(S, sm, dm, R, t);
+    double R[4], t[2], ga;
+    umeyama_finish(S, sm, dm, R, t, &ga);
+    galign = ga < galign ? ga : galign;
     double* o = out + 6 * v;
     o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
   }
@@ -384,7 +417,7 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
   // every column that received a bid is dirty for round 1
   for (int v = wave; v < n; v += kWaves) {
     int nw[2] = {n, n};
-    const int task = wave_select(n, v, lane, C, nw);
+    const int task = wave_select(n, v, lane, C, nw, mp);
     if (task >= 0 && lane == 0) {
       T[v * n + task] = (unsigned char)v;
       atomicOr(&dmask[2 * 1 + (task >> 6)], 1ull << (task & 63));
@@ -427,38 +460,50 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
         //    closed neighbours holds, unless that level is tied; vehicles
         //    no tracked level decides fall back to the exact ordered scan
         //    (ascending vehid, strict >).
+        // per vehicle: st 0 = undecided, 1 = winner level found (k1), 2 =
+        // done (k2 = the next level its neighbourhood holds, the margin's
+        // runner-up; 0 = none); need = exact ordered scan
         int nw0 = n, nw1 = n;
-        bool dec0 = !ok0, dec1 = !ok1, need0 = false, need1 = false;
+        int st0 = ok0 ? 0 : 2, st1 = ok1 ? 0 : 2;
+        unsigned k10 = 0u, k11 = 0u, k20 = 0u, k21 = 0u;
+        bool need0 = false, need1 = false, exhausted = false;
         unsigned cap = 0xFFFFFFFFu;
 #pragma unroll
-        for (int k = 0; k < kLevels; ++k) {
+        for (int k = 0; k < kLevels + 1; ++k) {
           const unsigned Mk = wave_max_u32(max(key0 < cap ? key0 : 0u, key1 < cap ? key1 : 0u));
-          if (Mk == 0u) break;  // no further level
+          if (Mk == 0u) {  // no further level
+            exhausted = true;
+            break;
+          }
           const bool e0 = key0 == Mk, e1 = key1 == Mk;
           const unsigned long long h0 = __ballot(e0), h1 = __ballot(e1);
           const int wk = h0 ? __builtin_amdgcn_readlane(wu0, __ffsll((long long)h0) - 1)
                             : __builtin_amdgcn_readlane(wu1, __ffsll((long long)h1) - 1);
           const bool tk = nonfinite || __ballot((e0 && wu0 != wk) || (e1 && wu1 != wk)) != 0ull;
-          const bool hit0 = !dec0 && ((h0 & vmy0[0]) | (h1 & vmy1[0])) != 0ull;
-          const bool hit1 = !dec1 && ((h0 & vmy0[1]) | (h1 & vmy1[1])) != 0ull;
-          nw0 = hit0 ? wk : nw0;
-          nw1 = hit1 ? wk : nw1;
-          need0 |= hit0 && tk;
-          need1 |= hit1 && tk;
-          dec0 |= hit0;
-          dec1 |= hit1;
-          if (__ballot(!dec0 || !dec1) == 0ull) break;
+          const bool hit0 = st0 < 2 && !need0 && ((h0 & vmy0[0]) | (h1 & vmy1[0])) != 0ull;
+          const bool hit1 = st1 < 2 && !need1 && ((h0 & vmy0[1]) | (h1 & vmy1[1])) != 0ull;
+          if (hit0) {
+            if (st0 == 0) { nw0 = wk; k10 = Mk; need0 = tk; st0 = 1; }
+            else { k20 = Mk; st0 = 2; }
+          }
+          if (hit1) {
+            if (st1 == 0) { nw1 = wk; k11 = Mk; need1 = tk; st1 = 1; }
+            else { k21 = Mk; st1 = 2; }
+          }
+          if (__ballot((st0 < 2 && !need0) || (st1 < 2 && !need1)) == 0ull) break;
           cap = Mk;
         }
-        need0 |= !dec0;
-        need1 |= !dec1;
+        need0 |= st0 == 0 || (st0 == 1 && !exhausted);
+        need1 |= st1 == 0 || (st1 == 1 && !exhausted);
+        if (!need0 && k20 != 0u) margin_track(mp, __uint_as_float(k10 - 1u), __uint_as_float(k20 - 1u));
+        if (!need1 && k21 != 0u) margin_track(mp, __uint_as_float(k11 - 1u), __uint_as_float(k21 - 1u));
         if (__ballot(need0 || need1) != 0ull) {
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
             if (c ? need1 : need0) {
-              float bp = 0.0f;
+              float bp = 0.0f, p2 = 0.0f;
               int bw = n;
-              bool first = true;
+              bool first = true, have2 = false;
 #pragma unroll
               for (int w2 = 0; w2 < 2; ++w2) {
                 unsigned long long mm = w2 ? vmy1[c] : vmy0[c];
@@ -468,10 +513,12 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
                   const int wx = T[u * n + j];
                   const float px = entry_price(C, n, wx, j);
                   if (first) { bp = px; bw = wx; first = false; }
-                  else if (px > bp) { bp = px; bw = wx; }
+                  else if (px > bp) { p2 = bp; have2 = true; bp = px; bw = wx; }
+                  else if (wx != bw) { if (!have2 || px > p2) p2 = px; have2 = true; }
                 }
               }
               if (c) nw1 = bw; else nw0 = bw;
+              if (have2) margin_track(mp, bp, p2);
             }
           }
         }
@@ -511,7 +558,7 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
           int nw[2];
           nw[0] = ok0 ? T[v * n + lane] : n;
           nw[1] = ok1 ? T[v * n + lane + 64] : n;
-          const int task = wave_select(n, v, lane, C, nw);
+          const int task = wave_select(n, v, lane, C, nw, mp);
           if (task >= 0 && lane == 0) {
             T[v * n + task] = (unsigned char)v;
             atomicOr(&dmask[2 * npar + (task >> 6)], 1ull << (task & 63));
@@ -528,6 +575,11 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
     const bool changed = (dmask[2 * npar] | dmask[2 * npar + 1]) != 0ull;
     if (changed) eff = r;
     else if (P.early_exit) break;  // fixed point
+  }
+  {  // swarm margin: every thread's CBAA pair and alignment gaps
+    const double gc = margin_gap(mp);
+    block_min_gap(reinterpret_cast<unsigned long long*>(misc + M_MARG),
+                  gc < galign ? gc : galign);
   }
   stamp(P, b, tid, 4);
   if (P.stamps && tid == 0) {
@@ -628,6 +680,10 @@ __global__ void __launch_bounds__(kBlock, kMinWavesPerEU) solve_kernel(const Sol
     if (misc[M_CHANGED]) fl |= ACL_SWARM_CHANGED;
     if (nonfinite) fl |= ACL_SWARM_NONFINITE;
     if (misc[M_NCA]) fl |= ACL_SWARM_CA_ACTIVE;
+    const double g = nonfinite ? 0.0
+        : __longlong_as_double((long long)*reinterpret_cast<unsigned long long*>(misc + M_MARG));
+    if (g < ACL_FRAGILE_MARGIN) fl |= ACL_SWARM_FRAGILE;
+    st.margin = (float)g;
     st.flags = fl;
     st.eff_rounds = (uint16_t)eff;
     st.rounds = (uint16_t)(2 * n);
@@ -716,6 +772,7 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   if (a->B == 0) return ACL_OK;
   if (!F->p || !F->adj || !a->fidx || !a->q || !a->P_in || !a->P_out || !a->status)
     return acl__set_error("acl_solve_batch: required pointer is NULL");
+  if (F->n_formations < 1) return acl__set_error("acl_solve_batch: n_formations < 1");
   if (!a->workspace)
     return acl__set_error("acl_solve_batch: workspace is NULL (acl_solve_workspace_bytes)");
   if (a->do_control && (!F->gains || !F->gain_off || !a->vel))
@@ -732,6 +789,7 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   P.ws = (unsigned char*)a->workspace;
   P.W = ws_layout(n, a->B);
   P.stamps = g_stamps;
+  P.gate_margin = a->do_control ? a->gate_margin : nullptr;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   kt_record(0, 0, s);
@@ -769,6 +827,8 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   C.g = a->cntrl; C.s = a->safety;
   C.only_nonuniform = 0;
   C.all_uniform = 0;
+  C.F = F->n_formations;
+  C.gate_margin = a->gate_margin;
   if (hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
     return acl__set_error("hipMemsetAsync failed");
   for (int which = 0; which < 2; ++which) {
@@ -793,6 +853,7 @@ acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_a
     return acl__set_error("acl_control_batch: required pointer is NULL");
   if (F->gain_planes != 0 && F->gain_planes != 9 && F->gain_planes != 5)
     return acl__set_error("acl_control_batch: gain_planes must be 9 (or 0) or 5");
+  if (F->n_formations < 1) return acl__set_error("acl_control_batch: n_formations < 1");
   const WsLayout W = ws_layout(n, a->B);
   unsigned char* ws = (unsigned char*)a->workspace;
   CtlParams C;
@@ -812,6 +873,8 @@ acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_a
   C.g = a->cntrl; C.s = a->safety;
   C.only_nonuniform = 0;
   C.all_uniform = 1;  // the hand-off of a given P is one assignment per swarm
+  C.F = F->n_formations;
+  C.gate_margin = a->gate_margin;
   if ((flags & CTL_RESET) && hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
     return acl__set_error("hipMemsetAsync failed");
   hipError_t e = hipSuccess;

@@ -64,31 +64,52 @@ __host__ __device__ inline WLayout make_wlayout(int n) {
 
 // selectTaskAssignment (auctioneer.cpp:517-542) on vehicle v's row: the
 // first task j maximizing C[v][j] among C[v][j] > 0 and C[v][j] > price_j.
-// `fresh`: the row is all `none` (the START bid).
+// `fresh`: the row is all `none` (the START bid). Tracks the margin of the
+// decisive comparisons (include/aclswarm_amd.h) in m.
 __device__ int wide_select(int n, int NW, int v, int lane, const float* C, const float* CT,
-                           const uint16_t* T, bool fresh) {
+                           const uint16_t* T, bool fresh, MarginPair& m) {
   unsigned key[kWMaxW];
+  float cvs[kWMaxW], prs[kWMaxW];
+  bool other[kWMaxW];
   unsigned lm = 0u;
 #pragma unroll
   for (int c = 0; c < kWMaxW; ++c) {
     key[c] = 0u;
+    cvs[c] = 0.0f;
+    prs[c] = 0.0f;
+    other[c] = false;
     const int j = lane + 64 * c;
     if (c < NW && j < n) {
       const float cv = C[(size_t)v * n + j];
       const int w = fresh ? n : T[(size_t)j * n + v];
       const float pr = w < n ? CT[(size_t)j * n + w] : 0.0f;
       if (cv > 0.0f && cv > pr) key[c] = __float_as_uint(cv);
+      cvs[c] = cv;
+      prs[c] = pr;
+      other[c] = w != v;
     }
     lm = lm > key[c] ? lm : key[c];
   }
   const unsigned M = wave_max_u32(lm);
-  if (M == 0u) return -1;
+  int js = -1;
+  if (M != 0u) {
+#pragma unroll
+    for (int c = 0; c < kWMaxW; ++c) {
+      const unsigned long long e = __ballot(key[c] == M);
+      if (js < 0 && e) js = 64 * c + __ffsll((long long)e) - 1;
+    }
+  }
+  const float cmax = __uint_as_float(M);
 #pragma unroll
   for (int c = 0; c < kWMaxW; ++c) {
-    const unsigned long long e = __ballot(key[c] == M);
-    if (e) return 64 * c + __ffsll((long long)e) - 1;
+    const int j = lane + 64 * c;
+    if (!other[c]) continue;
+    if (j == js) margin_track(m, cvs[c], prs[c]);
+    else if (key[c] != 0u) margin_track(m, cmax, cvs[c]);
+    else if (cvs[c] > 0.0f && (js < 0 || cvs[c] > cmax || (cvs[c] == cmax && j < js)))
+      margin_track(m, prs[c], cvs[c]);
   }
-  return -1;
+  return js;
 }
 
 __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParams P) {
@@ -121,8 +142,15 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   float* CT = C + (size_t)n * n;
   uint16_t* T = reinterpret_cast<uint16_t*>(CT + (size_t)n * n);
 
-  const int f = P.fidx[b];
+  // a formation index out of range is a bad input like a bad P_in (nothing
+  // of the formation table is read for it)
+  const int f_in = P.fidx[b];
+  const bool fbad = f_in < 0 || f_in >= P.F;
+  const int f = fbad ? 0 : f_in;
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+  MarginPair mp;
+  margin_init(mp);
+  double galign = 1.0;
 
   // ---------------- phase 0: load -----------------------------------------
   {
@@ -139,7 +167,12 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     if (tid < 16) misc[tid] = 0;
   }
   __syncthreads();
-  if (tid == 0) misc[M_AGREE] = 1;
+  if (tid == 0) {
+    misc[M_AGREE] = 1;
+    if (fbad) misc[M_BAD] = 1;
+    *reinterpret_cast<unsigned long long*>(misc + M_MARG) =
+        (unsigned long long)__double_as_longlong(1.0);
+  }
   unsigned long long* seenP = seen + kWWaves * NW;
   for (int v = tid; v < n; v += kWBlock) {
     const unsigned pv = P.P_in[(size_t)b * n + v];
@@ -165,10 +198,12 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     }
     if (P.who)
       for (int k = tid; k < n * n; k += kWBlock) P.who[(size_t)b * n * n + k] = 0xFFFF;
+    if (P.gate_margin && tid == 0) P.gate_margin[b] = __builtin_inf();
     if (tid == 0) {
       acl_swarm_status_t st = {};
       st.flags = ACL_SWARM_BAD_INPUT;
       st.rounds = (uint16_t)(2 * n);
+      st.margin = 1.0f;
       P.status[b] = st;
     }
     return;
@@ -282,8 +317,9 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     const double sm[2] = {sums[8 * v] * oon, sums[8 * v + 1] * oon};
     const double dm[2] = {sums[8 * v + 2] * oon, sums[8 * v + 3] * oon};
     const double S[4] = {sums[8 * v + 4], sums[8 * v + 6], sums[8 * v + 5], sums[8 * v + 7]};
-    double R[4], t[2];
-    umeyama_finish(S, sm, dm, R, t);
+    double R[4], t[2], ga;
+    umeyama_finish(S, sm, dm, R, t, &ga);
+    galign = ga < galign ? ga : galign;
     double* o = out + 6 * v;
     o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
   }
@@ -331,7 +367,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
 
   // ---------------- phase 3: CBAA ------------------------------------------
   for (int v = wave; v < n; v += kWWaves) {
-    const int task = wide_select(n, NW, v, lane, C, CT, T, true);
+    const int task = wide_select(n, NW, v, lane, C, CT, T, true, mp);
     if (task >= 0 && lane == 0) {
       T[(size_t)task * n + v] = (uint16_t)v;
       atomicOr(&dmask[NW + (task >> 6)], 1ull << (task & 63));
@@ -351,8 +387,12 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         if ((idx++ % kWWaves) != wave) continue;
         const uint16_t* Tc = T + (size_t)j * n;
         const float* CTc = CT + (size_t)j * n;
-        unsigned wu[kWMaxW], key[kWMaxW], nw[kWMaxW];
-        bool dec[kWMaxW], need[kWMaxW];
+        unsigned wu[kWMaxW], key[kWMaxW], nw[kWMaxW], k1[kWMaxW], k2[kWMaxW];
+        // per vehicle: st 0 = undecided, 1 = winner level found (k1), 2 =
+        // done (k2 = the next level its neighbourhood holds, 0 = none);
+        // need = exact ordered scan (ties, NaN, levels exhausted)
+        int st[kWMaxW];
+        bool need[kWMaxW];
 #pragma unroll
         for (int c = 0; c < kWMaxW; ++c) {
           const int u = lane + 64 * c;
@@ -360,11 +400,13 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           wu[c] = ok ? Tc[u] : (unsigned)n;
           key[c] = ok ? ((wu[c] < (unsigned)n ? __float_as_uint(CTc[wu[c]]) : 0u) + 1u) : 0u;
           nw[c] = (unsigned)n;
-          dec[c] = !ok;
+          k1[c] = k2[c] = 0u;
+          st[c] = ok ? 0 : 2;
           need[c] = false;
         }
         unsigned cap = 0xFFFFFFFFu;
-        for (int k = 0; k < kWLevels; ++k) {
+        bool exhausted = false;
+        for (int k = 0; k < kWLevels + 1; ++k) {
           unsigned lm = 0u;
 #pragma unroll
           for (int c = 0; c < kWMaxW; ++c) {
@@ -372,7 +414,10 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
             lm = lm > x ? lm : x;
           }
           const unsigned Mk = wave_max_u32(lm);
-          if (Mk == 0u) break;
+          if (Mk == 0u) {
+            exhausted = true;
+            break;
+          }
           unsigned long long h[kWMaxW];
           int wk = -1;
 #pragma unroll
@@ -384,42 +429,52 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
 #pragma unroll
           for (int c = 0; c < kWMaxW; ++c) tl |= key[c] == Mk && wu[c] != (unsigned)wk;
           const bool tk = nonfinite || __ballot(tl) != 0ull;
-          bool und = false;
+          bool open = false;
 #pragma unroll
           for (int c = 0; c < kWMaxW; ++c) {
-            if (!dec[c]) {
+            if (st[c] < 2 && !need[c]) {
               const int u = lane + 64 * c;
               bool hit = false;
 #pragma unroll
               for (int w2 = 0; w2 < kWMaxW; ++w2)
                 if (h[w2]) hit |= (vadj[u * NW + w2] & h[w2]) != 0ull;
               if (hit) {
-                nw[c] = (unsigned)wk;
-                dec[c] = true;
-                need[c] = tk;
+                if (st[c] == 0) {
+                  nw[c] = (unsigned)wk;
+                  k1[c] = Mk;
+                  st[c] = 1;
+                  need[c] = tk;
+                } else {
+                  k2[c] = Mk;
+                  st[c] = 2;
+                }
               }
             }
-            und |= !dec[c];
+            open |= st[c] < 2 && !need[c];
           }
-          if (__ballot(und) == 0ull) break;
+          if (__ballot(open) == 0ull) break;
           cap = Mk;
         }
         bool anyneed = false;
 #pragma unroll
         for (int c = 0; c < kWMaxW; ++c) {
-          need[c] |= !dec[c];
+          // undecided, or the runner-up level not found before the level cap
+          need[c] |= st[c] == 0 || (st[c] == 1 && !exhausted);
           anyneed |= need[c];
+          if (!need[c] && st[c] == 2 && k2[c] != 0u)
+            margin_track(mp, __uint_as_float(k1[c] - 1u), __uint_as_float(k2[c] - 1u));
         }
         if (__ballot(anyneed) != 0ull) {
           // exact ordered scan (ascending vehid, strict >): ties, NaN prices,
-          // vehicles no tracked level decides
+          // vehicles no tracked level decides; the runner-up is the best
+          // price of another `who` (entries of one `who` share its price)
 #pragma unroll
           for (int c = 0; c < kWMaxW; ++c) {
             if (need[c]) {
               const int u = lane + 64 * c;
-              float bp = 0.0f;
+              float bp = 0.0f, p2 = 0.0f;
               unsigned bw = (unsigned)n;
-              bool first = true;
+              bool first = true, have2 = false;
               for (int w2 = 0; w2 < NW; ++w2) {
                 unsigned long long mm = vadj[u * NW + w2];
                 while (mm) {
@@ -427,11 +482,19 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
                   mm &= mm - 1;
                   const unsigned wx = Tc[uu];
                   const float px = wx < (unsigned)n ? CTc[wx] : 0.0f;
-                  if (first) { bp = px; bw = wx; first = false; }
-                  else if (px > bp) { bp = px; bw = wx; }
+                  if (first) {
+                    bp = px; bw = wx; first = false;
+                  } else if (px > bp) {
+                    p2 = bp; have2 = true;  // the old winner's `who` differs
+                    bp = px; bw = wx;
+                  } else if (wx != bw) {
+                    if (!have2 || px > p2) p2 = px;
+                    have2 = true;
+                  }
                 }
               }
               nw[c] = bw;
+              if (have2) margin_track(mp, bp, p2);
             }
           }
         }
@@ -464,7 +527,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           const int v = 64 * w + __ffsll((long long)m) - 1;
           m &= m - 1;
           if ((idx2++ % kWWaves) != wave) continue;
-          const int task = wide_select(n, NW, v, lane, C, CT, T, false);
+          const int task = wide_select(n, NW, v, lane, C, CT, T, false, mp);
           if (task >= 0 && lane == 0) {
             T[(size_t)task * n + v] = (uint16_t)v;
             atomicOr(&dmask[npar * NW + (task >> 6)], 1ull << (task & 63));
@@ -477,6 +540,13 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     for (int w = 0; w < NW; ++w) changed |= dmask[npar * NW + w] != 0ull;
     if (changed) eff = r;
     else if (P.early_exit) break;
+  }
+
+  // swarm margin: min over every thread's CBAA pair and alignment gaps
+  {
+    const double gc = margin_gap(mp);
+    block_min_gap(reinterpret_cast<unsigned long long*>(misc + M_MARG),
+                  gc < galign ? gc : galign);
   }
 
   // ---------------- phase 4: adoption --------------------------------------
@@ -547,10 +617,14 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     if (misc[M_AGREE]) fl |= ACL_SWARM_AGREE;
     if (misc[M_CHANGED]) fl |= ACL_SWARM_CHANGED;
     if (nonfinite) fl |= ACL_SWARM_NONFINITE;
+    const double g = nonfinite ? 0.0
+        : __longlong_as_double((long long)*reinterpret_cast<unsigned long long*>(misc + M_MARG));
+    if (g < ACL_FRAGILE_MARGIN) fl |= ACL_SWARM_FRAGILE;
     st.flags = fl;
     st.eff_rounds = (uint16_t)eff;
     st.rounds = (uint16_t)(2 * n);
     st.n_invalid = (uint16_t)misc[M_NINV];
+    st.margin = (float)g;
     P.status[b] = st;
   }
 }

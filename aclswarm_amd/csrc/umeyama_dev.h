@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 
+#include "common.h"
+
 namespace acl_amd {
 
 // apply_rotation_in_the_plane(row p, row q, (c,s)) on a column-major 2x2
@@ -156,17 +158,22 @@ __device__ inline bool jacobi_svd2(const double* A, double* U, double* sv, doubl
 }
 
 // Finishes Eigen::umeyama (3.3.x rank rule) from the means and the
-// accumulated cross-covariance. R row-major 2x2, t[2].
+// accumulated cross-covariance. R row-major 2x2, t[2]; *gap the decision gap
+// of the determinant-sign and rank tests (common.h align_gap; 0 when the
+// input is not finite).
 __device__ inline bool umeyama_finish(const double* S, const double* sm, const double* dm,
-                                      double* R, double* t) {
+                                      double* R, double* t, double* gap) {
   double U[4], V[4], sv[2];
   if (!jacobi_svd2(S, U, sv, V)) {
     const double nan = __builtin_nan("");
     R[0] = R[1] = R[2] = R[3] = nan;
     t[0] = t[1] = nan;
+    *gap = 0.0;
     return false;
   }
-  double s1 = (det2_lu(S) < 0.0) ? -1.0 : 1.0;
+  const double det = det2_lu(S);
+  *gap = align_gap(S, det, sv);
+  double s1 = (det < 0.0) ? -1.0 : 1.0;
   int rank = 0;
 #pragma unroll
   for (int i = 0; i < 2; ++i)

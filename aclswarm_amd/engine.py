@@ -128,12 +128,14 @@ def workspace(n, B, device):
 
 
 def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
-          do_control=True, want_who=False, want_align=False, out=None, stream=None):
+          do_control=True, want_who=False, want_align=False, want_gate_margin=False, out=None,
+          stream=None):
     """Run acl_solve_batch for B = q.shape[0] swarms. All tensors on device.
 
     fidx [B] int32, q/vel [B][n][3] f64, P_in [B][n] int16 (uint16 bits).
     Returns a dict of device tensors: P_out, status (raw 16-byte records as
-    uint8 [B][16]), u, u_safe, ca_flag, who (if requested).
+    uint8 [B][16]), u, u_safe, ca_flag, and if requested who, align_Rt,
+    gate_margin [B] f64.
     """
     lib = L.lib()
     B, n = int(q.shape[0]), table.n
@@ -150,6 +152,8 @@ def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
             out["who"] = torch.empty((B, n, n), dtype=torch.int16, device=dev)
         if want_align:
             out["align_Rt"] = torch.empty((B, n, 6), dtype=torch.float64, device=dev)
+        if want_gate_margin:
+            out["gate_margin"] = torch.empty(B, dtype=torch.float64, device=dev)
     a = L.SolveArgs()
     a.B = B
     a.fidx = fidx.data_ptr(); a.q = q.data_ptr(); a.vel = vel.data_ptr()
@@ -160,6 +164,8 @@ def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
     a.ca_flag = out["ca_flag"].data_ptr() if out.get("ca_flag") is not None else None
     a.who = out["who"].data_ptr() if out.get("who") is not None else None
     a.align_Rt = out["align_Rt"].data_ptr() if out.get("align_Rt") is not None else None
+    a.gate_margin = (out["gate_margin"].data_ptr() if out.get("gate_margin") is not None
+                     else None)
     a.workspace = workspace(n, B, dev).data_ptr()
     a.cntrl = cntrl or L.default_gains()
     a.safety = safety or L.default_safety()
@@ -216,12 +222,14 @@ def control(table, fidx, q, vel, P, cntrl=None, safety=None, stream=None):
         "u_safe": torch.empty((B, n, 3), dtype=torch.float64, device=dev),
         "ca_flag": torch.empty((B, n), dtype=torch.uint8, device=dev),
         "status": torch.empty((B, 16), dtype=torch.uint8, device=dev),
+        "gate_margin": torch.empty(B, dtype=torch.float64, device=dev),
     }
     a = L.ControlArgs()
     a.B = B
     a.fidx = fidx.data_ptr(); a.q = q.data_ptr(); a.vel = vel.data_ptr(); a.P = P.data_ptr()
     a.u = out["u"].data_ptr(); a.u_safe = out["u_safe"].data_ptr()
     a.ca_flag = out["ca_flag"].data_ptr(); a.status = out["status"].data_ptr()
+    a.gate_margin = out["gate_margin"].data_ptr()
     a.workspace = workspace(n, B, dev).data_ptr()
     a.cntrl = cntrl or L.default_gains()
     a.safety = safety or L.default_safety()

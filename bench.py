@@ -1,16 +1,24 @@
 #!/usr/bin/env python3
 """Headline benchmark: swarm assignment+control solves/sec (N=100 vehicles).
 
-One step = one acl_solve_batch over B swarms (config C3: simform100
-noncomplete graphs, every swarm with its own formation -- points, graph and
-3x3 gain blocks with the structure admm::Solver::solve gives them, streamed
-as 40-byte records per edge -- so the per-swarm gain stream dominates the bytes), i.e.
-for every swarm: all vehicles' 2-D Umeyama alignment, CBAA to consensus
-(bit-exact, exact fixed-point exit), adoption, one DistCntrl step,
-saturation and collision avoidance. Inputs are resident in HBM before the
-timed region. With --gpus N (torchrun), every rank solves its own B swarms
-(weak scaling, no exchange during the solve) and the step ends with the
-RCCL gather of assignments + statistics to rank 0.
+One step = one acl_solve_batch over B swarms per GPU (config C3 by default:
+simform100 noncomplete graphs, every swarm with its own formation -- points,
+graph and 3x3 gain blocks with the structure admm::Solver::solve gives them,
+streamed as 40-byte records per edge -- so the per-swarm gain stream
+dominates the bytes), i.e. for every swarm: all vehicles' 2-D Umeyama
+alignment, CBAA to consensus (bit-exact, exact fixed-point exit), adoption,
+one DistCntrl step, saturation and collision avoidance, then the gather of
+every rank's assignments + status records to rank 0 (dist.gather_results).
+Inputs are resident in HBM before the timed region.
+
+--gpus N: one process per GPU. Launched by torchrun (WORLD_SIZE set) each
+rank solves its own B swarms (weak scaling, no exchange during the solve);
+launched directly with N > 1, this script starts the N ranks itself (child
+processes, before anything touches a GPU) and exits with rank 0's status.
+--config c2 / c4 run the other single-GPU shards (simform20 complete,
+B=4096; simform500, B=2048 per GPU = C4's 16384 over 8 GPUs).
+--dry-run exercises the launch + gather path on the CPU (gloo, synthetic
+outputs, no solve) for the multi-process tests.
 
 Prints ONE JSON line on rank 0 (the driver's contract).
 """
@@ -18,22 +26,51 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from aclswarm_amd import _lib as L  # noqa: E402
-from aclswarm_amd import dist as D  # noqa: E402
-from aclswarm_amd import engine, workload  # noqa: E402
-
 METRIC = "swarm assignment+control solves/sec (N=100) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+# per-GPU shards of the BASELINE.json configs
+CONFIGS = {
+    "c2": dict(n=20, B=4096, L=15.0, complete=True,
+               name="simform20_fc (config C2): complete formation graphs"),
+    "c3": dict(n=100, B=65536, L=40.0, complete=False,
+               name="simform100_nc (config C3): noncomplete random formation graphs"),
+    "c4": dict(n=500, B=2048, L=90.0, complete=False,
+               name="simform500_nc (config C4 shard: 2048 of 16384 swarms per GPU): "
+                    "noncomplete random formation graphs, u16 vehicle indices"),
+}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """One child process per rank (nothing here has touched a GPU), the
+    torchrun environment contract; returns rank 0's exit status (or the first
+    failure)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
 
 
 def algorithmic_bytes(w, lo, hi):
@@ -48,6 +85,7 @@ def algorithmic_bytes(w, lo, hi):
     listed (none in this workload): 0. Re-reads (the later kernels' q, p,
     adjacency, P_out, the workspace hand-off) are implementation traffic,
     not counted."""
+    import torch
     n = w["n"]
     W = (n + 63) // 64
     Bc = hi - lo
@@ -58,30 +96,29 @@ def algorithmic_bytes(w, lo, hi):
     return auction, gain, 0, E / used.numel()
 
 
-def pmc_traffic(n, B, kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/r*_pmc_traffic.json, scripts/gpu_pmc.sh + pmc_summary.py) when
-    it was measured on this same configuration; else None."""
+def committed_profile(prefix, n, B, kernel):
+    """The newest committed PMC summary profiles/r*_{prefix}.json measured on
+    this same configuration that has `kernel`; (entry, path) or (None, None)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{prefix}.json")))
     for f in reversed(files):
         d = json.load(open(f))
-        if d["config"]["n"] == n and d["config"]["B_per_gpu"] == B and kernel in d["kernels"]:
-            return d["kernels"][kernel]["hbm_bytes"], os.path.relpath(f, ROOT)
+        c = d.get("config", {})
+        if c.get("n") == n and c.get("B_per_gpu") == B and kernel in d.get("kernels", {}):
+            return d["kernels"][kernel], os.path.relpath(f, ROOT)
     return None, None
 
 
-def chunk_size(B):
-    """acl_solve_batch launches each kernel once over all B swarms."""
-    return B
-
-
 def cpu_baseline(w, out, budget_s, nthreads):
-    """Time the CPU restatement (oracle/, the reference's literal 2N-round
-    schedule) on a bounded sample of the same swarms; also check parity of
-    that sample against the GPU outputs."""
+    """Time the CPU restatement (oracle/, -O3 -ffp-contract=off, the
+    reference's literal 2N-round schedule) on bounded samples of the same
+    swarms, on all `nthreads` host threads and on one; also check the
+    sample's parity against the GPU outputs."""
+    import numpy as np
+    import torch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
+    from aclswarm_amd import engine, workload
     n = w["n"]
 
     def gather(idx):
@@ -95,34 +132,90 @@ def cpu_baseline(w, out, budget_s, nthreads):
         Pin = w["P_in"][idx].cpu().numpy().view(np.uint16)
         return inv.astype(np.int32), q, vel, pts, adj, G, Pin
 
-    # calibrate on a few swarms, then size the sample to the time budget
-    cal = torch.arange(min(2 * nthreads, w["q"].shape[0]))
+    Btot = w["q"].shape[0]
+    # calibrate on a few swarms, then size the samples to the time budget
+    cal = torch.arange(min(2 * nthreads, Btot))
     args = gather(cal)
-    _, t = O.solve_batch(*args, nthreads=nthreads, early_exit=False)
+    _, t = O.solve_batch(*args, nthreads=nthreads, early_exit=False, margin=False)
     per = t / len(cal)
-    S = int(max(len(cal), min(4096, budget_s / max(per, 1e-6))))
-    S = min(S, w["q"].shape[0])
+    S = int(max(len(cal), min(4096, 0.6 * budget_s / max(per, 1e-6))))
+    S = min(S, Btot)
     idx = torch.arange(S)
     args = gather(idx)
-    res, t_lit = O.solve_batch(*args, nthreads=nthreads, early_exit=False)
+    # timed: the reference's work (literal 2N rounds, no margin bookkeeping);
+    # the fixed-point-exit run carries the margin for the parity check
+    res, t_lit = O.solve_batch(*args, nthreads=nthreads, early_exit=False, margin=False)
     res_ee, t_ee = O.solve_batch(*args, nthreads=nthreads, early_exit=True)
+    # one core: a smaller sample of the same swarms
+    S1 = int(max(1, min(S, 0.25 * budget_s / max(per * nthreads, 1e-6))))
+    a1 = gather(torch.arange(S1))
+    _, t1 = O.solve_batch(*a1, nthreads=1, early_exit=False, margin=False)
     # parity of the sample (GPU ran with the exact fixed-point exit)
     gP = out["P_out"][idx].cpu().numpy().view(np.uint16)
     gst = engine.status_to_numpy(out["status"][idx])
     gus = out["u_safe"][idx].cpu().numpy()
     assign_ok = bool((gP == res["P_out"]).all() and (gP == res_ee["P_out"]).all())
-    status_ok = bool((gst["flags"] == res["status"]["flags"]).all()
-                     and (gst["eff_rounds"] == res["status"]["eff_rounds"]).all())
+    status_ok = bool((gst["flags"] == res_ee["status"]["flags"]).all()
+                     and (gst["eff_rounds"] == res["status"]["eff_rounds"]).all()
+                     and (gst["eff_rounds"] == res_ee["status"]["eff_rounds"]).all()
+                     and (gst["margin"] == res_ee["status"]["margin"]).all())
     rel = np.abs(gus - res["u_safe"]) / np.maximum(np.abs(res["u_safe"]), 1.0)
     return {
         "value": S / t_lit, "unit": "solves/s", "cores": nthreads, "kind": "port",
-        "sample": f"{S} of the benchmark's swarms (n={n}), CPU restatement oracle/ at -O2 "
-                  f"-ffp-contract=off, reference schedule of 2N={2 * n} CBAA rounds, "
-                  f"{nthreads} threads",
-        "value_fixed_point_exit": S / t_ee,
+        "sample": f"{S} of the benchmark's swarms (n={n}) on {nthreads} threads and the "
+                  f"first {S1} on 1 thread; CPU restatement oracle/ at -O3 "
+                  f"-ffp-contract=off, reference schedule of 2N={2 * n} CBAA rounds",
+        "value_1core": S1 / t1,
+        "value_fixed_point_exit_with_margin": S / t_ee,
         "parity_sample": {"swarms": S, "assignments_bit_exact": assign_ok,
-                          "status_exact": status_ok, "u_safe_max_rel_err": float(rel.max())},
+                          "status_and_margin_exact": status_ok,
+                          "u_safe_max_rel_err": float(rel.max())},
     }
+
+
+def dry_run(args, world, rank):
+    """CPU/gloo rehearsal of the multi-rank path: synthetic outputs of the
+    configured shard size, the same gather and max-over-ranks timing; no
+    solve, so `value` measures the plumbing only (dry_run: true)."""
+    import torch
+    import torch.distributed as dist
+    from aclswarm_amd import dist as D
+    cfg = CONFIGS[args.config]
+    B = args.B or cfg["B"]
+    n = cfg["n"]
+    if world > 1:
+        dist.init_process_group("gloo")
+    P = torch.arange(n, dtype=torch.int16).expand(B, n).contiguous()
+    st = torch.zeros((B, 16), dtype=torch.uint8)
+    st[:, 0] = 0x07
+    st[:, 4] = 3 + rank
+    st[:, 12:16] = torch.tensor([0.5], dtype=torch.float32).view(torch.uint8)
+    for _ in range(args.warmup):
+        D.gather_results(P, st)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = D.gather_results(P, st)
+    if world > 1:
+        dist.barrier()
+    dt = torch.tensor([(time.perf_counter() - t0) / args.steps], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": world * B / float(dt.item()), "unit": "solves/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": float(dt.item()) * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic", "dry_run": True,
+            "config": {"workload": cfg["name"], "n": n, "B_per_gpu": B, "B_total": world * B,
+                       "parallelism": f"swarm-sharded x{world}"},
+            "gathered": {"swarms": int(res[0].shape[0]), "status_records": int(res[1].shape[0])},
+            "stats": D.stats_dict(res[2], res[3])}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
 
 
 def main():
@@ -130,14 +223,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--B", type=int, default=65536, help="swarms per GPU")
-    ap.add_argument("--n", type=int, default=100, help="vehicles per swarm")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c3")
+    ap.add_argument("--B", type=int, default=0, help="swarms per GPU (default: the config's)")
     ap.add_argument("--formations", type=int, default=0,
                     help="0: every swarm has its own formation; F>0: F shared formations")
     ap.add_argument("--full-rounds", action="store_true",
                     help="run all 2N CBAA rounds instead of stopping at the fixed point")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=16.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-setup-ab", action="store_true",
+                    help="skip the row-major-records (no acl_tile_gains) comparison steps")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--gain-planes", type=int, default=5, choices=(5, 9),
                     help="5: ADMM-structured gain blocks (the reference's gains); "
@@ -145,11 +240,31 @@ def main():
     ap.add_argument("--no-tile-gains", action="store_true",
                     help="pair kernel reads the row-major records instead of the "
                          "tile-ordered copy made at formation setup (acl_tile_gains)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo rehearsal of the launch + gather path (no GPU, no solve)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return spawn_ranks(args.gpus)  # before any GPU call in this process
+    world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if args.dry_run:
+        return dry_run(args, world, rank)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from aclswarm_amd import _lib as L
+    from aclswarm_amd import dist as D
+    from aclswarm_amd import engine, workload
+
+    cfg = CONFIGS[args.config]
+    n, B = cfg["n"], (args.B or cfg["B"])
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -159,21 +274,24 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + 7919 * rank)
     t0 = time.time()
-    w = workload.simform_workload(args.B, args.n, gen, dev,
-                                  F=(args.formations or None), complete=False,
-                                  planes=args.gain_planes, seed0=rank * args.B)
+    w = workload.simform_workload(B, n, gen, dev, F=(args.formations or None), L=cfg["L"],
+                                  complete=cfg["complete"], planes=args.gain_planes,
+                                  seed0=rank * B)
     torch.cuda.synchronize()
     t_gen = time.time() - t0
     T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"],
                               w["planes"])
+    stream = torch.cuda.current_stream(dev)
     t_tile = None
-    if not args.no_tile_gains and w["planes"] == 5 and args.n <= 128:
+    if not args.no_tile_gains and w["planes"] == 5 and n <= 128:
         # formation setup (once per formation table, outside the timed solves)
-        t0 = time.time()
+        T.tile_gains()  # first call: code-object load; time the second
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
         T.tile_gains()
+        e1.record(stream)
         torch.cuda.synchronize()
-        t_tile = time.time() - t0
-    B, n = args.B, args.n
+        t_tile = e0.elapsed_time(e1) * 1e-3
     out = {
         "P_out": torch.empty((B, n), dtype=torch.int16, device=dev),
         "status": torch.empty((B, 16), dtype=torch.uint8, device=dev),
@@ -181,15 +299,14 @@ def main():
         "u_safe": torch.empty((B, n, 3), dtype=torch.float64, device=dev),
         "ca_flag": torch.empty((B, n), dtype=torch.uint8, device=dev),
     }
-    stream = torch.cuda.current_stream(dev)
 
-    def step():
+    def solve():
         engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], early_exit=not args.full_rounds,
                      out=out, stream=stream.cuda_stream)
-        return D.gather_results(out["P_out"], out["status"])
 
     for _ in range(args.warmup):
-        step()
+        solve()
+        D.gather_results(out["P_out"], out["status"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -202,8 +319,7 @@ def main():
     res = None
     for k in range(args.steps):
         evs[k][0].record(stream)
-        engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], early_exit=not args.full_rounds,
-                     out=out, stream=stream.cuda_stream)
+        solve()
         evs[k][1].record(stream)
         res = D.gather_results(out["P_out"], out["status"])
     torch.cuda.synchronize()
@@ -221,32 +337,60 @@ def main():
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt_max = float(dt_t.item())
-    stats = D.stats_dict(res[1], res[2])
+    stats = D.stats_dict(res[2], res[3])
 
-    # algorithmic bytes per launch (the chunk every launch but the last covers)
-    ch = chunk_size(B)
-    nlaunch = (B + ch - 1) // ch
+    # setup accounting: the same solve on the row-major records (no
+    # acl_tile_gains), untimed for the headline
+    setup = None
+    if t_tile is not None:
+        setup = {"tile_gains_ms": t_tile * 1e3, "tile_gains_us_per_formation": t_tile * 1e6 / w["F"],
+                 "value_if_tiled_every_step": world * B / (dt_max + t_tile),
+                 "break_even_solves_per_formation": None}
+        if not args.no_setup_ab:
+            tiled = T.gains_tiled
+            T.gains_tiled = None
+            for _ in range(2):
+                solve()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(3):
+                solve()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            T.gains_tiled = tiled
+            ms_rm = e0.elapsed_time(e1) / 3
+            setup["row_major_records"] = {"call_ms": ms_rm, "value_1gpu": B / (ms_rm * 1e-3)}
+            gain_s = ms_rm * 1e-3 - call_ms * 1e-3
+            setup["break_even_solves_per_formation"] = (
+                (t_tile / w["F"]) / (gain_s / B) if gain_s > 0 else None)
+
+    # algorithmic bytes per launch (every kernel is one launch over all B)
     a_all, g_all, s_all, e_avg = algorithmic_bytes(w, 0, B)
-    c_all = g_all + s_all
-    per_launch = {"auction": a_all / nlaunch, "gain": g_all / nlaunch, "ca": s_all / nlaunch}
+    per_launch = {"auction": a_all, "gain": g_all, "ca": s_all}
+    gain_sym = ("acl_amd::gain_pair_kernel<%s>" % ("true" if t_tile is not None else "false")
+                if w["planes"] == 5 and os.environ.get("ACLSWARM_AMD_GAIN_PAIR", "1") != "0"
+                else f"acl_amd::gain_kernel<{w['planes']}>")
+    auction_sym = "acl_amd::solve_kernel" if n <= 128 else "acl_amd::solve_wide_kernel"
     kern = {}
-    for k, (name, sym) in enumerate((("auction", "acl_amd::solve_kernel"),
-                                     ("gain", "acl_amd::gain_pair_kernel<%s>" % ("true" if t_tile is not None else "false")
-                                      if w["planes"] == 5
-                                      and os.environ.get("ACLSWARM_AMD_GAIN_PAIR", "1") != "0"
-                                      else f"acl_amd::gain_kernel<{w['planes']}>"),
+    for k, (name, sym) in enumerate((("auction", auction_sym), ("gain", gain_sym),
                                      ("ca", "acl_amd::ca_kernel"))):
         avg = kms[k] / max(kcnt[k], 1)
         ach = per_launch[name] / (avg * 1e-3) / 1e9
-        traffic, tsrc = pmc_traffic(n, B, sym) if args.formations == 0 else (None, None)
-        kern[name] = {"kernel": sym, "launches_per_step": nlaunch, "avg_launch_ms": avg,
+        pm, src = (committed_profile("pmc_traffic", n, B, sym) if args.formations == 0
+                   else (None, None))
+        kern[name] = {"kernel": sym, "launches_per_step": 1, "avg_launch_ms": avg,
                       "bytes_per_launch": per_launch[name], "achieved_GBs": ach,
-                      "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc}
-    # the roofline is an HBM roofline: its kernel is the one that carries the
-    # path's HBM stream (the gain kernel, ~98% of the algorithmic bytes); the
-    # auction kernel's own line in `kernels` shows it is not HBM-bound
-    dom = max(kern, key=lambda k: kern[k]["bytes_per_launch"])
-    pipe_ach = (a_all + c_all) / (call_ms * 1e-3) / 1e9
+                      "frac": ach / HBM_PEAK_GBS,
+                      "traffic": pm["hbm_bytes"] if pm else None, "traffic_source": src}
+    # the auction kernel is LDS/VALU/SALU-issue bound: its issue rates from the
+    # committed SQ counters of the same configuration (scripts/gpu_pmc_auction.sh)
+    iss, isrc = committed_profile("pmc_auction", n, B, auction_sym)
+    if iss:
+        kern["auction"]["issue"] = dict(iss, source=isrc)
+    pipe_bytes = a_all + g_all + s_all
+    pipe_ach = pipe_bytes / (call_ms * 1e-3) / 1e9
+    gk = kern["gain"]
     line = {
         "metric": METRIC,
         "value": world * B / dt_max,
@@ -261,13 +405,13 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": "simform100_nc (config C3): noncomplete random formation graphs, "
-                        + ("a unique formation (points, graph, gain blocks) per swarm"
-                           if not args.formations else f"{args.formations} shared formations"),
+            "workload": cfg["name"] + (", a unique formation (points, graph, gain blocks) per swarm"
+                                       if not args.formations else
+                                       f", {args.formations} shared formations"),
             "formations": "the reference generator (generate_random_formation.py:59-80, "
-                          "L=40, h=2, min_dist=2) after np.random.seed(s), "
-                          f"s = {rank * args.B}..{rank * args.B + (args.formations or args.B) - 1}, "
-                          "reproduced bit-exact on the device",
+                          f"L={cfg['L']:g}, h=2, min_dist=2, fc={cfg['complete']}) after "
+                          f"np.random.seed(s), s = {rank * B}..{rank * B + (args.formations or B) - 1}"
+                          " per rank, reproduced bit-exact on the device",
             "n": n, "B_per_gpu": B, "B_total": world * B,
             "edges_per_formation_avg": e_avg,
             "cbaa": "all 2N rounds" if args.full_rounds else "exact fixed-point exit",
@@ -275,23 +419,25 @@ def main():
             "gains": ("synthetic ADMM-structured blocks [a b 0; c d 0; 0 0 e] "
                       "(solver.cpp:49-77), 5-entry records = 40 B/edge" if w["planes"] == 5 else
                       "synthetic random 3x3 blocks, 9 planes = 72 B/edge"),
-            "gain_layout": ("tile-ordered copy (acl_tile_gains, formation setup: %.3f s, "
-                            "not timed)" % t_tile) if t_tile is not None else "row-major records",
+            "gain_layout": ("tile-ordered copy (acl_tile_gains at formation setup, see `setup`)"
+                            if t_tile is not None else "row-major records"),
         },
         "roofline": {
-            "bound": "hbm", "achieved": kern[dom]["achieved_GBs"], "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": kern[dom]["frac"], "traffic": kern[dom]["traffic"],
-            "traffic_source": kern[dom]["traffic_source"],
-            "kernel": kern[dom]["kernel"], "avg_launch_ms": kern[dom]["avg_launch_ms"],
-            "bytes_per_launch": kern[dom]["bytes_per_launch"],
-            "note": "kernel carrying the HBM stream (most algorithmic bytes); the auction "
-                    "kernel (LDS-resident CBAA) is VALU/LDS-issue bound, HBM frac in "
-                    "`kernels.auction`; whole call in `pipeline`; see DESIGN.md",
-            "kernels": kern,
-            "pipeline": {"what": "whole acl_solve_batch call (auction, gain, ca kernels)",
-                         "call_ms": call_ms, "bytes": a_all + c_all,
+            "bound": "hbm", "scope": "kernel", "kernel": gk["kernel"],
+            "achieved": gk["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gk["frac"], "traffic": gk["traffic"], "traffic_source": gk["traffic_source"],
+            "avg_launch_ms": gk["avg_launch_ms"], "bytes_per_launch": gk["bytes_per_launch"],
+            "pipeline": {"what": "whole acl_solve_batch call (auction, gain, ca kernels): "
+                                 "algorithmic bytes / call time",
+                         "call_ms": call_ms, "bytes": pipe_bytes,
                          "achieved_GBs": pipe_ach, "frac": pipe_ach / HBM_PEAK_GBS},
+            "note": "scope=kernel: the kernel that carries the HBM stream (the gain "
+                    "stream, nearly all algorithmic bytes); the auction kernel is "
+                    "LDS/VALU/SALU-issue bound (kernels.auction.issue); the whole "
+                    "call's HBM fraction is `pipeline.frac`",
+            "kernels": kern,
         },
+        "setup": setup,
         "stats": stats,
         "gen_s": t_gen,
     }
@@ -304,7 +450,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

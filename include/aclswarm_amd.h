@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define ACL_ABI_VERSION 2
+#define ACL_ABI_VERSION 3
 
 typedef enum {
   ACL_OK = 0,
@@ -101,6 +101,32 @@ void acl_default_admm_params(acl_admm_params_t* a);
 #define ACL_SWARM_NONFINITE 0x08u /* a bid price was NaN: exact ordered-scan path */
 #define ACL_SWARM_BAD_INPUT 0x10u /* P_in not a permutation: swarm skipped */
 #define ACL_SWARM_CA_ACTIVE 0x20u /* collision avoidance modified >= 1 command */
+#define ACL_SWARM_FRAGILE   0x40u /* margin < ACL_FRAGILE_MARGIN: a last-ulp change
+                                     of a compared value could change the outcome */
+#define ACL_FRAGILE_MARGIN 1e-6
+
+/* Decision margin (SURVEY §7 "Umeyama fidelity", §8b): the smallest relative
+ * gap of the float comparisons that decided the swarm's outcome, over
+ *   - every updateTaskAssignment evaluation (auctioneer.cpp:480-509) of
+ *     vehicle v, task j: p1 = the winning price, p2 = the highest price in
+ *     v's closed neighbourhood whose `who` differs from the winner's (a tie
+ *     gives p2 = p1); gap (p1 - p2) / p1;
+ *   - every selectTaskAssignment (auctioneer.cpp:521-541) of vehicle v,
+ *     c_k = getPrice of task k, (price_k, who_k) its table entry, j* the
+ *     selected task (if any), tasks with who_k == v skipped (a value compared
+ *     with itself): j*: (c_j* - price_j*) / c_j*; another eligible task k:
+ *     (c_j* - c_k) / c_j*; an ineligible task k with c_k > 0 that would be
+ *     selected if it became eligible (no j*, c_k > c_j*, or c_k == c_j* and
+ *     k < j*): (price_k - c_k) / price_k;
+ *   - every alignment (Eigen::umeyama, auctioneer.cpp:397): the determinant
+ *     sign test |det S| / (|S00 S11| + |S01 S10|) and the rank test
+ *     |s1 - 1e-12 s0| / max(s1, 1e-12 s0) (0 when both are 0).
+ * The f32 pairs are ranked exactly by their ratio p2/p1 (products of two
+ * floats are exact in f64); the gap of the extreme pair is then computed in
+ * f64 as (p1 - p2) / p1, or 1 when p2 < 2^-28 p1, and the swarm's margin is
+ * the f64 minimum over all of it, rounded to f32 (1 when nothing was
+ * compared, BAD_INPUT swarms included; 0 for NONFINITE swarms). Equal prices held by different vehicles
+ * give margin 0. */
 
 typedef struct {
   uint32_t flags;
@@ -110,7 +136,7 @@ typedef struct {
                           (auctioneer.cpp:50-51, 441-444) */
   uint16_t n_invalid;  /* vehicles whose final table is not a permutation */
   uint16_t n_ca;       /* vehicles whose command collision avoidance modified */
-  uint32_t reserved;
+  float margin;        /* decision margin (above); in [0, 1] */
 } acl_swarm_status_t; /* 16 bytes */
 
 /* ---- formation table (device memory) ------------------------------------
@@ -157,6 +183,11 @@ typedef struct {
   const double* gains_tiled;
 } acl_formations_t;
 
+/* Zero-initialises *F (every optional pointer NULL, gain_planes 9) and sets
+ * n and n_formations. ABI 3 added gains_tiled: a caller that fills the struct
+ * field by field must start from this (or from a zeroed struct). */
+void acl_formations_init(acl_formations_t* F, int32_t n, int32_t n_formations);
+
 /* Formation-setup step (once per formation table, like acl_pack_gains; not
  * part of a solve): writes the tiled copy of F->gains (gain_planes must be 5,
  * n <= 128) to `out` (device, 5 * sum(E_f) doubles, not aliasing F->gains).
@@ -180,7 +211,8 @@ acl_status_t acl_tile_gains(const acl_formations_t* F, double* out, void* stream
  *   (5) Safety::cmdinCb saturation and Safety::collisionAvoidance
  *       (safety.cpp:172-197, 412-541).
  * All pointers are device pointers.
- *   fidx    [B]        formation of swarm b (0 <= fidx < F)
+ *   fidx    [B]        formation of swarm b (0 <= fidx < F; a swarm with
+ *                      fidx out of range gets BAD_INPUT like a bad P_in)
  *   q       [B][n][3]  vehicle positions, vehicle space (PtsMat q, one row
  *                      per vehicle)
  *   vel     [B][n][3]  vehicle velocities (the controller's damping input)
@@ -226,6 +258,12 @@ typedef struct {
                          R row-major 2x2 then t (Auctioneer::alignFormation,
                          auctioneer.cpp:347-415); the `aligned` points of
                          logAssignment are R p + t (z unchanged) */
+  double* gate_margin; /* [B] optional (NULL ok): the control law's gate
+                          margin, min over the swarm's evaluated edges of
+                          | |e| - thr | / thr for the gates |e_xy| > e_xy_thr
+                          and |e_z| > e_z_thr (distcntrl.cpp:75,80); +inf
+                          without edges. The gates themselves are decided on
+                          correctly rounded e (the oracle's arithmetic) */
 } acl_solve_args_t;
 
 /* Largest n acl_solve_batch accepts (512). */
@@ -262,8 +300,8 @@ acl_status_t acl_pack_gains_planes(int32_t n, const uint8_t* adj_colmajor,
  * DistCntrl::setAssignment + compute (distcntrl.cpp:38-102) and
  * Safety::cmdinCb/collisionAvoidance for B swarms whose assignment P is
  * already known (e.g. between auto-auctions, coordination_ros.cpp:370-378).
- * P [B][n] vehicle -> formation point; a P that is not a permutation gives
- * status BAD_INPUT and zero commands. status [B] gets flags (BAD_INPUT,
+ * P [B][n] vehicle -> formation point; a P that is not a permutation (or a
+ * fidx out of range) gives status BAD_INPUT and zero commands. status [B] gets flags (BAD_INPUT,
  * CA_ACTIVE) and n_ca; the other fields are zero. Device pointers; workspace
  * of acl_solve_workspace_bytes(n, B). Stream-ordered. */
 typedef struct {
@@ -279,6 +317,7 @@ typedef struct {
   void* workspace;
   acl_cntrl_gains_t cntrl;
   acl_safety_params_t safety;
+  double* gate_margin; /* [B] optional, as in acl_solve_args_t */
 } acl_control_args_t;
 
 acl_status_t acl_control_batch(const acl_formations_t* formations,

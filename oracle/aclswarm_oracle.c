@@ -182,8 +182,26 @@ int orc_jacobi_svd2(const double A[4], double U[4], double sv[2],
   return 0;
 }
 
+/* Decision gaps of the alignment's two sign/rank tests (the margin of
+ * include/aclswarm_amd.h): |det S| / (|S00 S11| + |S01 S10|) for the
+ * determinant sign, |s1 - 1e-12 s0| / max(s1, 1e-12 s0) for the rank. */
+static double align_gap(const double S[4], double det, const double sv[2]) {
+  const double den = fabs(S[0] * S[3]) + fabs(S[2] * S[1]);
+  double g = (den > 0.0) ? fabs(det) / den : 0.0;
+  if (!(g <= 1.0)) g = (g > 1.0) ? 1.0 : 0.0;
+  const double th = fabs(sv[0]) * 1e-12, a = fabs(sv[1]);
+  const double mx = (a > th) ? a : th;
+  const double gr = (mx > 0.0) ? fabs(a - th) / mx : 0.0;
+  return (gr < g) ? gr : g;
+}
+
 int orc_umeyama2(int k, const double* src, const double* dst, double R[4],
                  double t[2], int variant) {
+  return orc_umeyama2_gap(k, src, dst, R, t, variant, NULL);
+}
+
+int orc_umeyama2_gap(int k, const double* src, const double* dst, double R[4],
+                     double t[2], int variant, double* gap) {
   /* Eigen::umeyama(src, dst, false), Eigen/src/Geometry/Umeyama.h (3.3.4),
    * Dimension = Dynamic since pp.topRows(d) has a runtime row count. */
   const double one_over_n = 1.0 / (double)k;
@@ -222,6 +240,7 @@ int orc_umeyama2(int k, const double* src, const double* dst, double R[4],
     }
   }
   double U[4], V[4], sv[2];
+  if (gap) *gap = 0.0;
   if (orc_jacobi_svd2(S, U, sv, V) != 0) {
     R[0] = R[1] = R[2] = R[3] = NAN;
     t[0] = t[1] = NAN;
@@ -233,7 +252,9 @@ int orc_umeyama2(int k, const double* src, const double* dst, double R[4],
     if (det2_lu(U) * det2_lu(V) < 0.0) s1 = -1.0;
   } else {
     /* Eigen 3.3.x: S from det(sigma); rank-deficient branch */
-    if (det2_lu(S) < 0.0) s1 = -1.0;
+    const double det = det2_lu(S);
+    if (gap) *gap = align_gap(S, det, sv);
+    if (det < 0.0) s1 = -1.0;
     int rank = 0;
     for (int i = 0; i < 2; ++i)
       if (!(fabs(sv[i]) <= fabs(sv[0]) * 1e-12)) ++rank;
@@ -275,6 +296,12 @@ static int is_perm(int n, const uint16_t* P) {
 void orc_align(int n, int v, const double* q, const double* p,
                const uint8_t* adj, const uint16_t* P, double R[4],
                double t[2]) {
+  orc_align_gap(n, v, q, p, adj, P, R, t, NULL);
+}
+
+void orc_align_gap(int n, int v, const double* q, const double* p,
+                   const uint8_t* adj, const uint16_t* P, double R[4],
+                   double t[2], double* gap) {
   /* auctioneer.cpp:347-415. Formation space: i = P[v]; neighbourhood
    * {j : adj(i,j) || i == j} ascending; p rows j, q rows Pt[j]. */
   uint16_t* Pt = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)n);
@@ -292,7 +319,7 @@ void orc_align(int n, int v, const double* q, const double* p,
       ++k;
     }
   }
-  orc_umeyama2(k, src, dst, R, t, 0);
+  orc_umeyama2_gap(k, src, dst, R, t, 0, gap);
   free(src);
   free(dst);
   free(Pt);
@@ -300,9 +327,16 @@ void orc_align(int n, int v, const double* q, const double* p,
 
 void orc_prices(int n, const double* q, const double* p, const uint8_t* adj,
                 const uint16_t* P, float* C, double* Rt) {
+  orc_prices_gap(n, q, p, adj, P, C, Rt, NULL);
+}
+
+void orc_prices_gap(int n, const double* q, const double* p, const uint8_t* adj,
+                    const uint16_t* P, float* C, double* Rt, double* gap_min) {
+  if (gap_min) *gap_min = 1.0;
   for (int v = 0; v < n; ++v) {
-    double R[4], t[2];
-    orc_align(n, v, q, p, adj, P, R, t);
+    double R[4], t[2], g = 1.0;
+    orc_align_gap(n, v, q, p, adj, P, R, t, &g);
+    if (gap_min && g < *gap_min) *gap_min = g;
     if (Rt) {
       Rt[6 * v + 0] = R[0]; Rt[6 * v + 1] = R[1];
       Rt[6 * v + 2] = R[2]; Rt[6 * v + 3] = R[3];
@@ -323,9 +357,33 @@ void orc_prices(int n, const double* q, const double* p, const uint8_t* adj,
   }
 }
 
-/* selectTaskAssignment (auctioneer.cpp:517-542) */
+/* Decision-margin tracker (include/aclswarm_amd.h): the compared pair
+ * (hi, lo), hi >= lo >= 0, with the largest ratio lo / hi, ranked exactly
+ * (products of two floats are exact in double). A tie (lo == hi) is the
+ * largest ratio, 1. */
+void orc_margin_track(float* m, float hi, float lo) {
+  if (!(lo < hi)) {
+    if (lo == hi) { m[0] = 1.0f; m[1] = 1.0f; }
+    return; /* NaN: the swarm is NONFINITE, margin 0 */
+  }
+  if ((double)lo * (double)m[0] > (double)m[1] * (double)hi) {
+    m[0] = hi;
+    m[1] = lo;
+  }
+}
+
+/* Gap of the tracked pair: (hi - lo) / hi in double, 1 when lo < 2^-28 hi
+ * (where hi - lo is exact in double the gap is monotone in the ratio). */
+double orc_margin_gap(const float* m) {
+  const double hi = m[0], lo = m[1];
+  if (lo * 268435456.0 < hi) return 1.0;
+  return (hi - lo) / hi;
+}
+
+/* selectTaskAssignment (auctioneer.cpp:517-542), plus the margin of its
+ * decisive comparisons (include/aclswarm_amd.h) when m != NULL */
 static void cbaa_select(int n, int v, const float* C, int32_t* who,
-                        float* price) {
+                        float* price, float* m) {
   float max = 0.0f;
   int task = 0, assigned = 0;
   for (int j = 0; j < n; ++j) {
@@ -336,6 +394,20 @@ static void cbaa_select(int n, int v, const float* C, int32_t* who,
       assigned = 1;
     }
   }
+  if (m) {
+    const int js = assigned ? task : -1;
+    for (int k = 0; k < n; ++k) {
+      if (who[k] == v) continue; /* compared with itself */
+      const float c = C[(size_t)v * n + k];
+      if (k == js) {
+        orc_margin_track(m, c, price[k]);
+      } else if (c > price[k] && c > 0.0f) {
+        orc_margin_track(m, max, c); /* an eligible task that lost */
+      } else if (c > 0.0f && (js < 0 || c > max || (c == max && k < js))) {
+        orc_margin_track(m, price[k], c); /* would win if it became eligible */
+      }
+    }
+  }
   if (assigned) {
     price[task] = max;
     who[task] = v;
@@ -344,6 +416,11 @@ static void cbaa_select(int n, int v, const float* C, int32_t* who,
 
 int orc_cbaa(int n, const float* C, const uint8_t* adj, const uint16_t* P,
              int early_exit, int32_t* who_out, float* price_out) {
+  return orc_cbaa_m(n, C, adj, P, early_exit, who_out, price_out, NULL);
+}
+
+int orc_cbaa_m(int n, const float* C, const uint8_t* adj, const uint16_t* P,
+               int early_exit, int32_t* who_out, float* price_out, float* m) {
   const size_t nn = (size_t)n * n;
   int32_t* who = (int32_t*)malloc(sizeof(int32_t) * nn);
   int32_t* who2 = (int32_t*)malloc(sizeof(int32_t) * nn);
@@ -351,6 +428,7 @@ int orc_cbaa(int n, const float* C, const uint8_t* adj, const uint16_t* P,
   float* pr2 = (float*)malloc(sizeof(float) * nn);
   int* nb = (int*)malloc(sizeof(int) * nn);
   int* deg = (int*)malloc(sizeof(int) * (size_t)n);
+  if (m) { m[0] = 1.0f; m[1] = 0.0f; }
   /* Closed neighbourhood in vehicle space, ascending vehid = std::map order
    * of bids_curr_ (auctioneer.cpp:419-437, 480): u is a neighbour of v iff
    * adj(P[v], P[u]) (u = Pt[j] <=> j = P[u]), plus v itself. */
@@ -366,7 +444,7 @@ int orc_cbaa(int n, const float* C, const uint8_t* adj, const uint16_t* P,
     pr[k] = 0.0f;
   }
   for (int v = 0; v < n; ++v)
-    cbaa_select(n, v, C, who + (size_t)v * n, pr + (size_t)v * n);
+    cbaa_select(n, v, C, who + (size_t)v * n, pr + (size_t)v * n, m);
   const int max_iter = n * 2; /* cbaa_max_iter_ = n * diameter (:50-51) */
   int eff = 0;
   for (int r = 1; r <= max_iter; ++r) {
@@ -381,11 +459,26 @@ int orc_cbaa(int n, const float* C, const uint8_t* adj, const uint16_t* P,
           if (pr[(size_t)u * n + j] > pr[(size_t)maxit * n + j]) maxit = u;
         }
         const int32_t wnew = who[(size_t)maxit * n + j];
+        if (m) {
+          /* margin: the winning price vs the best price of another `who` */
+          const float p1 = pr[(size_t)maxit * n + j];
+          int have = 0;
+          float p2 = 0.0f;
+          for (int a = 0; a < deg[v]; ++a) {
+            const int u = nbv[a];
+            if (who[(size_t)u * n + j] == wnew) continue;
+            const float px = pr[(size_t)u * n + j];
+            if (!have || px > p2) p2 = px;
+            have = 1;
+          }
+          if (have) orc_margin_track(m, p1, p2);
+        }
         if (who[(size_t)v * n + j] == v && wnew != v) outbid = 1;
         who2[(size_t)v * n + j] = wnew;
         pr2[(size_t)v * n + j] = pr[(size_t)maxit * n + j];
       }
-      if (outbid) cbaa_select(n, v, C, who2 + (size_t)v * n, pr2 + (size_t)v * n);
+      if (outbid)
+        cbaa_select(n, v, C, who2 + (size_t)v * n, pr2 + (size_t)v * n, m);
     }
     const int changed = memcmp(who, who2, sizeof(int32_t) * nn) != 0 ||
                         memcmp(pr, pr2, sizeof(float) * nn) != 0;
@@ -425,7 +518,15 @@ void orc_control(int n, int v, const double* q, const double* vel_v,
                  const uint16_t* Pt, const uint8_t* adj, const double* gains,
                  const double* dxy, const double* dz,
                  const acl_cntrl_gains_t* g, double u[3]) {
-  /* DistCntrl::compute (distcntrl.cpp:46-102) */
+  orc_control_g(n, v, q, vel_v, Pt, adj, gains, dxy, dz, g, u, NULL);
+}
+
+void orc_control_g(int n, int v, const double* q, const double* vel_v,
+                   const uint16_t* Pt, const uint8_t* adj, const double* gains,
+                   const double* dxy, const double* dz,
+                   const acl_cntrl_gains_t* g, double u[3], double* gate_min) {
+  /* DistCntrl::compute (distcntrl.cpp:46-102); gate_min (optional) takes the
+   * minimum of | |e| - thr | / thr over the two gates of every edge */
   int i = 0;
   while (Pt[i] != v) ++i; /* i = P[v] */
   const size_t ld = (size_t)3 * n;
@@ -439,6 +540,12 @@ void orc_control(int n, int v, const double* q, const double* vel_v,
         sqrt(qij[0] * qij[0] + qij[1] * qij[1]) - dxy[(size_t)i * n + j];
     const double e_z = sqrt(qij[2] * qij[2]) - dz[(size_t)i * n + j];
     double F[3] = {0.0, 0.0, 0.0};
+    if (gate_min) {
+      const double gx = fabs(fabs(e_xy) - g->e_xy_thr) / g->e_xy_thr;
+      const double gz = fabs(fabs(e_z) - g->e_z_thr) / g->e_z_thr;
+      if (gx < *gate_min) *gate_min = gx;
+      if (gz < *gate_min) *gate_min = gz;
+    }
     if (fabs(e_xy) > g->e_xy_thr) F[0] = F[1] = g->K1_xy * atan(g->K2_xy * e_xy);
     if (fabs(e_z) > g->e_z_thr) F[2] = g->K1_z * atan(g->K2_z * e_z);
     for (int r = 0; r < 3; ++r) {
@@ -588,11 +695,27 @@ void orc_solve(int n, const double* q, const double* vel, const double* p,
                const acl_cntrl_gains_t* g, const acl_safety_params_t* s,
                int early_exit, uint16_t* P_out, acl_swarm_status_t* st,
                double* u, double* u_safe, uint8_t* ca, uint16_t* who_out) {
+  orc_solve_g(n, q, vel, p, adj, gains, P_in, g, s, early_exit, P_out, st, u, u_safe, ca,
+              who_out, NULL);
+}
+
+/* 1: orc_solve skips the decision-margin bookkeeping (the CPU baseline
+ * times the reference's work only; the margin is then reported as 1). */
+static __thread int orc_no_margin = 0;
+
+void orc_solve_g(int n, const double* q, const double* vel, const double* p,
+                 const uint8_t* adj, const double* gains, const uint16_t* P_in,
+                 const acl_cntrl_gains_t* g, const acl_safety_params_t* s,
+                 int early_exit, uint16_t* P_out, acl_swarm_status_t* st,
+                 double* u, double* u_safe, uint8_t* ca, uint16_t* who_out,
+                 double* gate_margin) {
   const size_t nn = (size_t)n * n;
+  if (gate_margin) *gate_margin = INFINITY;
   memset(st, 0, sizeof(*st));
   st->rounds = (uint16_t)(2 * n);
   if (!is_perm(n, P_in)) {
     st->flags = ACL_SWARM_BAD_INPUT;
+    st->margin = 1.0f; /* nothing compared */
     for (int v = 0; v < n; ++v) {
       P_out[v] = P_in[v];
       for (int r = 0; r < 3; ++r) {
@@ -612,11 +735,21 @@ void orc_solve(int n, const double* q, const double* vel, const double* p,
   double* dxy = (double*)malloc(sizeof(double) * nn);
   double* dz = (double*)malloc(sizeof(double) * nn);
   invert_perm(n, P_in, Pt_in);
-  orc_prices(n, q, p, adj, P_in, C, NULL);
+  double gmin = 1.0;
+  orc_prices_gap(n, q, p, adj, P_in, C, NULL, &gmin);
   uint32_t flags = 0;
   for (size_t k = 0; k < nn; ++k)
     if (isnan(C[k])) flags |= ACL_SWARM_NONFINITE;
-  st->eff_rounds = (uint16_t)orc_cbaa(n, C, adj, P_in, early_exit, who, NULL);
+  float mpair[2] = {1.0f, 0.0f};
+  st->eff_rounds = (uint16_t)orc_cbaa_m(n, C, adj, P_in, early_exit, who, NULL,
+                                        orc_no_margin ? NULL : mpair);
+  {
+    const double gc = orc_margin_gap(mpair);
+    if (gc < gmin) gmin = gc;
+    if (flags & ACL_SWARM_NONFINITE) gmin = 0.0;
+    st->margin = (float)gmin;
+    if (gmin < ACL_FRAGILE_MARGIN) flags |= ACL_SWARM_FRAGILE;
+  }
   if (who_out)
     for (size_t k = 0; k < nn; ++k) who_out[k] = (uint16_t)who[k];
   int n_invalid = 0, agree = 1, changed = 0, n_ca = 0;
@@ -642,7 +775,7 @@ void orc_solve(int n, const double* q, const double* vel, const double* p,
     P_out[v] = (uint16_t)i;
     if (P_out[v] != P_in[v]) changed = 1;
     double cmd[3];
-    orc_control(n, v, q, vel + 3 * v, Pt_v, adj, gains, dxy, dz, g, cmd);
+    orc_control_g(n, v, q, vel + 3 * v, Pt_v, adj, gains, dxy, dz, g, cmd, gate_margin);
     if (u) {
       u[3 * v] = cmd[0];
       u[3 * v + 1] = cmd[1];
@@ -673,7 +806,7 @@ void orc_solve(int n, const double* q, const double* vel, const double* p,
 /* ------------------------------------------------------------------------ */
 
 typedef struct {
-  int B, n, early_exit;
+  int B, n, early_exit, with_margin;
   const int32_t* fidx;
   const double *q, *vel, *p, *gains;
   const uint8_t* adj;
@@ -691,6 +824,7 @@ typedef struct {
 static void* orc_worker(void* arg) {
   orc_job_t* J = (orc_job_t*)arg;
   const size_t n = (size_t)J->n;
+  orc_no_margin = !J->with_margin;
   for (;;) {
     pthread_mutex_lock(&J->mu);
     const int b = J->next++;
@@ -713,9 +847,9 @@ double orc_solve_batch(int B, int n, int nthreads, const int32_t* fidx,
                        const uint16_t* P_in, const acl_cntrl_gains_t* g,
                        const acl_safety_params_t* s, int early_exit,
                        uint16_t* P_out, acl_swarm_status_t* st, double* u,
-                       double* u_safe, uint8_t* ca) {
+                       double* u_safe, uint8_t* ca, int with_margin) {
   orc_job_t J;
-  J.B = B; J.n = n; J.early_exit = early_exit; J.fidx = fidx;
+  J.B = B; J.n = n; J.early_exit = early_exit; J.with_margin = with_margin; J.fidx = fidx;
   J.q = q; J.vel = vel; J.p = p; J.gains = gains; J.adj = adj; J.P_in = P_in;
   J.g = g; J.s = s; J.P_out = P_out; J.st = st; J.u = u; J.u_safe = u_safe;
   J.ca = ca; J.next = 0;

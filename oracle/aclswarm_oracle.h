@@ -59,10 +59,23 @@ int orc_jacobi_svd2(const double A[4], double U[4], double sv[2], double V[4]);
 int orc_umeyama2(int k, const double* src, const double* dst, double R[4],
                  double t[2], int variant);
 
+/* orc_umeyama2 (variant 0) plus the decision gap of its determinant-sign
+ * and rank tests (the margin of include/aclswarm_amd.h); gap may be NULL. */
+int orc_umeyama2_gap(int k, const double* src, const double* dst, double R[4],
+                     double t[2], int variant, double* gap);
+
 /* Auctioneer::alignFormation for vehicle v: R (row-major 2x2), t (2). */
 void orc_align(int n, int v, const double* q, const double* p,
                const uint8_t* adj, const uint16_t* P, double R[4],
                double t[2]);
+
+void orc_align_gap(int n, int v, const double* q, const double* p,
+                   const uint8_t* adj, const uint16_t* P, double R[4],
+                   double t[2], double* gap);
+
+/* orc_prices plus the smallest alignment decision gap over the vehicles. */
+void orc_prices_gap(int n, const double* q, const double* p, const uint8_t* adj,
+                    const uint16_t* P, float* C, double* Rt, double* gap_min);
 
 /* getPrice for every (vehicle v, task j) with v's own alignment:
  * C[v*n+j] = (float)(1.0 / (||q_v - (R_v p_j + t_v)|| + 1e-8)).
@@ -77,6 +90,13 @@ void orc_prices(int n, const double* q, const double* p, const uint8_t* adj,
 int orc_cbaa(int n, const float* C, const uint8_t* adj, const uint16_t* P,
              int early_exit, int32_t* who_out, float* price_out);
 
+/* orc_cbaa plus the decision-margin tracker m[2] = (hi, lo) of the CBAA
+ * comparisons (include/aclswarm_amd.h); m may be NULL. */
+int orc_cbaa_m(int n, const float* C, const uint8_t* adj, const uint16_t* P,
+               int early_exit, int32_t* who_out, float* price_out, float* m);
+void orc_margin_track(float* m, float hi, float lo);
+double orc_margin_gap(const float* m);
+
 /* utils::pdistmat on the xy columns and on the z column of p. */
 void orc_pdist(int n, const double* p, double* dxy, double* dz);
 
@@ -86,6 +106,13 @@ void orc_control(int n, int v, const double* q, const double* vel_v,
                  const uint16_t* Pt, const uint8_t* adj, const double* gains,
                  const double* dxy, const double* dz,
                  const acl_cntrl_gains_t* g, double u[3]);
+
+/* orc_control plus the gate margin: *gate_min = min(*gate_min, | |e| - thr |
+ * / thr) over both gates of every edge (gate_min may be NULL). */
+void orc_control_g(int n, int v, const double* q, const double* vel_v,
+                   const uint16_t* Pt, const uint8_t* adj, const double* gains,
+                   const double* dxy, const double* dz,
+                   const acl_cntrl_gains_t* g, double u[3], double* gate_min);
 
 /* Safety::cmdinCb saturation, in place on g[3]. */
 void orc_saturate(const acl_safety_params_t* s, double g[3]);
@@ -103,16 +130,26 @@ void orc_solve(int n, const double* q, const double* vel, const double* p,
                int early_exit, uint16_t* P_out, acl_swarm_status_t* st,
                double* u, double* u_safe, uint8_t* ca, uint16_t* who_out);
 
+/* orc_solve plus the swarm's gate margin (acl_solve_args_t::gate_margin;
+ * +inf without edges; may be NULL). */
+void orc_solve_g(int n, const double* q, const double* vel, const double* p,
+                 const uint8_t* adj, const double* gains, const uint16_t* P_in,
+                 const acl_cntrl_gains_t* g, const acl_safety_params_t* s,
+                 int early_exit, uint16_t* P_out, acl_swarm_status_t* st,
+                 double* u, double* u_safe, uint8_t* ca, uint16_t* who_out,
+                 double* gate_margin);
+
 /* Batched solve over a thread pool (the CPU baseline). Swarm b uses
  * formation fidx[b]: p [F][n][3], adj [F][n][n], gains [F][3n][3n].
- * Returns wall seconds. */
+ * with_margin = 0 skips the decision-margin bookkeeping (not part of the
+ * reference's work; status margin reported as 1). Returns wall seconds. */
 double orc_solve_batch(int B, int n, int nthreads, const int32_t* fidx,
                        const double* q, const double* vel, const double* p,
                        const uint8_t* adj, const double* gains,
                        const uint16_t* P_in, const acl_cntrl_gains_t* g,
                        const acl_safety_params_t* s, int early_exit,
                        uint16_t* P_out, acl_swarm_status_t* st, double* u,
-                       double* u_safe, uint8_t* ca);
+                       double* u_safe, uint8_t* ca, int with_margin);
 
 /* ---- centralized comparator (hungarian_oracle.c) -------------------------
  * assignment.py:15-137 restated; see hungarian_oracle.c for the pinning. */

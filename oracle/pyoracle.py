@@ -26,12 +26,12 @@ class SafetyParams(ct.Structure):
 class SwarmStatus(ct.Structure):
     _fields_ = [("flags", ct.c_uint32), ("eff_rounds", ct.c_uint16),
                 ("rounds", ct.c_uint16), ("n_invalid", ct.c_uint16),
-                ("n_ca", ct.c_uint16), ("reserved", ct.c_uint32)]
+                ("n_ca", ct.c_uint16), ("margin", ct.c_float)]
 
 
 STATUS_DTYPE = np.dtype([("flags", "<u4"), ("eff_rounds", "<u2"),
                          ("rounds", "<u2"), ("n_invalid", "<u2"),
-                         ("n_ca", "<u2"), ("reserved", "<u4")])
+                         ("n_ca", "<u2"), ("margin", "<f4")])
 
 
 def default_gains():
@@ -64,6 +64,13 @@ def lib():
         L.orc_umeyama2.restype = ct.c_int
         L.orc_align.argtypes = [ct.c_int, ct.c_int, D, D, U8, U16, D, D]
         L.orc_prices.argtypes = [ct.c_int, D, D, U8, U16, F, D]
+        L.orc_prices_gap.argtypes = [ct.c_int, D, D, U8, U16, F, D, D]
+        L.orc_umeyama2_gap.argtypes = [ct.c_int, D, D, D, D, ct.c_int, D]
+        L.orc_umeyama2_gap.restype = ct.c_int
+        L.orc_cbaa_m.argtypes = [ct.c_int, F, U8, U16, ct.c_int, I32, F, F]
+        L.orc_cbaa_m.restype = ct.c_int
+        L.orc_margin_gap.argtypes = [F]
+        L.orc_margin_gap.restype = ct.c_double
         L.orc_cbaa.argtypes = [ct.c_int, F, U8, U16, ct.c_int, I32, F]
         L.orc_cbaa.restype = ct.c_int
         L.orc_pdist.argtypes = [ct.c_int, D, D, D]
@@ -76,10 +83,11 @@ def lib():
         L.orc_solve.argtypes = [ct.c_int, D, D, D, U8, D, U16,
                                 ct.POINTER(CntrlGains), ct.POINTER(SafetyParams),
                                 ct.c_int, U16, ct.POINTER(SwarmStatus), D, D, U8, U16]
+        L.orc_solve_g.argtypes = L.orc_solve.argtypes + [D]
         L.orc_solve_batch.argtypes = [ct.c_int, ct.c_int, ct.c_int, I32, D, D, D,
                                       U8, D, U16, ct.POINTER(CntrlGains),
                                       ct.POINTER(SafetyParams), ct.c_int, U16,
-                                      ct.c_void_p, D, D, U8]
+                                      ct.c_void_p, D, D, U8, ct.c_int]
         L.orc_solve_batch.restype = ct.c_double
         L.orc_lsap.argtypes = [ct.c_int, D, I32]
         L.orc_lsap.restype = ct.c_int
@@ -119,6 +127,40 @@ def prices(q, p, adj, P):
     lib().orc_prices(n, _p(q, ct.c_double), _p(p, ct.c_double), _p(adj, ct.c_uint8),
                      _p(P, ct.c_uint16), _p(C, ct.c_float), _p(Rt, ct.c_double))
     return C, Rt
+
+
+def prices_gap(q, p, adj, P):
+    """orc_prices plus the smallest alignment decision gap (det sign / rank
+    tests) over the vehicles."""
+    n = q.shape[0]
+    q = _c(q, np.float64); p = _c(p, np.float64); adj = _c(adj, np.uint8)
+    P = _c(P, np.uint16)
+    C = np.zeros((n, n), np.float32); Rt = np.zeros((n, 6)); g = np.zeros(1)
+    lib().orc_prices_gap(n, _p(q, ct.c_double), _p(p, ct.c_double), _p(adj, ct.c_uint8),
+                         _p(P, ct.c_uint16), _p(C, ct.c_float), _p(Rt, ct.c_double),
+                         _p(g, ct.c_double))
+    return C, Rt, float(g[0])
+
+
+def umeyama2_gap(src, dst):
+    src = _c(src, np.float64); dst = _c(dst, np.float64)
+    R = np.zeros(4); t = np.zeros(2); g = np.zeros(1)
+    lib().orc_umeyama2_gap(src.shape[0], _p(src, ct.c_double), _p(dst, ct.c_double),
+                           _p(R, ct.c_double), _p(t, ct.c_double), 0, _p(g, ct.c_double))
+    return R.reshape(2, 2), t, float(g[0])
+
+
+def cbaa_margin(C, adj, P, early_exit=True):
+    """orc_cbaa_m: (who, price, eff, gap) with gap the f64 decision gap of the
+    CBAA comparisons (include/aclswarm_amd.h, margin)."""
+    n = C.shape[0]
+    C = _c(C, np.float32); adj = _c(adj, np.uint8); P = _c(P, np.uint16)
+    who = np.zeros((n, n), np.int32); pr = np.zeros((n, n), np.float32)
+    m = np.zeros(2, np.float32)
+    eff = lib().orc_cbaa_m(n, _p(C, ct.c_float), _p(adj, ct.c_uint8), _p(P, ct.c_uint16),
+                           int(early_exit), _p(who, ct.c_int32), _p(pr, ct.c_float),
+                           _p(m, ct.c_float))
+    return who, pr, eff, float(lib().orc_margin_gap(_p(m, ct.c_float)))
 
 
 def cbaa(C, adj, P, early_exit=True):
@@ -177,19 +219,22 @@ def solve(q, vel, p, adj, gains, P_in, g=None, s=None, early_exit=True):
     P_out = np.zeros(n, np.uint16); st = SwarmStatus()
     u = np.zeros((n, 3)); us = np.zeros((n, 3)); ca = np.zeros(n, np.uint8)
     who = np.zeros((n, n), np.uint16)
-    lib().orc_solve(n, _p(q, ct.c_double), _p(vel, ct.c_double), _p(p, ct.c_double),
-                    _p(adj, ct.c_uint8), _p(gains, ct.c_double), _p(P_in, ct.c_uint16),
-                    ct.byref(g), ct.byref(s), int(early_exit), _p(P_out, ct.c_uint16),
-                    ct.byref(st), _p(u, ct.c_double), _p(us, ct.c_double),
-                    _p(ca, ct.c_uint8), _p(who, ct.c_uint16))
+    gm = np.zeros(1)
+    lib().orc_solve_g(n, _p(q, ct.c_double), _p(vel, ct.c_double), _p(p, ct.c_double),
+                      _p(adj, ct.c_uint8), _p(gains, ct.c_double), _p(P_in, ct.c_uint16),
+                      ct.byref(g), ct.byref(s), int(early_exit), _p(P_out, ct.c_uint16),
+                      ct.byref(st), _p(u, ct.c_double), _p(us, ct.c_double),
+                      _p(ca, ct.c_uint8), _p(who, ct.c_uint16), _p(gm, ct.c_double))
     status = {k: getattr(st, k) for k, _ in SwarmStatus._fields_}
-    return dict(P_out=P_out, status=status, u=u, u_safe=us, ca=ca, who=who)
+    return dict(P_out=P_out, status=status, u=u, u_safe=us, ca=ca, who=who,
+                gate_margin=float(gm[0]))
 
 
 def solve_batch(fidx, q, vel, p, adj, gains, P_in, nthreads=1, g=None, s=None,
-                early_exit=True):
+                early_exit=True, margin=True):
     """B swarms; p [F][n][3], adj [F][n][n], gains [F][3n][3n]. Returns outputs and
-    the wall time (s)."""
+    the wall time (s). margin=False skips the decision-margin bookkeeping
+    (the CPU baseline times the reference's work only)."""
     B, n = q.shape[0], q.shape[1]
     g = g or default_gains(); s = s or default_safety()
     fidx = _c(fidx, np.int32); q = _c(q, np.float64); vel = _c(vel, np.float64)
@@ -202,7 +247,7 @@ def solve_batch(fidx, q, vel, p, adj, gains, P_in, nthreads=1, g=None, s=None,
                               _p(gains, ct.c_double), _p(P_in, ct.c_uint16), ct.byref(g),
                               ct.byref(s), int(early_exit), _p(P_out, ct.c_uint16),
                               st.ctypes.data_as(ct.c_void_p), _p(u, ct.c_double),
-                              _p(us, ct.c_double), _p(ca, ct.c_uint8))
+                              _p(us, ct.c_double), _p(ca, ct.c_uint8), int(bool(margin)))
     return dict(P_out=P_out, status=st, u=u, u_safe=us, ca=ca), t
 
 

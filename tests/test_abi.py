@@ -116,6 +116,29 @@ def test_tile_gains_argument_errors_without_gpu():
 def test_status_record_is_16_bytes():
     from aclswarm_amd import _lib as L
     assert L.STATUS_DTYPE.itemsize == 16
+    assert L.STATUS_DTYPE.fields["margin"][1] == 12  # f32 decision margin at byte 12
+
+
+def test_abi_version_and_formations_init():
+    """ABI 3 (gains_tiled in acl_formations_t, margin in the status, gate
+    margins): acl_formations_init zero-fills the struct so no optional pointer
+    is left as garbage; the solve rejects an empty formation table."""
+    from aclswarm_amd import _lib as L
+    with open(os.path.join(ROOT, "include", "aclswarm_amd.h")) as f:
+        assert "#define ACL_ABI_VERSION 3" in f.read()
+    lib = L.lib()
+    F = L.Formations()
+    ct.memset(ct.byref(F), 0xAB, ct.sizeof(F))
+    lib.acl_formations_init(ct.byref(F), 100, 7)
+    assert (F.n, F.n_formations, F.gain_planes) == (100, 7, 9)
+    assert not F.p and not F.adj and not F.gains and not F.gain_off and not F.gains_tiled
+    a = L.SolveArgs()
+    a.B = 1
+    a.fidx = a.q = a.P_in = a.P_out = a.status = a.workspace = 8  # never dereferenced
+    F.p = F.adj = 8
+    F.n_formations = 0
+    assert lib.acl_solve_batch(ct.byref(F), ct.byref(a), None) == 1
+    assert b"n_formations" in lib.acl_last_error()
 
 
 def test_cpp_facade_compiles_and_exports():

@@ -25,7 +25,8 @@ def _gpu_solve(points, adjs, gains, fidx, q, vel, P_in, early_exit=True, do_cont
         torch.from_numpy(np.ascontiguousarray(q)).to(dev),
         torch.from_numpy(np.ascontiguousarray(vel)).to(dev),
         torch.from_numpy(np.asarray(P_in, np.uint16).view(np.int16)).to(dev),
-        early_exit=early_exit, do_control=do_control, want_who=True)
+        early_exit=early_exit, do_control=do_control, want_who=True,
+        want_gate_margin=do_control)
     torch.cuda.synchronize()
     res = {k: v.cpu().numpy() for k, v in out.items()}
     res["P_out"] = res["P_out"].view(np.uint16)
@@ -53,7 +54,13 @@ def _compare(gpu, ref, check_control=True):
         st = gpu["status"][b]
         for k in ("flags", "eff_rounds", "rounds", "n_invalid"):
             assert int(st[k]) == int(r["status"][k]), (b, k, st, r["status"])
+        # decision margin: an exact function of the compared values (bit-exact)
+        assert np.float32(st["margin"]) == np.float32(r["status"]["margin"]), (
+            b, st["margin"], r["status"]["margin"])
         if check_control:
+            # gate margin from the fast e (tolerance), the gates themselves exact
+            gm, rg = float(gpu["gate_margin"][b]), r["gate_margin"]
+            assert (gm == rg) if not np.isfinite(rg) else abs(gm - rg) <= 1e-10, (b, gm, rg)
             assert int(st["n_ca"]) == int(r["status"]["n_ca"]), (b, st, r["status"])
             np.testing.assert_array_equal(gpu["ca_flag"][b], r["ca"], err_msg=f"ca swarm {b}")
             for key, rk in (("u", "u"), ("u_safe", "u_safe")):

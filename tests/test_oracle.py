@@ -66,11 +66,22 @@ def test_alignment_collinear_is_rotation():
 
 # --------------------------------------------------------------------- CBAA --
 
-def _py_cbaa(C, adj, P, rounds):
+def _gap(hi, lo):
+    """Relative gap of one decisive comparison of f32 values hi >= lo >= 0
+    (include/aclswarm_amd.h): (hi - lo) / hi in double (the numerator is
+    exact there), 1 when lo < 2^-28 hi."""
+    hi, lo = float(hi), float(lo)
+    if lo * 2.0 ** 28 < hi:
+        return 1.0
+    return (hi - lo) / hi
+
+
+def _py_cbaa(C, adj, P, rounds, gaps=None):
     """Second, independent formulation of the lockstep CBAA (App. A) with
-    explicit (price, who) pairs, pure Python, for small n."""
+    explicit (price, who) pairs, pure Python, for small n. With a list
+    `gaps`, appends the gap of every decisive comparison (the literal
+    definition of the decision margin: the minimum over them)."""
     n = C.shape[0]
-    Pt = np.argsort(P)
     nb = [[u for u in range(n) if u == v or adj[P[v], P[u]]] for v in range(n)]
     price = np.zeros((n, n), np.float32)
     who = -np.ones((n, n), np.int64)
@@ -81,6 +92,18 @@ def _py_cbaa(C, adj, P, rounds):
             c = C[v, j]
             if c > best and c > pr[j]:
                 best, task, ok = c, j, True
+        if gaps is not None:
+            js = task if ok else -1
+            for k in range(n):
+                c = C[v, k]
+                if wh[k] == v:
+                    continue
+                if k == js:
+                    gaps.append(_gap(c, pr[k]))
+                elif c > pr[k] and c > 0:
+                    gaps.append(_gap(best, c))
+                elif c > 0 and (js < 0 or c > best or (c == best and k < js)):
+                    gaps.append(_gap(pr[k], c))
         if ok:
             pr[task], wh[task] = best, v
 
@@ -95,6 +118,10 @@ def _py_cbaa(C, adj, P, rounds):
                 for u in nb[v]:
                     if price[u, j] > price[win, j]:
                         win = u
+                if gaps is not None:
+                    others = [price[u, j] for u in nb[v] if who[u, j] != who[win, j]]
+                    if others:
+                        gaps.append(_gap(price[win, j], max(others)))
                 if who[v, j] == v and who[win, j] != v:
                     outbid = True
                 nw_[v, j], np_[v, j] = who[win, j], price[win, j]
@@ -118,6 +145,71 @@ def test_cbaa_independent_formulation():
         who2, pr2 = _py_cbaa(C, adj, Pin, 2 * n)
         np.testing.assert_array_equal(who, who2)
         np.testing.assert_array_equal(pr, pr2)
+
+
+def test_margin_independent_formulation():
+    """The decision margin (include/aclswarm_amd.h) of the oracle equals the
+    literal minimum over every decisive comparison of the pure-Python CBAA
+    (a different evaluation order: every (v, j) every round, plain min over
+    rounded gaps), and the swarm margin is min(CBAA, alignment) as f32."""
+    for name, L in (("simform20_nc", 20.0), ("simform20_fc", 20.0)):
+        P, A = H.simform(name)
+        rng = np.random.RandomState(11)
+        for s in range(3):
+            n = P.shape[2]
+            q = H.random_positions(rng, n, L)
+            Pin = H.random_perm(rng, n)
+            C, _, ga = O.prices_gap(q, P[s, 0], A[s], Pin)
+            who, pr, eff, gc = O.cbaa_margin(C, A[s], Pin, early_exit=False)
+            gaps = []
+            _py_cbaa(C, A[s], Pin, 2 * n, gaps)
+            assert gc == min(gaps + [1.0])
+            r = O.solve(q, np.zeros((n, 3)), P[s, 0], A[s], np.zeros((3 * n, 3 * n)), Pin)
+            assert r["status"]["margin"] == np.float32(min(gc, ga))
+            assert bool(r["status"]["flags"] & 0x40) == (min(gc, ga) < 1e-6)
+            # the early exit drops only repeated evaluations
+            _, _, _, ge = O.cbaa_margin(C, A[s], Pin, early_exit=True)
+            assert ge == gc
+
+
+def test_margin_ties_are_fragile():
+    """Two vehicles with bit-identical prices for a task they both want: the
+    update (or select) is decided by vehid order alone -> margin 0, FRAGILE."""
+    n = 6
+    adj = np.ones((n, n), np.uint8) - np.eye(n, dtype=np.uint8)
+    C = np.random.RandomState(4).uniform(0.1, 1.0, (n, n)).astype(np.float32)
+    C[0, 3] = C[1, 3] = np.float32(5.0)   # vehicles 0 and 1 both prefer task 3 equally
+    _, _, _, g = O.cbaa_margin(C, adj, np.arange(n, dtype=np.uint16), early_exit=False)
+    assert g == 0.0
+    gaps = []
+    _py_cbaa(C, adj, np.arange(n), 2 * n, gaps)
+    assert min(gaps) == 0.0
+    C[1, 3] = np.float32(4.0)             # distinct prices: no tie
+    _, _, _, g2 = O.cbaa_margin(C, adj, np.arange(n, dtype=np.uint16), early_exit=False)
+    gaps = []
+    _py_cbaa(C, adj, np.arange(n), 2 * n, gaps)
+    assert g2 == min(gaps) > 0.0
+
+
+def test_alignment_gap():
+    """Alignment decision gap: the determinant-sign and rank tests of
+    Eigen::umeyama (3.3.x), against numpy on the same cross-covariance."""
+    rng = np.random.RandomState(3)
+    for _ in range(100):
+        k = rng.randint(3, 25)
+        src = rng.uniform(-5, 5, (k, 2))
+        dst = rng.uniform(-5, 5, (k, 2))
+        _, _, g = O.umeyama2_gap(src, dst)
+        S = (dst - dst.mean(0)).T @ (src - src.mean(0)) / k
+        s = np.linalg.svd(S, compute_uv=False)
+        gd = abs(np.linalg.det(S)) / (abs(S[0, 0] * S[1, 1]) + abs(S[0, 1] * S[1, 0]))
+        gr = abs(s[1] - 1e-12 * s[0]) / max(s[1], 1e-12 * s[0])
+        assert abs(g - min(gd, gr, 1.0)) < 1e-9
+    # collinear points: rank 1 -> the rank test is decided by 1e-12 s0 vs ~0
+    src = np.array([[0, 0], [1, 0], [2, 0], [3, 0.0]])
+    dst = np.array([[5, 5], [5, 6], [5, 7], [5, 8.0]])
+    _, _, g = O.umeyama2_gap(src, dst)
+    assert g == 0.0 or g > 0.5  # det exactly 0 -> 0
 
 
 def test_cbaa_early_exit_exact_and_invariants():
