@@ -15,7 +15,7 @@ ROOT = os.path.dirname(HERE)
 # C++ facade exerciser (include/aclswarm_amd.hpp), run by tests/test_gpu_facade.py
 DRIVER_SRC = os.path.join(ROOT, "tests", "facade_driver.cpp")
 DRIVER = os.path.join(HERE, "lib", "libfacade_driver.so")
-SOURCES = ["solve.hip", "solve_wide.hip", "control.hip", "admm.hip", "hungarian.hip", "episode.hip",
+SOURCES = ["solve.hip", "auction.hip", "solve_wide.hip", "control.hip", "admm.hip", "hungarian.hip", "episode.hip",
            "formation_gen.hip", "api.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",

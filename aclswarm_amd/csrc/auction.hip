@@ -1,0 +1,982 @@
+// auction.hip -- the LDS-resident batched auction for n <= 128 (gfx950).
+//
+// One workgroup (512 threads = 8 wave64) owns one swarm for the whole
+// auction; every per-swarm table lives in LDS (~53 KB at n = 100, three
+// swarms per CU):
+//
+//   phase 0  load p, the adjacency bits, P_in (permutation check), q in
+//            formation order; vehicle-space closed neighbourhoods and their
+//            transpose (`listeners`); the alignment work list
+//   phase 1  2-D Umeyama alignment (Auctioneer::alignFormation,
+//            auctioneer.cpp:347-415). A vehicle's alignment depends only on
+//            its closed formation neighbourhood N[P[v]] (the formation-ordered
+//            q is shared), so one alignment per distinct neighbourhood: every
+//            row with an incomplete neighbourhood plus one row for all the
+//            complete ones (all of them at config C2, ~45% of the rows at C3).
+//            One lane per work item runs both of Eigen's sequential passes
+//            (ascending members; the loads are broadcast, non-members are
+//            masked out of the wave by exec, not by selects) and the 2x2
+//            JacobiSVD finish in registers.
+//   phase 2  price matrix C[v][j] = getPrice (auctioneer.cpp:546-549), fp64
+//            math, f32 result; row n of C is the `none` entry's price 0
+//   phase 3  CBAA rounds (auctioneer.cpp:182-306,469-542) on the `who` table
+//            T (u8, vehicle rows; price of an entry = C[who][j]): per round
+//            the dirty columns (a clean column is a fixed point of
+//            updateTaskAssignment), one wave per column, lanes = vehicles.
+//            A column is resolved level by level: the highest price level of
+//            the column, its holders H (ballot) and `who`; vehicle v takes it
+//            iff H meets N(v) -- a listeners row when |H| = 1, the holders
+//            themselves when every open vehicle holds it, else a per-lane mask
+//            test -- and the next level it meets is its runner-up (decision
+//            margin). Ties, NaN and vehicles no tracked level resolves take
+//            the exact ordered scan. Then outbid vehicles re-select
+//            (selectTaskAssignment) as wave argmaxes. Exact fixed-point exit.
+//   phase 4  adoption (isValidAssignment, auctioneer.cpp:250-295): one
+//            permutation check when every table agrees, per vehicle otherwise
+//
+// Compiled with -ffp-contract=off: every f64 op is one IEEE rounding, so the
+// alignment, prices, assignments and decision margins are bit-identical to
+// the CPU restatement (oracle/). Per-lane booleans are SGPR lane masks
+// (inverse_ballot / ballot convert at no VALU cost).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/aclswarm_amd.h"
+#include "common.h"
+#include "control_params.h"
+#include "umeyama_dev.h"
+
+namespace acl_amd {
+
+constexpr int kAB = 512;       // threads per swarm
+constexpr int kAW = kAB / 64;  // waves per swarm
+#ifndef ACL_AUCTION_LEVELS
+#define ACL_AUCTION_LEVELS 4   // price levels per dirty column before the exact scan
+#endif
+constexpr int kAL = ACL_AUCTION_LEVELS;
+
+__host__ __device__ inline int a16(int x) { return (x + 15) & ~15; }
+
+// LDS layout (byte offsets). C's region first holds the alignment inputs
+// (pq, adjF, items: phases 0-1 only); region A (p, qf, out: phases 0-2) is
+// overlaid by the who table T from phase 3 on.
+struct ALayout {
+  int C, pq, adjF, items;
+  int A, p, qf, out;
+  int T, TS;
+  int vadj, lst, Pin, Ptin, itm, valid, H, misc, total;
+};
+
+__host__ __device__ inline ALayout make_alayout(int n) {
+  ALayout L;
+  int o = 0;
+  L.TS = (n + 3) & ~3;  // T row stride: rows compare as dwords
+  L.C = o;
+  {
+    const int csz = (n + 1) * n * 4;
+    const int pre = a16(n * 32) + a16(n * 16) + a16(n);
+    o = a16(o + (csz > pre ? csz : pre));
+  }
+  L.pq = L.C;                      // [n] {p.x, p.y, qf.x, qf.y} f64
+  L.adjF = L.pq + a16(n * 32);     // [n][2] u64 formation rows (no diagonal)
+  L.items = L.adjF + a16(n * 16);  // [n] u8 alignment work list (rows)
+  L.A = o;
+  L.p = o;    o = a16(o + n * 24);
+  L.qf = o;   o = a16(o + n * 24);
+  L.out = o;  o = a16(o + n * 48);   // R, t per work item
+  L.T = L.A;
+  if (L.A + n * L.TS > o) o = a16(L.A + n * L.TS);
+  L.vadj = o;  o = a16(o + n * 16);  // [v][2] closed neighbourhood of vehicle v
+  L.lst = o;   o = a16(o + n * 16);  // [h][2] vehicles whose neighbourhood holds h
+  L.Pin = o;   o = a16(o + n);
+  L.Ptin = o;  o = a16(o + n);
+  L.itm = o;   o = a16(o + n);       // work item of formation row i
+  L.valid = o; o = a16(o + n);
+  L.H = o;     o = a16(o + 16 * 8);  // dmask[2][2], obm[2][2], seen[2]
+  L.misc = o;  o = a16(o + 16 * 4);
+  L.total = o;
+  return L;
+}
+
+enum { A_NITEMS = 2 };
+
+// diagnostic builds (-DACL_AUCTION_STOP=k): the kernel returns after phase
+// k, for per-phase instruction counts (scripts/auction_phase_pmc.sh)
+#ifndef ACL_AUCTION_STOP
+#define ACL_AUCTION_STOP 0
+#endif
+#define ACL_AUCTION_STOP_AT(k) \
+  if (ACL_AUCTION_STOP == (k)) return
+
+// the four doubles of pq[j] (broadcast LDS reads)
+__device__ __forceinline__ void load4(const double* pq, int j, double (&v)[4]) {
+  const double2 a = *reinterpret_cast<const double2*>(pq + 4 * j);
+  const double2 c = *reinterpret_cast<const double2*>(pq + 4 * j + 2);
+  v[0] = a.x; v[1] = a.y; v[2] = c.x; v[3] = c.y;
+}
+
+// For j = 0 .. n-1 in order: f(mask, pq[j]) with mask = the lanes whose
+// neighbourhood bits r hold j. pq[j] is a broadcast read issued one term
+// ahead (ping-pong buffers, so no register copies wait on it).
+template <int NC, typename F>
+__device__ __forceinline__ void for_members(int n, const double* pq,
+                                            const unsigned long long (&r)[2], F&& f) {
+  double A[4], B[4];
+  load4(pq, 0, A);
+#pragma unroll
+  for (int w = 0; w < NC; ++w) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const unsigned word = (unsigned)(r[w] >> (32 * hf));
+      const int j0 = 64 * w + 32 * hf;
+#pragma unroll 1
+      for (int x = 0; x < 32; x += 2) {
+        const int j = j0 + x;
+        if (j >= n) break;
+        load4(pq, j + 1 < n ? j + 1 : j, B);
+        f(__ballot(word & (1u << x)), A);
+        if (j + 1 >= n) break;
+        load4(pq, j + 2 < n ? j + 2 : j + 1, A);
+        f(__ballot(word & (2u << x)), B);
+      }
+    }
+  }
+}
+
+// a_k += v_k in the lanes of `mask` only (the others keep a_k): exec is
+// narrowed around the four adds, so non-members cost no selects and leave no
+// trace in the sums (Eigen's sums run over the members only)
+__device__ __forceinline__ void masked_add4(unsigned long long mask, double& a0, double& a1,
+                                            double& a2, double& a3, double v0, double v1,
+                                            double v2, double v3) {
+  unsigned long long sv;
+  asm volatile(
+      "s_and_saveexec_b64 %[sv], %[m]\n\t"
+      "v_add_f64 %[a0], %[a0], %[v0]\n\t"
+      "v_add_f64 %[a1], %[a1], %[v1]\n\t"
+      "v_add_f64 %[a2], %[a2], %[v2]\n\t"
+      "v_add_f64 %[a3], %[a3], %[v3]\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3), [sv] "=&s"(sv)
+      : [m] "s"(mask), [v0] "v"(v0), [v1] "v"(v1), [v2] "v"(v2), [v3] "v"(v3)
+      : "scc");  // s_and_saveexec writes SCC
+}
+
+// diagnostic: s_memtime at phase ends (scripts/phase_profile.py)
+__device__ __forceinline__ void stamp_phase(const SolveParams& P, int b, int tid, int k) {
+  if (P.stamps && tid == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
+}
+
+// margin_track on a wave-uniform pair, branch-free (selects)
+__device__ __forceinline__ void margin_track_u(float& hi, float& lo, float h, float l) {
+  const bool tie = l == h;
+  const bool up = l < h && (double)l * (double)hi > (double)lo * (double)h;
+  hi = tie ? 1.0f : (up ? h : hi);
+  lo = tie ? 1.0f : (up ? l : lo);
+}
+
+__device__ __forceinline__ bool lanebit(unsigned long long m) {
+  return __builtin_amdgcn_inverse_ballot_w64(m);
+}
+
+// the who-table entry of lane-vehicle row `row`, task j, and its price key
+// (price bits + 1; `none` = row n of C has price 0 -> key 1)
+__device__ __forceinline__ unsigned entry_key(const float* C, int n, int w, int j) {
+  return __float_as_uint(C[w * n + j]) + 1u;
+}
+
+// selectTaskAssignment (auctioneer.cpp:517-542) for vehicle v as a wave
+// argmax over its row (lanes = tasks), with the margin of its decisive
+// comparisons (include/aclswarm_amd.h). fresh: the START bid on an all-`none`
+// row. Returns the selected task (wave-uniform) or -1.
+template <int NC>
+__device__ __forceinline__ int wave_select(int n, int TS, int v, int lane, const float* C,
+                                           const unsigned char* T, bool fresh, MarginPair& m) {
+  unsigned key[NC];
+  float cv[NC], pr[NC];
+  bool oth[NC];
+  unsigned lm = 0u;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int j = lane + 64 * c;
+    const bool ok = j < n;
+    const int jj = ok ? j : 0;
+    const int w = fresh ? n : T[v * TS + jj];
+    cv[c] = C[v * n + jj];
+    pr[c] = C[w * n + jj];
+    key[c] = (ok && cv[c] > 0.0f && cv[c] > pr[c]) ? __float_as_uint(cv[c]) : 0u;
+    oth[c] = ok && w != v;
+    lm = lm > key[c] ? lm : key[c];
+  }
+  const unsigned M = wave_max_u32(lm);
+  int js = -1;
+  if (M != 0u) {
+#pragma unroll
+    for (int c = NC - 1; c >= 0; --c) {
+      const unsigned long long e = __ballot(key[c] == M);
+      if (e) js = 64 * c + __ffsll((long long)e) - 1;
+    }
+  }
+  const float cmax = __uint_as_float(M);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int j = lane + 64 * c;
+    if (oth[c]) {
+      if (j == js) margin_track(m, cv[c], pr[c]);
+      else if (key[c] != 0u) margin_track(m, cmax, cv[c]);
+      else if (cv[c] > 0.0f && (js < 0 || cv[c] > cmax || (cv[c] == cmax && j < js)))
+        margin_track(m, pr[c], cv[c]);
+    }
+  }
+  return js;
+}
+
+// `who` of the first holder (lowest vehicle index) of a level
+template <int NC>
+__device__ __forceinline__ int first_who(const unsigned long long (&h)[NC], const int (&wu)[NC]) {
+  int hl = 0, src = wu[0];
+#pragma unroll
+  for (int c = NC - 1; c >= 0; --c)
+    if (h[c]) {
+      hl = __ffsll((long long)h[c]) - 1;
+      src = wu[c];
+    }
+  return __builtin_amdgcn_readlane(src, hl);
+}
+
+// the highest price key of the column below `cap` (0: none)
+template <int NC>
+__device__ __forceinline__ unsigned level_key(const unsigned (&key)[NC], unsigned cap) {
+  unsigned x = 0u;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const unsigned y = key[c] < cap ? key[c] : 0u;
+    x = x > y ? x : y;
+  }
+  return wave_max_u32(x);
+}
+
+// vehicles (lane masks of `open`) whose closed neighbourhood holds a level
+// held by h (nh holders, the first hl): the listeners row of hl when it is
+// the only holder; the open vehicles themselves when all of them hold it
+// (v is in N(v)); otherwise a per-lane mask test
+template <int NC>
+__device__ __forceinline__ void level_hits(const unsigned long long (&open)[NC],
+                                           const unsigned long long (&h)[NC],
+                                           const unsigned long long (&vm)[NC][NC],
+                                           unsigned long long (&hitm)[NC]) {
+  // a per-lane mask test (vector work; the scalar unit is the kernel's
+  // bottleneck, so no branches on the holder set)
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    unsigned long long t = 0ull;
+#pragma unroll
+    for (int w = 0; w < NC; ++w) t |= vm[c][w] & h[w];
+    hitm[c] = __ballot(t != 0ull) & open[c];
+  }
+}
+
+// The exact decision gaps of a column's level-resolved vehicles (k1 != 0):
+// walk the levels again; a vehicle's runner-up is the first level below its
+// winning level that its neighbourhood holds. The largest ratio among the
+// vehicles that meet their runner-up at a level belongs to the lowest winning
+// level among them (wave minimum of k1), tracked into the wave's pair.
+template <int NC>
+__device__ __forceinline__ void runner_up_walk(int n, const unsigned (&key)[NC],
+                                               const unsigned (&k1)[NC],
+                                               const unsigned long long (&Nd)[NC],
+                                               const unsigned long long (&vm)[NC][NC],
+                                               float& uhi, float& ulo) {
+  unsigned long long D[NC];  // resolved by a level, runner-up not met yet
+#pragma unroll
+  for (int c = 0; c < NC; ++c) D[c] = __ballot(k1[c] != 0u) & ~Nd[c];
+  unsigned cap = 0xFFFFFFFFu;
+  int cum = 0;
+  for (int k = 0; k < 2 * kMaxN + 2; ++k) {
+    unsigned long long any = 0ull;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) any |= D[c];
+    if (!any || cum >= n) break;
+    const unsigned Mk = level_key<NC>(key, cap);
+    if (Mk == 0u) break;
+    unsigned long long h[NC], open[NC], hitm[NC];
+    int nh = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      h[c] = __ballot(key[c] == Mk);
+      nh += __popcll(h[c]);
+      open[c] = D[c] & __ballot(k1[c] > Mk);  // only below the winning level
+    }
+    cum += nh;
+    level_hits<NC>(open, h, vm, hitm);
+    unsigned lowest = 0u;  // ~min k1 over the vehicles meeting it here
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const unsigned x = lanebit(hitm[c]) ? ~k1[c] : 0u;
+      lowest = lowest > x ? lowest : x;
+      D[c] &= ~hitm[c];
+    }
+    lowest = wave_max_u32(lowest);
+    if (lowest != 0u)
+      margin_track_u(uhi, ulo, __uint_as_float(~lowest - 1u), __uint_as_float(Mk - 1u));
+    cap = Mk;
+  }
+}
+
+template <int NC>
+__global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = P.n;
+  const ALayout L = make_alayout(n);
+  const int TS = L.TS;
+  const int b = P.b0 + blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  float* C = reinterpret_cast<float*>(smem + L.C);
+  double* pq = reinterpret_cast<double*>(smem + L.pq);
+  unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
+  unsigned char* items = smem + L.items;
+  double* p = reinterpret_cast<double*>(smem + L.p);
+  double* qf = reinterpret_cast<double*>(smem + L.qf);
+  double* out = reinterpret_cast<double*>(smem + L.out);
+  unsigned char* T = smem + L.T;
+  unsigned long long* vadj = reinterpret_cast<unsigned long long*>(smem + L.vadj);
+  unsigned long long* lst = reinterpret_cast<unsigned long long*>(smem + L.lst);
+  unsigned char* Pin = smem + L.Pin;
+  unsigned char* Ptin = smem + L.Ptin;
+  unsigned char* itm = smem + L.itm;
+  unsigned char* validv = smem + L.valid;
+  unsigned long long* H = reinterpret_cast<unsigned long long*>(smem + L.H);
+  int* misc = reinterpret_cast<int*>(smem + L.misc);
+  unsigned long long* margw = reinterpret_cast<unsigned long long*>(misc + M_MARG);
+
+  // a formation index out of range is a bad input like a bad P_in (nothing
+  // of the formation table is read for it)
+  const int f_in = P.fidx[b];
+  const bool fbad = f_in < 0 || f_in >= P.F;
+  const int f = fbad ? 0 : f_in;
+  const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+  MarginPair mp;
+  margin_init(mp);
+  double galign = 1.0;
+  stamp_phase(P, b, tid, 0);
+
+  // ---------------- phase 0: load ------------------------------------------
+  {
+    const double* gp = P.p + (size_t)f * n * 3;
+    for (int k = tid; k < 3 * n; k += kAB) p[k] = gp[k];
+    const uint64_t* ga = P.adj + (size_t)f * n * NC;
+    for (int k = tid; k < 2 * n; k += kAB) {
+      const int i = k >> 1, w = k & 1;
+      unsigned long long x = 0ull;
+      if (w < NC) {
+        x = ga[(size_t)i * NC + w];
+        if (w == NC - 1) x &= lastmask;
+      }
+      adjF[k] = x;
+    }
+    if (tid < 16) {
+      misc[tid] = 0;
+      H[tid] = 0ull;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    misc[M_AGREE] = 1;
+    if (fbad) misc[M_BAD] = 1;
+    *margw = (unsigned long long)__double_as_longlong(1.0);
+  }
+  for (int v = tid; v < n; v += kAB) {
+    const unsigned pv = P.P_in[(size_t)b * n + v];
+    Pin[v] = (unsigned char)pv;
+    if (pv >= (unsigned)n) {
+      misc[M_BAD] = 1;
+    } else {
+      const unsigned long long bit = 1ull << (pv & 63);
+      if (atomicOr(&H[8 + (pv >> 6)], bit) & bit) misc[M_BAD] = 1;  // not a permutation
+      Ptin[pv] = (unsigned char)v;
+    }
+  }
+  __syncthreads();
+  if (misc[M_BAD]) {
+    // P_in is not a permutation (or fidx is out of range): nothing is solved
+    for (int v = tid; v < n; v += kAB) {
+      P.P_out[(size_t)b * n + v] = P.P_in[(size_t)b * n + v];
+      if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 0;
+    }
+    for (int k = tid; k < 3 * n; k += kAB) {
+      if (P.u) P.u[(size_t)b * n * 3 + k] = 0.0;
+      if (P.u_safe) P.u_safe[(size_t)b * n * 3 + k] = 0.0;
+    }
+    if (P.who)
+      for (int k = tid; k < n * n; k += kAB) P.who[(size_t)b * n * n + k] = 0xFFFF;
+    if (P.gate_margin && tid == 0) P.gate_margin[b] = __builtin_inf();
+    if (tid == 0) {
+      acl_swarm_status_t st = {};
+      st.flags = ACL_SWARM_BAD_INPUT;
+      st.rounds = (uint16_t)(2 * n);
+      st.margin = 1.0f;
+      P.status[b] = st;
+    }
+    return;
+  }
+  // q in formation order: qf[j] = q[Pt[j]]; pq[j] = {p_j.xy, qf_j.xy}
+  {
+    const double* gq = P.q + (size_t)b * n * 3;
+    for (int j = tid; j < n; j += kAB) {
+      const double* qv = gq + 3 * Ptin[j];
+      const double x = qv[0], y = qv[1], z = qv[2];
+      qf[3 * j] = x; qf[3 * j + 1] = y; qf[3 * j + 2] = z;
+      double* o = pq + 4 * j;
+      o[0] = p[3 * j]; o[1] = p[3 * j + 1]; o[2] = x; o[3] = y;
+    }
+  }
+  // closed neighbourhoods in vehicle space (bidIterComplete, auctioneer.cpp:
+  // 419-437): u ~ v iff u == v or adj(P[v], P[u]); and the transpose
+  // lst[h] = {v : h in N(v)} (u ~ v with the roles swapped)
+  {
+    int pu[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) pu[c] = (lane + 64 * c < n) ? Pin[lane + 64 * c] : 0;
+    for (int v = wave; v < n; v += kAW) {
+      const int i = Pin[v];
+      const unsigned long long r0 = adjF[2 * i], r1 = adjF[2 * i + 1];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int u = lane + 64 * c;
+        const bool okl = u < n;
+        const bool e = okl && (u == v || (((pu[c] < 64 ? r0 : r1) >> (pu[c] & 63)) & 1ull));
+        const unsigned long long ru = adjF[2 * pu[c] + (i >> 6)];
+        const bool t = okl && (u == v || ((ru >> (i & 63)) & 1ull));
+        const unsigned long long me = __ballot(e), mt = __ballot(t);
+        if (lane == 0) {
+          vadj[2 * v + c] = me;
+          lst[2 * v + c] = mt;
+        }
+      }
+      if (NC == 1 && lane == 0) {
+        vadj[2 * v + 1] = 0ull;
+        lst[2 * v + 1] = 0ull;
+      }
+    }
+  }
+  // alignment work list (wave 0): incomplete rows ascending, then one row
+  // standing for every complete closed neighbourhood
+  if (wave == 0) {
+    unsigned long long cm[NC], im[NC];
+    int base = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = lane + 64 * c;
+      bool comp = false;
+      if (i < n) {
+        unsigned long long r0 = adjF[2 * i], r1 = adjF[2 * i + 1];
+        if (i < 64) r0 |= 1ull << i; else r1 |= 1ull << (i - 64);
+        comp = (__popcll(r0) + __popcll(r1)) == n;
+      }
+      cm[c] = __ballot(comp);
+      im[c] = __ballot(i < n && !comp);
+    }
+    int rep = -1;
+#pragma unroll
+    for (int c = NC - 1; c >= 0; --c)
+      if (cm[c]) rep = 64 * c + __ffsll((long long)cm[c]) - 1;
+    int ninc = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) ninc += __popcll(im[c]);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = lane + 64 * c;
+      const int rk = base + (int)__builtin_amdgcn_mbcnt_hi(
+                                (unsigned)(im[c] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im[c], 0u));
+      if (lanebit(im[c])) {
+        items[rk] = (unsigned char)i;
+        itm[i] = (unsigned char)rk;
+      } else if (lanebit(cm[c])) {
+        itm[i] = (unsigned char)ninc;
+      }
+      base += __popcll(im[c]);
+    }
+    if (lane == 0) {
+      if (rep >= 0) items[ninc] = (unsigned char)rep;
+      misc[A_NITEMS] = ninc + (rep >= 0 ? 1 : 0);
+    }
+  }
+  __syncthreads();
+  stamp_phase(P, b, tid, 1);
+  ACL_AUCTION_STOP_AT(1);
+
+  // ---------------- phase 1: alignment --------------------------------------
+  // Eigen::umeyama (3.3.x) per work item, one lane each: pass 1 rowwise sums
+  // of src (p) and dst (qf) over the members in ascending order, pass 2
+  // sigma = one_over_n * dst_demean * src_demean^T -- the lazy product
+  // (scaled lhs, from the first term) when k + 4 < 20, else the GEMM form
+  // (0.0 + every term, alpha after). A sum starts at -0.0, the identity of
+  // IEEE addition (x + -0.0 = x for every x), which is the first-element
+  // start exactly. The members' values are broadcast loads; a lane adds a
+  // term only for its members (exec-masked branch: asm barriers keep the
+  // compiler from turning it into selects).
+  {
+    const int nitems = misc[A_NITEMS];
+    if (wave * 64 < nitems) {
+      const int k = wave * 64 + lane;
+      const bool act = k < nitems;
+      const int i = act ? items[k] : 0;
+      unsigned long long r[2] = {adjF[2 * i], adjF[2 * i + 1]};
+      if (i < 64) r[0] |= 1ull << i; else r[1] |= 1ull << (i - 64);
+      if (!act) r[0] = r[1] = 0ull;
+      const int cnt = __popcll(r[0]) + __popcll(r[1]);
+      // pass 1: rowwise sums of src (p.xy) and dst (qf.xy)
+      double s0 = -0.0, s1 = -0.0, s2 = -0.0, s3 = -0.0;
+      for_members<NC>(n, pq, r, [&](unsigned long long mk, const double (&v)[4]) {
+        masked_add4(mk, s0, s1, s2, s3, v[0], v[1], v[2], v[3]);
+      });
+      const double oon = 1.0 / (double)(act ? cnt : 1);
+      const double sm0 = s0 * oon, sm1 = s1 * oon, dm0 = s2 * oon, dm1 = s3 * oon;
+      const bool lazy = (cnt + 4) < 20;
+      const double scale = lazy ? oon : 1.0;  // 1.0 * x == x
+      const double a0 = lazy ? -0.0 : 0.0;
+      double a00 = a0, a01 = a0, a10 = a0, a11 = a0;  // a(di, sj)
+      for_members<NC>(n, pq, r, [&](unsigned long long mk, const double (&v)[4]) {
+        const double e0 = v[0] - sm0, e1 = v[1] - sm1;
+        const double d0 = scale * (v[2] - dm0), d1 = scale * (v[3] - dm1);
+        masked_add4(mk, a00, a01, a10, a11, d0 * e0, d0 * e1, d1 * e0, d1 * e1);
+      });
+      if (act) {
+        // column-major sigma S(di, sj)
+        const double S[4] = {lazy ? a00 : a00 * oon, lazy ? a10 : a10 * oon,
+                             lazy ? a01 : a01 * oon, lazy ? a11 : a11 * oon};
+        const double sm[2] = {sm0, sm1}, dm[2] = {dm0, dm1};
+        double R[4], t[2], ga;
+        umeyama_finish(S, sm, dm, R, t, &ga);
+        galign = ga;
+        double* o = out + 6 * k;
+        o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
+      }
+    }
+  }
+  __syncthreads();
+  stamp_phase(P, b, tid, 2);
+  ACL_AUCTION_STOP_AT(2);
+  if (P.align_Rt)
+    for (int k = tid; k < 6 * n; k += kAB) {
+      const int v = k / 6;
+      P.align_Rt[(size_t)b * n * 6 + k] = out[6 * itm[Pin[v]] + (k - 6 * v)];
+    }
+
+  // ---------------- phase 2: prices -----------------------------------------
+  {
+    int nonfin = 0;
+    const int per = kAB / n;
+    const int j = tid % n, v0 = tid / n;
+    const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
+    for (int v = v0; v0 < per && v < n; v += per) {
+      const int ip = Pin[v];
+      const double* o = out + 6 * itm[ip];
+      const double* qv = qf + 3 * ip;
+      const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
+      const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
+      const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
+      const double dx = qv[0] - ax, dy = qv[1] - ay, dz = qv[2] - az;
+      const double nrm = sqrt((dx * dx + dy * dy) + dz * dz);
+      const float c = (float)(1.0 / (nrm + 1e-8));
+      C[v * n + j] = c;
+      nonfin |= (c != c);
+    }
+    if (__any(nonfin) && lane == 0) misc[M_NONFIN] = 1;
+    for (int jj = tid; jj < n; jj += kAB) C[n * n + jj] = 0.0f;  // the `none` row
+  }
+  // per-lane neighbourhood masks of this lane's vehicles (lane + 64 c)
+  unsigned long long vm[NC][NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int v = lane + 64 * c;
+#pragma unroll
+    for (int w = 0; w < NC; ++w) vm[c][w] = (v < n) ? vadj[2 * v + w] : 0ull;
+  }
+  __syncthreads();  // region A (p, qf, out) is dead from here: T overlays it
+  const bool nonfinite = misc[M_NONFIN] != 0;
+  {
+    // reset (auctioneer.cpp:448-465): every entry `none`
+    const unsigned fill = (unsigned)n * 0x01010101u;
+    unsigned* T32 = reinterpret_cast<unsigned*>(T);
+    for (int k = tid; k < n * TS / 4; k += kAB) T32[k] = fill;
+  }
+  stamp_phase(P, b, tid, 3);
+  ACL_AUCTION_STOP_AT(3);
+
+  // ---------------- phase 3: CBAA -------------------------------------------
+  unsigned long long* dmask = H;      // [2 parities][2 words]
+  unsigned long long* obm = H + 4;    // [2][2]
+  // round 0: the START bid, select from the zero table (start, auctioneer.cpp:105)
+  for (int v = wave; v < n; v += kAW) {
+    const int task = wave_select<NC>(n, TS, v, lane, C, T, true, mp);
+    if (task >= 0 && lane == 0) {
+      T[v * TS + task] = (unsigned char)v;
+      atomicOr(&dmask[2 + (task >> 6)], 1ull << (task & 63));
+    }
+  }
+  __syncthreads();
+  ACL_AUCTION_STOP_AT(4);
+
+  bool okv[NC];
+  unsigned long long okm[NC];
+  unsigned okk[NC];  // key mask: all ones for real vehicles, 0 past n
+  int rowa[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    okv[c] = lane + 64 * c < n;
+    okm[c] = __ballot(okv[c]);
+    okk[c] = okv[c] ? 0xFFFFFFFFu : 0u;
+    rowa[c] = (okv[c] ? lane + 64 * c : 0) * TS;
+  }
+  // the wave's uniform margin pair over the level-resolved evaluations
+  float uhi = 1.0f, ulo = 0.0f;
+  int eff = 0;
+  const int max_rounds = 2 * n;  // cbaa_max_iter_ = n * diameter (:50-51)
+  for (int r = 1; r <= max_rounds; ++r) {
+    const int par = r & 1, npar = par ^ 1;
+    // this wave's dirty columns: every 8th set bit in rank order
+    unsigned long long mine[NC];
+    {
+      int base = 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const unsigned long long D = uni_u64(dmask[2 * par + c]);
+        const int rk = base + (int)__builtin_amdgcn_mbcnt_hi(
+                                  (unsigned)(D >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)D, 0u));
+        mine[c] = __ballot(((D >> lane) & 1ull) && (rk & (kAW - 1)) == wave);
+        base += __popcll(D);
+      }
+    }
+    {
+      // one loop over both words (the column body is emitted once)
+      unsigned long long mm = mine[0], m1 = NC > 1 ? mine[NC - 1] : 0ull;
+      int jb = 0;
+      for (;;) {
+        if (!mm) {
+          if (!m1) break;
+          mm = m1;
+          m1 = 0ull;
+          jb = 64;
+        }
+        const int j = jb + __ffsll((long long)mm) - 1;
+        mm &= mm - 1;
+        // one wave per dirty column, lanes = vehicles
+        int wu[NC], nw[NC];
+        unsigned key[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          // every lane reads (rows clamped, who <= n): no exec masking
+          wu[c] = T[rowa[c] + j];
+          key[c] = entry_key(C, n, wu[c], j) & okk[c];
+          nw[c] = wu[c];
+        }
+        // level 0: the column's highest price key, its holders and `who`.
+        // A column whose every entry is that one (price, who) is a fixed
+        // point with no runner-up: nothing to do (a third of the dirty
+        // columns: the round after the last vehicles adopted an entry).
+        unsigned M0 = level_key<NC>(key, 0xFFFFFFFFu);
+        unsigned long long h[NC];
+        int cum = 0;
+        bool full = true;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          h[c] = __ballot(key[c] == M0);
+          cum += __popcll(h[c]);
+          full = full && h[c] == okm[c];
+        }
+        int wk = first_who<NC>(h, wu);
+        unsigned long long tie = 0ull;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) tie |= h[c] & __ballot(wu[c] != wk);
+        if (full && !tie && !nonfinite) continue;
+        // winners, level by level. Per-vehicle state as lane masks: U = not
+        // yet resolved, Nd = exact scan. Each resolving level's successor
+        // bounds the decision gap of the vehicles it resolved (their
+        // runner-up is that level or a lower one).
+        unsigned long long U[NC], Nd[NC];
+        unsigned k1[NC];  // a vehicle's winning level key (0: tie / scan)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          U[c] = okm[c];
+          Nd[c] = 0ull;
+          k1[c] = 0u;
+        }
+        unsigned Mk = M0, kres = 0u;  // kres: the last level that resolved a vehicle
+        float bhi = 1.0f, blo = 0.0f;  // bound pair (largest ratio)
+#pragma unroll 1
+        for (int k = 0;;) {
+          const bool tk = nonfinite || tie != 0ull;
+          unsigned long long hitm[NC];
+          level_hits<NC>(U, h, vm, hitm);
+          const unsigned kv = tk ? 0u : Mk;
+          unsigned long long left = 0ull, res = 0ull;
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            const bool hit = lanebit(hitm[c]);
+            nw[c] = hit ? wk : nw[c];
+            k1[c] = hit ? kv : k1[c];
+            Nd[c] |= tk ? hitm[c] : 0ull;
+            U[c] &= ~hitm[c];
+            left |= U[c];
+            res |= hitm[c];
+          }
+          kres = (!tk && res) ? Mk : 0u;
+          if (!left || ++k == kAL) break;
+          // the next level
+          Mk = level_key<NC>(key, Mk);
+          margin_track_u(bhi, blo, __uint_as_float(kres - 1u), __uint_as_float(Mk - 1u));
+          // (kres == 0 or Mk == 0: a pair with lo > hi or lo == 0, no effect
+          // -- except kres == 0 == Mk, a tie of two -0.0f... excluded below)
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            h[c] = __ballot(key[c] == Mk);
+            cum += __popcll(h[c]);
+          }
+          wk = first_who<NC>(h, wu);
+          tie = 0ull;
+#pragma unroll
+          for (int c = 0; c < NC; ++c) tie |= h[c] & __ballot(wu[c] != wk);
+        }
+        if (kres != 0u && cum < n) {  // the resolving level's successor
+          const unsigned Mn = level_key<NC>(key, kres);
+          margin_track_u(bhi, blo, __uint_as_float(kres - 1u), __uint_as_float(Mn - 1u));
+        }
+        // the exact runner-ups only where the bound could lower the wave's
+        // running minimum (an evaluation skipped here has a gap >= the bound
+        // >= a gap already tracked, so the minimum is unchanged)
+        if ((double)blo * (double)uhi > (double)ulo * (double)bhi)
+          runner_up_walk<NC>(n, key, k1, Nd, vm, uhi, ulo);
+        // the exact ordered scan (ascending vehid, strict >) for ties, NaN
+        // prices and vehicles the levels did not resolve; the runner-up is the
+        // best price of another `who` (entries of one `who` share its price)
+        unsigned long long scan = 0ull;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          Nd[c] |= U[c];
+          scan |= Nd[c];
+        }
+        if (scan) {
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            if (lanebit(Nd[c])) {
+              float bp = 0.0f, p2 = 0.0f;
+              int bw = n;
+              bool first = true, have2 = false;
+#pragma unroll
+              for (int w2 = 0; w2 < NC; ++w2) {
+                unsigned long long m2 = vm[c][w2];
+                while (m2) {
+                  const int u = 64 * w2 + __ffsll((long long)m2) - 1;
+                  m2 &= m2 - 1;
+                  const int wx = T[u * TS + j];
+                  const float px = C[wx * n + j];
+                  if (first) {
+                    bp = px; bw = wx; first = false;
+                  } else if (px > bp) {
+                    p2 = bp; have2 = true;  // the old winner's `who` differs
+                    bp = px; bw = wx;
+                  } else if (wx != bw) {
+                    if (!have2 || px > p2) p2 = px;
+                    have2 = true;
+                  }
+                }
+              }
+              nw[c] = bw;
+              if (have2) margin_track(mp, bp, p2);
+            }
+          }
+        }
+        // the scan read the column: rewrite it only now
+        __builtin_amdgcn_wave_barrier();
+        unsigned long long ch = 0ull;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          if (okv[c]) T[rowa[c] + j] = (unsigned char)nw[c];
+          const int u = lane + 64 * c;
+          const unsigned long long ob = __ballot(okv[c] && wu[c] == u && nw[c] != u);
+          if (ob && lane == 0) atomicOr(&obm[2 * par + c], ob);  // outbid (auctioneer.cpp:502)
+          ch |= __ballot(nw[c] != wu[c]);
+        }
+        if (ch && lane == 0) atomicOr(&dmask[2 * npar + (j >> 6)], 1ull << (j & 63));
+      }
+    }
+    __syncthreads();
+    // outbid vehicles re-select on their updated rows (auctioneer.cpp:224)
+    {
+      if (tid == 0) {
+        dmask[2 * par] = 0ull;  // consumed; becomes round r+2's mask
+        dmask[2 * par + 1] = 0ull;
+        obm[2 * npar] = 0ull;   // round r+1's outbid mask
+        obm[2 * npar + 1] = 0ull;
+      }
+      int base = 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const unsigned long long O = uni_u64(obm[2 * par + c]);
+        const int rk = base + (int)__builtin_amdgcn_mbcnt_hi(
+                                  (unsigned)(O >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)O, 0u));
+        unsigned long long mv = __ballot(((O >> lane) & 1ull) && (rk & (kAW - 1)) == wave);
+        base += __popcll(O);
+        while (mv) {
+          const int v = 64 * c + __ffsll((long long)mv) - 1;
+          mv &= mv - 1;
+          const int task = wave_select<NC>(n, TS, v, lane, C, T, false, mp);
+          if (task >= 0 && lane == 0) {
+            T[v * TS + task] = (unsigned char)v;
+            atomicOr(&dmask[2 * npar + (task >> 6)], 1ull << (task & 63));
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const bool changed = (dmask[2 * npar] | dmask[2 * npar + 1]) != 0ull;
+    if (changed) eff = r;
+    else if (P.early_exit) break;  // fixed point
+  }
+  stamp_phase(P, b, tid, 4);
+  ACL_AUCTION_STOP_AT(5);
+  {  // swarm margin: every lane's pair, the wave's level pair, the alignments
+    margin_track(mp, uhi, ulo);
+    const double gc = margin_gap(mp);
+    block_min_gap(margw, gc < galign ? gc : galign);
+  }
+
+  // ---------------- phase 4: adoption ---------------------------------------
+  // do all vehicles hold vehicle 0's table? (rows compared as dwords; the
+  // padding bytes of a row are `none` in every row)
+  {
+    const unsigned* T32 = reinterpret_cast<const unsigned*>(T);
+    const int rw = TS / 4;
+    bool diff = false;
+    for (int k = tid; k < n * rw; k += kAB) diff |= T32[k] != T32[k % rw];
+    if (__any(diff) && lane == 0) misc[M_AGREE] = 0;
+  }
+  __syncthreads();
+  const bool allagree = misc[M_AGREE] != 0;
+  // isValidAssignment (auctioneer.cpp:325-343) of a table row: one wave,
+  // lanes over tasks; a permutation <=> every entry < n and the OR of the
+  // one-hot entries has n bits
+  auto row_valid = [&](const unsigned char* row) -> bool {
+    unsigned lo[4] = {0u, 0u, 0u, 0u};
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int jj = lane + 64 * c;
+      if (jj < n) {
+        const int w = row[jj];
+        if (w >= n) bad = true;
+        else lo[w >> 5] |= 1u << (w & 31);
+      }
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int q4 = 0; q4 < 2 * NC; ++q4) cnt += __popc(wave_or_u32(lo[q4]));
+    return !__any(bad) && cnt == n;
+  };
+  if (allagree) {
+    // one table: its validity is every vehicle's; vehicle T[0][j] adopts j
+    const bool valid0 = row_valid(T);  // every wave checks row 0 (no barrier)
+    if (tid == 0 && !valid0) misc[M_NINV] = n;
+    for (int jj = tid; jj < n; jj += kAB) {
+      const int v = valid0 ? T[jj] : Ptin[jj];
+      P.P_out[(size_t)b * n + v] = (uint16_t)jj;
+      validv[v] = valid0;
+      if (jj != Pin[v]) misc[M_CHANGED] = 1;
+    }
+  } else {
+    for (int v = wave; v < n; v += kAW) {
+      const unsigned char* row = T + v * TS;
+      bool ismine[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int jj = lane + 64 * c;
+        ismine[c] = (jj < n) && (row[jj] == v);
+      }
+      int mine = -1;
+#pragma unroll
+      for (int c = NC - 1; c >= 0; --c) {
+        const unsigned long long mm = __ballot(ismine[c]);
+        if (mm) mine = 64 * c + __ffsll((long long)mm) - 1;
+      }
+      const bool valid = row_valid(row) && mine >= 0;
+      const int adopted = valid ? mine : Pin[v];
+      if (lane == 0) {
+        validv[v] = valid;
+        if (!valid) atomicAdd(&misc[M_NINV], 1);
+        if (adopted != Pin[v]) misc[M_CHANGED] = 1;
+        P.P_out[(size_t)b * n + v] = (uint16_t)adopted;
+      }
+    }
+  }
+  if (P.who) {
+    for (int k = tid; k < n * n; k += kAB) {
+      const int v = k / n, jj = k - v * n;
+      const int w = T[v * TS + jj];
+      P.who[(size_t)b * n * n + k] = (w >= n) ? (uint16_t)0xFFFF : (uint16_t)w;
+    }
+  }
+  __syncthreads();
+  stamp_phase(P, b, tid, 5);
+
+  // ---------------- hand-off to the control kernels --------------------------
+  // Each vehicle's adopted inverse assignment (formation point -> vehicle):
+  // one shared row when every vehicle adopts the same one (all tables valid
+  // and identical, or none valid), else one row per vehicle.
+  {
+    const int ninv = misc[M_NINV];
+    const bool allvalid = ninv == 0;
+    const bool uniform = (allvalid && misc[M_AGREE]) || ninv == n;
+    uint16_t* wsPt = reinterpret_cast<uint16_t*>(P.ws + P.W.pt) + (size_t)b * n;
+    if (tid == 0) P.ws[P.W.mode + b] = uniform ? 0 : 1;
+    if (uniform) {
+      for (int jj = tid; jj < n; jj += kAB) wsPt[jj] = allvalid ? T[jj] : Ptin[jj];
+    } else {
+      uint16_t* rows = reinterpret_cast<uint16_t*>(P.ws + P.W.rows) + (size_t)b * n * n;
+      for (int k = tid; k < n * n; k += kAB) {
+        const int v = k / n, jj = k - v * n;
+        rows[k] = validv[v] ? T[v * TS + jj] : Ptin[jj];
+      }
+    }
+    if (tid == 0) {
+      acl_swarm_status_t st = {};
+      uint32_t fl = 0;
+      if (allvalid) fl |= ACL_SWARM_VALID;
+      if (misc[M_AGREE]) fl |= ACL_SWARM_AGREE;
+      if (misc[M_CHANGED]) fl |= ACL_SWARM_CHANGED;
+      if (nonfinite) fl |= ACL_SWARM_NONFINITE;
+      const double g = nonfinite ? 0.0 : __longlong_as_double((long long)*margw);
+      if (g < ACL_FRAGILE_MARGIN) fl |= ACL_SWARM_FRAGILE;
+      st.flags = fl;
+      st.eff_rounds = (uint16_t)eff;
+      st.rounds = (uint16_t)(2 * n);
+      st.n_invalid = (uint16_t)ninv;
+      st.margin = (float)g;
+      P.status[b] = st;
+    }
+  }
+  stamp_phase(P, b, tid, 6);
+}
+
+hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream) {
+  const ALayout L = make_alayout(P.n);
+  static bool configured = false;
+  if (!configured) {
+    for (const void* k : {(const void*)auction_kernel<1>, (const void*)auction_kernel<2>}) {
+      const hipError_t e =
+          hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+    }
+    configured = true;
+  }
+  if (P.n <= 64)
+    hipLaunchKernelGGL(auction_kernel<1>, dim3(nb), dim3(kAB), L.total, stream, P);
+  else
+    hipLaunchKernelGGL(auction_kernel<2>, dim3(nb), dim3(kAB), L.total, stream, P);
+  return hipGetLastError();
+}
+
+}  // namespace acl_amd

@@ -126,6 +126,9 @@ enum { CTL_PREP = 1, CTL_RESET = 2 };
 acl_status_t run_control(const acl_formations_t* F, const acl_control_args_t* a, hipStream_t s,
                          int flags);
 
+// The n <= 128 auction kernel (auction.hip).
+hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream);
+
 // The n > 128 auction kernel (solve_wide.hip).
 hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream);
 

@@ -34,6 +34,7 @@
 // CPU restatement (oracle/).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -756,6 +757,17 @@ extern "C" int acl_internal_kernel_times(double* ms, int* count) {
   return 0;
 }
 
+// ACLSWARM_AMD_AUCTION=old selects the previous LDS auction kernel
+// (solve_kernel) for n <= 128 (diagnostic A/B switch; read once).
+static bool auction_v2_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("ACLSWARM_AMD_AUCTION");
+    on = (e && e[0] == 'o') ? 0 : 1;
+  }
+  return on != 0;
+}
+
 // The batch runs as three stream-ordered launches: the auction kernel over
 // all B swarms (solve_kernel for n <= 128, tables in LDS; solve_wide_kernel
 // for n <= 512, tables in the workspace), the gain kernel, and the
@@ -793,7 +805,9 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   kt_record(0, 0, s);
-  if (n <= kMaxN) {
+  if (n <= kMaxN && auction_v2_enabled()) {
+    e = launch_auction(P, a->B, s);
+  } else if (n <= kMaxN) {
     static int configured = 0;
     if (!configured) {
       if (hipFuncSetAttribute((const void*)solve_kernel,

@@ -16,44 +16,44 @@
 
 namespace acl_amd {
 
-// apply_rotation_in_the_plane(row p, row q, (c,s)) on a column-major 2x2
-// (MatrixBase::applyOnTheLeft); the c==1 && s==0 early return is kept.
+// apply_rotation_in_the_plane on the pair (x, y): x' = c x + s y,
+// y' = -s x + c y, with Eigen's early return for (c, s) == (1, 0) kept as a
+// select (the unrotated values, -0.0 and NaN included): branch-free, so the
+// sweep keeps one copy of W, U, V in registers.
+__device__ __forceinline__ void rot_pair(double& x, double& y, double c, double s, bool id) {
+  const double xn = c * x + s * y;
+  const double yn = -s * x + c * y;
+  x = id ? x : xn;
+  y = id ? y : yn;
+}
+
+// MatrixBase::applyOnTheLeft(p, q, (c, s)) on a column-major 2x2: rows p, q
 __device__ __forceinline__ void rot_rows(double* W, int p, int q, double c, double s) {
-  if (c == 1.0 && s == 0.0) return;
+  const bool id = c == 1.0 && s == 0.0;
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const double xi = W[p + 2 * k], yi = W[q + 2 * k];
-    W[p + 2 * k] = c * xi + s * yi;
-    W[q + 2 * k] = -s * xi + c * yi;
-  }
+  for (int k = 0; k < 2; ++k) rot_pair(W[p + 2 * k], W[q + 2 * k], c, s, id);
 }
 
-// apply_rotation_in_the_plane(col p, col q, (c,s)) (applyOnTheRight).
+// applyOnTheRight(p, q, (c, s)): columns p, q
 __device__ __forceinline__ void rot_cols(double* M, int p, int q, double c, double s) {
-  if (c == 1.0 && s == 0.0) return;
+  const bool id = c == 1.0 && s == 0.0;
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const double xi = M[k + 2 * p], yi = M[k + 2 * q];
-    M[k + 2 * p] = c * xi + s * yi;
-    M[k + 2 * q] = -s * xi + c * yi;
-  }
+  for (int k = 0; k < 2; ++k) rot_pair(M[k + 2 * p], M[k + 2 * q], c, s, id);
 }
 
-// JacobiRotation::makeJacobi(x, y, z), real case.
+// JacobiRotation::makeJacobi(x, y, z), real case; the deno < DBL_MIN early
+// return (identity) as a select.
 __device__ __forceinline__ void make_jacobi(double x, double y, double z, double& c, double& s) {
   const double deno = 2.0 * fabs(y);
-  if (deno < DBL_MIN) {
-    c = 1.0;
-    s = 0.0;
-    return;
-  }
+  const bool tiny = deno < DBL_MIN;
   const double tau = (x - z) / deno;
   const double w = sqrt(tau * tau + 1.0);
   const double t = (tau > 0.0) ? 1.0 / (tau + w) : 1.0 / (tau - w);
   const double sign_t = t > 0.0 ? 1.0 : -1.0;
   const double n = 1.0 / sqrt(t * t + 1.0);
-  s = -sign_t * (y / fabs(y)) * fabs(t) * n;
-  c = n;
+  const double sj = -sign_t * (y / fabs(y)) * fabs(t) * n;
+  c = tiny ? 1.0 : n;
+  s = tiny ? 0.0 : sj;
 }
 
 // PartialPivLU determinant of a dynamic 2x2 (only its sign is consumed).
@@ -107,18 +107,13 @@ __device__ inline bool jacobi_svd2(const double* A, double* U, double* sv, doubl
     m[2] = W[1];
     m[1] = W[2];
     m[3] = W[0];
-    double c1, s1;
     const double t = m[0] + m[3];
     const double d = m[1] - m[2];
-    if (fabs(d) < DBL_MIN) {
-      s1 = 0.0;
-      c1 = 1.0;
-    } else {
-      const double u = t / d;
-      const double tmp = sqrt(1.0 + u * u);
-      s1 = 1.0 / tmp;
-      c1 = u / tmp;
-    }
+    const bool dz = fabs(d) < DBL_MIN;
+    const double u = t / d;
+    const double tmp = sqrt(1.0 + u * u);
+    const double s1 = dz ? 0.0 : 1.0 / tmp;
+    const double c1 = dz ? 1.0 : u / tmp;
     rot_rows(m, 0, 1, c1, s1);
     double cr, sr;
     make_jacobi(m[0], m[2], m[3], cr, sr);
