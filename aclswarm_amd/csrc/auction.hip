@@ -1,12 +1,12 @@
 // auction.hip -- the LDS-resident batched auction for n <= 128 (gfx950).
 //
 // One workgroup (512 threads = 8 wave64) owns one swarm for the whole
-// auction; every per-swarm table lives in LDS (~53 KB at n = 100, three
-// swarms per CU):
+// auction; every per-swarm table lives in LDS (51.4 KiB at n = 100: three
+// swarms per CU -- 53 KiB did not fit three after allocation rounding):
 //
 //   phase 0  load p, the adjacency bits, P_in (permutation check), q in
 //            formation order; vehicle-space closed neighbourhoods and their
-//            transpose (`listeners`); the alignment work list
+//            the alignment work list
 //   phase 1  2-D Umeyama alignment (Auctioneer::alignFormation,
 //            auctioneer.cpp:347-415). A vehicle's alignment depends only on
 //            its closed formation neighbourhood N[P[v]] (the formation-ordered
@@ -25,9 +25,9 @@
 //            updateTaskAssignment), one wave per column, lanes = vehicles.
 //            A column is resolved level by level: the highest price level of
 //            the column, its holders H (ballot) and `who`; vehicle v takes it
-//            iff H meets N(v) -- a listeners row when |H| = 1, the holders
-//            themselves when every open vehicle holds it, else a per-lane mask
-//            test -- and the next level it meets is its runner-up (decision
+//            iff H meets N(v) (a per-lane mask test: vector work, since the
+//            scalar unit is the kernel's busiest) and the next level it meets
+//            is its runner-up (decision
 //            margin). Ties, NaN and vehicles no tracked level resolves take
 //            the exact ordered scan. Then outbid vehicles re-select
 //            (selectTaskAssignment) as wave argmaxes. Exact fixed-point exit.
@@ -64,7 +64,7 @@ struct ALayout {
   int C, pq, adjF, items;
   int A, p, qf, out;
   int T, TS;
-  int vadj, lst, Pin, Ptin, itm, valid, H, misc, total;
+  int vadj, Pin, Ptin, itm, valid, H, misc, total;
 };
 
 __host__ __device__ inline ALayout make_alayout(int n) {
@@ -74,11 +74,11 @@ __host__ __device__ inline ALayout make_alayout(int n) {
   L.C = o;
   {
     const int csz = (n + 1) * n * 4;
-    const int pre = a16(n * 32) + a16(n * 16) + a16(n);
+    const int pre = a16((n + 8) * 32) + a16(n * 16) + a16(n);
     o = a16(o + (csz > pre ? csz : pre));
   }
-  L.pq = L.C;                      // [n] {p.x, p.y, qf.x, qf.y} f64
-  L.adjF = L.pq + a16(n * 32);     // [n][2] u64 formation rows (no diagonal)
+  L.pq = L.C;                      // [n + 8] {p.x, p.y, qf.x, qf.y} f64 (padded)
+  L.adjF = L.pq + a16((n + 8) * 32);  // [n][2] u64 formation rows (no diagonal)
   L.items = L.adjF + a16(n * 16);  // [n] u8 alignment work list (rows)
   L.A = o;
   L.p = o;    o = a16(o + n * 24);
@@ -87,7 +87,6 @@ __host__ __device__ inline ALayout make_alayout(int n) {
   L.T = L.A;
   if (L.A + n * L.TS > o) o = a16(L.A + n * L.TS);
   L.vadj = o;  o = a16(o + n * 16);  // [v][2] closed neighbourhood of vehicle v
-  L.lst = o;   o = a16(o + n * 16);  // [h][2] vehicles whose neighbourhood holds h
   L.Pin = o;   o = a16(o + n);
   L.Ptin = o;  o = a16(o + n);
   L.itm = o;   o = a16(o + n);       // work item of formation row i
@@ -116,30 +115,30 @@ __device__ __forceinline__ void load4(const double* pq, int j, double (&v)[4]) {
 }
 
 // For j = 0 .. n-1 in order: f(mask, pq[j]) with mask = the lanes whose
-// neighbourhood bits r hold j. pq[j] is a broadcast read issued one term
-// ahead (ping-pong buffers, so no register copies wait on it).
+// neighbourhood bits r hold j. pq[j] is a broadcast read issued four terms
+// ahead (a ring of four buffers: the reads' latency, not the adds, would
+// otherwise set the pace of the sequential sums). pq is padded to n + 4
+// entries; terms past n have an empty mask (exec = 0: no lane adds).
 template <int NC, typename F>
 __device__ __forceinline__ void for_members(int n, const double* pq,
                                             const unsigned long long (&r)[2], F&& f) {
-  double A[4], B[4];
-  load4(pq, 0, A);
-#pragma unroll
-  for (int w = 0; w < NC; ++w) {
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      const unsigned word = (unsigned)(r[w] >> (32 * hf));
-      const int j0 = 64 * w + 32 * hf;
+  double R0[4], R1[4], R2[4], R3[4];
+  load4(pq, 0, R0);
+  load4(pq, 1, R1);
+  load4(pq, 2, R2);
+  load4(pq, 3, R3);
 #pragma unroll 1
-      for (int x = 0; x < 32; x += 2) {
-        const int j = j0 + x;
-        if (j >= n) break;
-        load4(pq, j + 1 < n ? j + 1 : j, B);
-        f(__ballot(word & (1u << x)), A);
-        if (j + 1 >= n) break;
-        load4(pq, j + 2 < n ? j + 2 : j + 1, A);
-        f(__ballot(word & (2u << x)), B);
-      }
-    }
+  for (int j = 0; j < n; j += 4) {
+    const unsigned long long w = j < 64 ? r[0] : r[1];
+    const unsigned long long bits = w >> (j & 63);  // j % 4 == 0: four bits in one word
+    f(__ballot(bits & 1ull), R0);
+    load4(pq, j + 4, R0);
+    f(__ballot(bits & 2ull), R1);
+    load4(pq, j + 5, R1);
+    f(__ballot(bits & 4ull), R2);
+    load4(pq, j + 6, R2);
+    f(__ballot(bits & 8ull), R3);
+    load4(pq, j + 7, R3);
   }
 }
 
@@ -257,16 +256,13 @@ __device__ __forceinline__ unsigned level_key(const unsigned (&key)[NC], unsigne
 }
 
 // vehicles (lane masks of `open`) whose closed neighbourhood holds a level
-// held by h (nh holders, the first hl): the listeners row of hl when it is
-// the only holder; the open vehicles themselves when all of them hold it
-// (v is in N(v)); otherwise a per-lane mask test
+// held by h
 template <int NC>
 __device__ __forceinline__ void level_hits(const unsigned long long (&open)[NC],
                                            const unsigned long long (&h)[NC],
                                            const unsigned long long (&vm)[NC][NC],
                                            unsigned long long (&hitm)[NC]) {
-  // a per-lane mask test (vector work; the scalar unit is the kernel's
-  // bottleneck, so no branches on the holder set)
+  // a per-lane mask test (no branches on the holder set)
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     unsigned long long t = 0ull;
@@ -343,7 +339,6 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   double* out = reinterpret_cast<double*>(smem + L.out);
   unsigned char* T = smem + L.T;
   unsigned long long* vadj = reinterpret_cast<unsigned long long*>(smem + L.vadj);
-  unsigned long long* lst = reinterpret_cast<unsigned long long*>(smem + L.lst);
   unsigned char* Pin = smem + L.Pin;
   unsigned char* Ptin = smem + L.Ptin;
   unsigned char* itm = smem + L.itm;
@@ -434,8 +429,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     }
   }
   // closed neighbourhoods in vehicle space (bidIterComplete, auctioneer.cpp:
-  // 419-437): u ~ v iff u == v or adj(P[v], P[u]); and the transpose
-  // lst[h] = {v : h in N(v)} (u ~ v with the roles swapped)
+  // 419-437): u ~ v iff u == v or adj(P[v], P[u])
   {
     int pu[NC];
 #pragma unroll
@@ -448,18 +442,10 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         const int u = lane + 64 * c;
         const bool okl = u < n;
         const bool e = okl && (u == v || (((pu[c] < 64 ? r0 : r1) >> (pu[c] & 63)) & 1ull));
-        const unsigned long long ru = adjF[2 * pu[c] + (i >> 6)];
-        const bool t = okl && (u == v || ((ru >> (i & 63)) & 1ull));
-        const unsigned long long me = __ballot(e), mt = __ballot(t);
-        if (lane == 0) {
-          vadj[2 * v + c] = me;
-          lst[2 * v + c] = mt;
-        }
+        const unsigned long long me = __ballot(e);
+        if (lane == 0) vadj[2 * v + c] = me;
       }
-      if (NC == 1 && lane == 0) {
-        vadj[2 * v + 1] = 0ull;
-        lst[2 * v + 1] = 0ull;
-      }
+      if (NC == 1 && lane == 0) vadj[2 * v + 1] = 0ull;
     }
   }
   // alignment work list (wave 0): incomplete rows ascending, then one row

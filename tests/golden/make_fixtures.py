@@ -22,7 +22,8 @@ Fixtures (all data -- inputs and expected outputs):
   admm_test_admm.json    the two n=4 MATLAB goldens of
                      aclswarm/test/test_admm.cpp:26-37,64-75 with their inputs.
 
-Usage: python tests/golden/make_fixtures.py
+Usage: python tests/golden/make_fixtures.py [simform set names ...]
+  (no names: every fixture; names: only those simform sets)
 """
 import json
 import os
@@ -160,16 +161,27 @@ def admm_test_fixture():
                  "adj": adj_nc, "A": noncomplete}]}
 
 
+SETS = [
+    ("simform20_fc", 20, True, 15.0, range(0, 8)),
+    ("simform20_nc", 20, False, 15.0, range(0, 8)),
+    ("simform100_nc", 100, False, 40.0, range(0, 4)),
+    ("simform500_nc", 500, False, 90.0, range(0, 2)),
+]
+
+
 def main():
     grf, assignment = _import_reference_modules()
+    only = sys.argv[1:]
+    if only:
+        for name, n, fc, L, seeds in SETS:
+            if name in only:
+                d = simform_fixture(grf, n, fc, L, list(seeds))
+                np.savez_compressed(os.path.join(OUT, name + ".npz"), **d)
+                print("wrote", name)
+        return
     with open(os.path.join(OUT, "swarm6_3d.json"), "w") as f:
         json.dump(swarm6_fixture(), f)
-    sets = [
-        ("simform20_fc", 20, True, 15.0, range(0, 8)),
-        ("simform20_nc", 20, False, 15.0, range(0, 8)),
-        ("simform100_nc", 100, False, 40.0, range(0, 4)),
-    ]
-    for name, n, fc, L, seeds in sets:
+    for name, n, fc, L, seeds in SETS:
         d = simform_fixture(grf, n, fc, L, list(seeds))
         np.savez_compressed(os.path.join(OUT, name + ".npz"), **d)
     with open(os.path.join(OUT, "arun_golden.json"), "w") as f:

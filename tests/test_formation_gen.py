@@ -28,7 +28,7 @@ def test_mt19937_stream_matches_numpy_randomstate(seed):
     assert mt.uniform(0.0, 1.0) == rs.uniform(0.0, 1.0)
 
 
-@pytest.mark.parametrize("name", ["simform20_fc", "simform20_nc", "simform100_nc"])
+@pytest.mark.parametrize("name", ["simform20_fc", "simform20_nc", "simform100_nc", "simform500_nc"])
 def test_generator_reproduces_reference_fixtures(name):
     d = np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"))
     n, fc, L, h, md = int(d["n"]), bool(d["fc"]), float(d["L"]), float(d["h"]), float(d["min_dist"])

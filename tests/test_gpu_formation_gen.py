@@ -24,7 +24,7 @@ def _gen(seeds, n, fc, l, w, h, md=2.0, maxc=0):
     return {k: v.cpu().numpy() for k, v in out.items()}
 
 
-@pytest.mark.parametrize("name", ["simform20_fc", "simform20_nc", "simform100_nc"])
+@pytest.mark.parametrize("name", ["simform20_fc", "simform20_nc", "simform100_nc", "simform500_nc"])
 def test_generator_matches_reference_fixtures(cuda, name):
     d = np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"))
     n, fc, L, h, md = int(d["n"]), bool(d["fc"]), float(d["L"]), float(d["h"]), float(d["min_dist"])

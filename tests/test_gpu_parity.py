@@ -106,6 +106,34 @@ def test_simform20(cuda, name):
     _compare(gpu, ref)
 
 
+def test_c2_full_batch(cuda):
+    """Config C2 at its full size: B = 4096 swarms on the 16 simform20_fc
+    formations, every swarm against the CPU restatement's batch entry point
+    (assignments, status and margin bit-exact, commands 1e-5)."""
+    P, A = H.simform("simform20_fc")
+    rng = np.random.RandomState(4096)
+    pts = [P[s, k] for s in range(P.shape[0]) for k in range(2)]
+    adjs = [A[s] for s in range(P.shape[0]) for k in range(2)]
+    gains = [H.synth_gains(rng, a) for a in adjs]
+    B, n = 4096, 20
+    fidx = (np.arange(B) % len(pts)).astype(np.int32)
+    q = np.stack([H.random_positions(rng, n, 20.0) for _ in range(B)])
+    vel = rng.normal(0, 0.2, (B, n, 3))
+    P_in = np.stack([H.random_perm(rng, n) if b % 2 else np.arange(n, dtype=np.uint16)
+                     for b in range(B)])
+    gpu = _gpu_solve(pts, adjs, gains, fidx, q, vel, P_in)
+    ref, _ = O.solve_batch(fidx, q, vel, np.stack(pts), np.stack(adjs), np.stack(gains), P_in,
+                           nthreads=8)
+    np.testing.assert_array_equal(gpu["P_out"], ref["P_out"])
+    for k in ("flags", "eff_rounds", "rounds", "n_invalid", "n_ca"):
+        np.testing.assert_array_equal(gpu["status"][k], ref["status"][k], err_msg=k)
+    np.testing.assert_array_equal(gpu["status"]["margin"], ref["status"]["margin"])
+    np.testing.assert_array_equal(gpu["ca_flag"], ref["ca"])
+    for k in ("u", "u_safe"):
+        err = np.abs(gpu[k] - ref[k]) / np.maximum(np.abs(ref[k]), 1.0)
+        assert err.max() <= U_RTOL, (k, err.max())
+
+
 def test_simform100(cuda):
     """Config C3 shape (n=100 noncomplete, L=40 generator formations)."""
     P, A = H.simform("simform100_nc")
@@ -268,14 +296,48 @@ def test_wide_collision_avoidance(cuda):
     _compare(gpu, ref)
 
 
+def _c4_inputs(B, seed):
+    """Config C4: simform500 formations (N=500, L=90, the reference generator's
+    own output, tests/golden/simform500_nc.npz), u16 indices."""
+    P, A = H.simform("simform500_nc")
+    rng = np.random.RandomState(seed)
+    pts = [P[s, k] for s in range(P.shape[0]) for k in range(2)]
+    adjs = [A[s] for s in range(P.shape[0]) for k in range(2)]
+    gains = [H.synth_gains(rng, a) for a in adjs]
+    n = 500
+    fidx = np.arange(B) % len(pts)
+    q = np.stack([H.random_positions(rng, n, 20.0 * (n / 20.0) ** 0.5) for _ in range(B)])
+    vel = rng.normal(0, 0.1, (B, n, 3))
+    P_in = np.stack([H.random_perm(rng, n) if b % 2 else np.arange(n, dtype=np.uint16)
+                     for b in range(B)])
+    return pts, adjs, gains, fidx, q, vel, P_in
+
+
 def test_n500_config_c4(cuda):
-    """Config C4 size (N=500, noncomplete; u16 indices): one swarm against the
-    CPU restatement."""
-    rng = np.random.RandomState(500)
-    args = _wide_case(rng, 500, 1, 90.0, 400)
+    """Config C4 (simform500 formations): every output of three swarms against
+    the CPU restatement (~8 s of oracle time per swarm)."""
+    args = _c4_inputs(3, 500)
     gpu = _gpu_solve(*args)
     ref = _oracle(*args)
     _compare(gpu, ref)
+
+
+def test_c4_batch_sampled(cuda):
+    """C4 at a batch of 256 swarms (the tables-in-HBM kernel with many
+    workgroups in flight): every P_out a permutation, status valid, a second
+    run bit-identical, and two sampled swarms against the oracle."""
+    B = 256
+    pts, adjs, gains, fidx, q, vel, P_in = _c4_inputs(B, 501)
+    gpu = _gpu_solve(pts, adjs, gains, fidx, q, vel, P_in)
+    again = _gpu_solve(pts, adjs, gains, fidx, q, vel, P_in)
+    for k in ("P_out", "who", "u", "u_safe"):
+        np.testing.assert_array_equal(gpu[k], again[k])
+    assert (gpu["status"]["flags"] & 0x01).all()  # valid
+    srt = np.sort(gpu["P_out"].astype(np.int64), axis=1)
+    assert (srt == np.arange(500)).all()
+    for b in (17, 200):
+        ref = _oracle(pts, adjs, gains, fidx[[b]], q[[b]], vel[[b]], P_in[[b]])
+        _compare({k: v[[b]] for k, v in gpu.items()}, ref)
 
 
 def test_control_batch_given_assignment(cuda):
