@@ -10,7 +10,7 @@
 
 namespace acl_amd {
 
-constexpr int kMaxN = 128;      // LDS-resident auction kernel (solve.hip)
+constexpr int kMaxN = 128;      // LDS-resident auction kernel (auction.hip)
 constexpr int kMaxNWide = 512;  // tables-in-HBM auction kernel (solve_wide.hip)
 
 // Solve workspace (acl_solve_workspace_bytes), 256-byte aligned regions:

@@ -371,7 +371,8 @@ def main():
     gain_sym = ("acl_amd::gain_pair_kernel<%s>" % ("true" if t_tile is not None else "false")
                 if w["planes"] == 5 and os.environ.get("ACLSWARM_AMD_GAIN_PAIR", "1") != "0"
                 else f"acl_amd::gain_kernel<{w['planes']}>")
-    auction_sym = "acl_amd::solve_kernel" if n <= 128 else "acl_amd::solve_wide_kernel"
+    auction_sym = ("acl_amd::auction_kernel<%d>" % (1 if n <= 64 else 2) if n <= 128
+                   else "acl_amd::solve_wide_kernel")
     kern = {}
     for k, (name, sym) in enumerate((("auction", auction_sym), ("gain", gain_sym),
                                      ("ca", "acl_amd::ca_kernel"))):
@@ -388,6 +389,15 @@ def main():
     iss, isrc = committed_profile("pmc_auction", n, B, auction_sym)
     if iss:
         kern["auction"]["issue"] = dict(iss, source=isrc)
+        # the auction's own roofline: its busiest issue port (SQ counters of
+        # the same configuration, scaled to this run's kernel time)
+        ports = {p: iss[p + "_issue_frac"] * iss_ms / kern["auction"]["avg_launch_ms"]
+                 for p in ("salu", "valu", "lds") if p + "_issue_frac" in iss
+                 for iss_ms in [iss.get("kernel_ms") or kern["auction"]["avg_launch_ms"]]}
+        if ports:
+            top = max(ports, key=ports.get)
+            kern["auction"]["roofline"] = {"bound": top + "-issue", "frac": ports[top],
+                                           "ports": ports, "source": isrc}
     pipe_bytes = a_all + g_all + s_all
     pipe_ach = pipe_bytes / (call_ms * 1e-3) / 1e9
     gk = kern["gain"]

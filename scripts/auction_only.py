@@ -13,12 +13,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--B", type=int, default=8192)
 ap.add_argument("--n", type=int, default=100)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--L", type=float, default=None, help="generator area (default: the bench config's)")
+ap.add_argument("--complete", action="store_true", help="complete formation graphs (config C2)")
 ap.add_argument("--control", action="store_true", help="run the control kernels too")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 gen = torch.Generator(device=dev)
 gen.manual_seed(1)
-w = workload.simform_workload(a.B, a.n, gen, dev)
+w = workload.simform_workload(a.B, a.n, gen, dev, L=a.L, complete=a.complete)
 T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"],
                               w["planes"])
 engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=a.control)  # warm

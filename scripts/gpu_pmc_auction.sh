@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counters of the auction kernel alone (instruction mix, stalls), one
 # rocprofv3 pass per counter group, counters only. OUT=<dir under gpurun_out>
-# (default pmca); ACLSWARM_AMD_AUCTION=old profiles the previous kernel.
+# (default pmca).
 set -o pipefail
 cd /root/repo
 export TMPDIR=/tmp

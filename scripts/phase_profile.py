@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase cycle shares of solve_kernel (s_memtime stamps
+"""Diagnostic: per-phase cycle shares of the auction kernel (s_memtime stamps
 written by thread 0 of each workgroup at the end of every phase), on the
 bench workload. Uses the library's internal hook acl_internal_set_stamps."""
 import argparse
