@@ -132,10 +132,14 @@ def cpu_baseline(w, out, budget_s, nthreads):
         Pin = w["P_in"][idx].cpu().numpy().view(np.uint16)
         return inv.astype(np.int32), q, vel, pts, adj, G, Pin
 
+    def note(msg):  # progress on stderr (a long CPU leg must not look hung)
+        print(f"[bench] cpu_baseline: {msg}", file=sys.stderr, flush=True)
+
     Btot = w["q"].shape[0]
-    # calibrate on a few swarms, then size the samples to the time budget
-    cal = torch.arange(min(2 * nthreads, Btot))
+    # calibrate on one swarm per thread, then size the samples to the time budget
+    cal = torch.arange(min(nthreads, Btot))
     args = gather(cal)
+    note(f"calibrating on {len(cal)} swarms")
     _, t = O.solve_batch(*args, nthreads=nthreads, early_exit=False, margin=False)
     per = t / len(cal)
     S = int(max(len(cal), min(4096, 0.6 * budget_s / max(per, 1e-6))))
@@ -144,11 +148,14 @@ def cpu_baseline(w, out, budget_s, nthreads):
     args = gather(idx)
     # timed: the reference's work (literal 2N rounds, no margin bookkeeping);
     # the fixed-point-exit run carries the margin for the parity check
+    note(f"{S} swarms, literal 2N rounds, {nthreads} threads")
     res, t_lit = O.solve_batch(*args, nthreads=nthreads, early_exit=False, margin=False)
+    note(f"{S} swarms, fixed-point exit with margins")
     res_ee, t_ee = O.solve_batch(*args, nthreads=nthreads, early_exit=True)
     # one core: a smaller sample of the same swarms
     S1 = int(max(1, min(S, 0.25 * budget_s / max(per * nthreads, 1e-6))))
     a1 = gather(torch.arange(S1))
+    note(f"{S1} swarms on 1 thread")
     _, t1 = O.solve_batch(*a1, nthreads=1, early_exit=False, margin=False)
     # parity of the sample (GPU ran with the exact fixed-point exit)
     gP = out["P_out"][idx].cpu().numpy().view(np.uint16)
