@@ -22,6 +22,7 @@ FLAG_CHANGED = 0x04
 FLAG_NONFINITE = 0x08
 FLAG_BAD_INPUT = 0x10
 FLAG_CA_ACTIVE = 0x20
+ABI_VERSION = 3  # include/aclswarm_amd.h ACL_ABI_VERSION
 FLAG_FRAGILE = 0x40
 FRAGILE_MARGIN = 1e-6
 
@@ -32,7 +33,7 @@ STATUS_DTYPE = np.dtype([("flags", "<u4"), ("eff_rounds", "<u2"),
 # every symbol include/aclswarm_amd.h declares
 EXPORTS = (
     "acl_default_cntrl_gains", "acl_default_safety_params", "acl_default_admm_params",
-    "acl_formations_init", "acl_max_vehicles", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
+    "acl_formations_init", "acl_max_vehicles", "acl_abi_version", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
     "acl_pack_gains", "acl_gain_planes", "acl_pack_gains_planes", "acl_tile_gains", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
     "acl_control_batch", "acl_write_assignment_log", "acl_read_assignment_log",
     "acl_hungarian_batch",
@@ -149,6 +150,10 @@ def lib():
     L.acl_formations_init.argtypes = [ct.POINTER(Formations), I32, I32]
     L.acl_formations_init.restype = None
     L.acl_max_vehicles.restype = I32
+    L.acl_abi_version.restype = I32
+    if L.acl_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"aclswarm_amd: {LIB_PATH} has ABI {L.acl_abi_version()}, this "
+                           f"package expects {ABI_VERSION}: rebuild (python -m aclswarm_amd.build)")
     L.acl_solve_workspace_bytes.argtypes = [I32, I32]
     L.acl_solve_workspace_bytes.restype = ct.c_size_t
     L.acl_solve_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(SolveArgs), VP]

@@ -250,3 +250,5 @@ extern "C" acl_status_t acl_memset(void* dst, int value, size_t bytes, void* str
 extern "C" acl_status_t acl_stream_synchronize(void* stream) {
   return hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
 }
+
+extern "C" int32_t acl_abi_version(void) { return ACL_ABI_VERSION; }

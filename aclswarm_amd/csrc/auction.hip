@@ -166,6 +166,20 @@ __device__ __forceinline__ void stamp_phase(const SolveParams& P, int b, int tid
   if (P.stamps && tid == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
 }
 
+// diagnostic builds (-DACL_AUCTION_NO_MARGIN): the CBAA rounds skip the
+// decision-margin bookkeeping (a cost measurement only; margins then wrong)
+#ifndef ACL_AUCTION_NO_MARGIN
+#define ACL_AUCTION_NO_MARGIN 0
+#endif
+
+// margin_gap of a (hi, lo) pair (common.h margin_gap)
+__device__ __forceinline__ double margin_gap_pair(float hi, float lo) {
+  MarginPair m;
+  m.hi = hi;
+  m.lo = lo;
+  return margin_gap(m);
+}
+
 // margin_track on a wave-uniform pair, branch-free (selects)
 __device__ __forceinline__ void margin_track_u(float& hi, float& lo, float h, float l) {
   const bool tie = l == h;
@@ -355,7 +369,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
   MarginPair mp;
   margin_init(mp);
-  double galign = 1.0;
+  double galign = 1.0;  // this lane's alignment gap (phase 1)
   stamp_phase(P, b, tid, 0);
 
   // ---------------- phase 0: load ------------------------------------------
@@ -542,6 +556,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
       }
     }
+    // the alignments' gaps go into the swarm margin now: the CBAA rounds
+    // prune their margin work against it (below)
+    block_min_gap(margw, galign);
   }
   __syncthreads();
   stamp_phase(P, b, tid, 2);
@@ -624,6 +641,11 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   const int max_rounds = 2 * n;  // cbaa_max_iter_ = n * diameter (:50-51)
   for (int r = 1; r <= max_rounds; ++r) {
     const int par = r & 1, npar = par ^ 1;
+    // the swarm's smallest gap published so far (alignments, and every
+    // wave's evaluations up to the last round): an evaluation whose gap is
+    // bounded below by it cannot lower the margin, so its runner-up walk is
+    // skipped (margin_gap is monotone in the pair's ratio)
+    const double Gpub = __longlong_as_double((long long)*margw);
     // this wave's dirty columns: every 8th set bit in rank order
     unsigned long long mine[NC];
     {
@@ -714,7 +736,8 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           if (!left || ++k == kAL) break;
           // the next level
           Mk = level_key<NC>(key, Mk);
-          margin_track_u(bhi, blo, __uint_as_float(kres - 1u), __uint_as_float(Mk - 1u));
+          if (!ACL_AUCTION_NO_MARGIN)
+            margin_track_u(bhi, blo, __uint_as_float(kres - 1u), __uint_as_float(Mk - 1u));
           // (kres == 0 or Mk == 0: a pair with lo > hi or lo == 0, no effect
           // -- except kres == 0 == Mk, a tie of two -0.0f... excluded below)
 #pragma unroll
@@ -727,14 +750,15 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
 #pragma unroll
           for (int c = 0; c < NC; ++c) tie |= h[c] & __ballot(wu[c] != wk);
         }
-        if (kres != 0u && cum < n) {  // the resolving level's successor
+        if (!ACL_AUCTION_NO_MARGIN && kres != 0u && cum < n) {  // the resolving level's successor
           const unsigned Mn = level_key<NC>(key, kres);
           margin_track_u(bhi, blo, __uint_as_float(kres - 1u), __uint_as_float(Mn - 1u));
         }
         // the exact runner-ups only where the bound could lower the wave's
         // running minimum (an evaluation skipped here has a gap >= the bound
         // >= a gap already tracked, so the minimum is unchanged)
-        if ((double)blo * (double)uhi > (double)ulo * (double)bhi)
+        if (!ACL_AUCTION_NO_MARGIN && (double)blo * (double)uhi > (double)ulo * (double)bhi &&
+            margin_gap_pair(bhi, blo) < Gpub)
           runner_up_walk<NC>(n, key, k1, Nd, vm, uhi, ulo);
         // the exact ordered scan (ascending vehid, strict >) for ties, NaN
         // prices and vehicles the levels did not resolve; the runner-up is the
@@ -790,6 +814,12 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         if (ch && lane == 0) atomicOr(&dmask[2 * npar + (j >> 6)], 1ull << (j & 63));
       }
     }
+    {
+      // publish this wave's smallest gap so far (its lanes' select and scan
+      // evaluations, its level pair) for the next round's pruning
+      const double gl = margin_gap(mp), gu = margin_gap_pair(uhi, ulo);
+      block_min_gap(margw, gl < gu ? gl : gu);
+    }
     __syncthreads();
     // outbid vehicles re-select on their updated rows (auctioneer.cpp:224)
     {
@@ -825,10 +855,10 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   }
   stamp_phase(P, b, tid, 4);
   ACL_AUCTION_STOP_AT(5);
-  {  // swarm margin: every lane's pair, the wave's level pair, the alignments
+  {  // swarm margin: every lane's pair and the wave's level pair (the
+     // alignments' gaps are in already)
     margin_track(mp, uhi, ulo);
-    const double gc = margin_gap(mp);
-    block_min_gap(margw, gc < galign ? gc : galign);
+    block_min_gap(margw, margin_gap(mp));
   }
 
   // ---------------- phase 4: adoption ---------------------------------------

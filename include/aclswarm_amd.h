@@ -269,6 +269,10 @@ typedef struct {
 /* Largest n acl_solve_batch accepts (512). */
 int32_t acl_max_vehicles(void);
 
+/* ACL_ABI_VERSION of the built library (a binding checks it at load time:
+ * the status record and argument structs change between versions). */
+int32_t acl_abi_version(void);
+
 /* Bytes of device workspace acl_solve_batch needs for B swarms of n. */
 size_t acl_solve_workspace_bytes(int32_t n, int32_t B);
 
