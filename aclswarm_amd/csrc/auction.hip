@@ -715,40 +715,56 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         }
         unsigned Mk = M0, kres = 0u;  // kres: the last level that resolved a vehicle
         float bhi = 1.0f, blo = 0.0f;  // bound pair (largest ratio)
+        if (nonfinite) {  // NaN prices: the exact scan for every vehicle
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            Nd[c] = U[c];
+            U[c] = 0ull;
+          }
+        } else {
 #pragma unroll 1
-        for (int k = 0;;) {
-          const bool tk = nonfinite || tie != 0ull;
-          unsigned long long hitm[NC];
-          level_hits<NC>(U, h, vm, hitm);
-          const unsigned kv = tk ? 0u : Mk;
-          unsigned long long left = 0ull, res = 0ull;
+          for (int k = 0;;) {
+            if (tie) {
+              // a level held under two `who`s (equal prices): the exact scan
+              // for every vehicle not resolved above it (rare; the bound of
+              // the last resolving level was taken against this level)
 #pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            const bool hit = lanebit(hitm[c]);
-            nw[c] = hit ? wk : nw[c];
-            k1[c] = hit ? kv : k1[c];
-            Nd[c] |= tk ? hitm[c] : 0ull;
-            U[c] &= ~hitm[c];
-            left |= U[c];
-            res |= hitm[c];
+              for (int c = 0; c < NC; ++c) {
+                Nd[c] = U[c];
+                U[c] = 0ull;
+              }
+              kres = 0u;
+              break;
+            }
+            unsigned long long hitm[NC];
+            level_hits<NC>(U, h, vm, hitm);
+            unsigned long long left = 0ull, res = 0ull;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+              const bool hit = lanebit(hitm[c]);
+              nw[c] = hit ? wk : nw[c];
+              k1[c] = hit ? Mk : k1[c];
+              U[c] &= ~hitm[c];
+              left |= U[c];
+              res |= hitm[c];
+            }
+            kres = res ? Mk : 0u;
+            if (!left || ++k == kAL) break;
+            // the next level
+            Mk = level_key<NC>(key, Mk);
+            if (!ACL_AUCTION_NO_MARGIN)
+              margin_track_u(bhi, blo, __uint_as_float(kres - 1u), __uint_as_float(Mk - 1u));
+            // (kres == 0: a NaN pair, no effect; Mk == 0: lo = NaN, no effect)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+              h[c] = __ballot(key[c] == Mk);
+              cum += __popcll(h[c]);
+            }
+            wk = first_who<NC>(h, wu);
+            tie = 0ull;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) tie |= h[c] & __ballot(wu[c] != wk);
           }
-          kres = (!tk && res) ? Mk : 0u;
-          if (!left || ++k == kAL) break;
-          // the next level
-          Mk = level_key<NC>(key, Mk);
-          if (!ACL_AUCTION_NO_MARGIN)
-            margin_track_u(bhi, blo, __uint_as_float(kres - 1u), __uint_as_float(Mk - 1u));
-          // (kres == 0 or Mk == 0: a pair with lo > hi or lo == 0, no effect
-          // -- except kres == 0 == Mk, a tie of two -0.0f... excluded below)
-#pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            h[c] = __ballot(key[c] == Mk);
-            cum += __popcll(h[c]);
-          }
-          wk = first_who<NC>(h, wu);
-          tie = 0ull;
-#pragma unroll
-          for (int c = 0; c < NC; ++c) tie |= h[c] & __ballot(wu[c] != wk);
         }
         if (!ACL_AUCTION_NO_MARGIN && kres != 0u && cum < n) {  // the resolving level's successor
           const unsigned Mn = level_key<NC>(key, kres);
