@@ -33,8 +33,10 @@ def swarm_stats(status_u8):
     c = [torch.tensor(s.shape[0], device=dev, dtype=torch.int64)]
     c += [((flags & bit) != 0).sum() for bit in FLAG_BITS]
     c += [ninv.sum(), nca.sum(), eff.sum()]
-    hist = torch.bincount(eff.clamp(max=HIST_BINS - 1), minlength=HIST_BINS)
-    counters = torch.cat([torch.stack(c), hist.to(torch.int64)])
+    # a fixed-size scatter (bincount sizes its output from the data: a host sync)
+    hist = torch.zeros(HIST_BINS, dtype=torch.int64, device=dev)
+    hist.scatter_add_(0, eff.clamp(max=HIST_BINS - 1), torch.ones_like(eff))
+    counters = torch.cat([torch.stack(c), hist])
     if eff.numel():
         ext = torch.stack([eff.max().to(torch.float64), -margin.min().to(torch.float64)])
     else:
