@@ -898,9 +898,15 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
             "hipMemcpyAsync");
     ACL_HIP(hipMemcpyAsync(dp, hp.data(), NP * sizeof(Part), hipMemcpyHostToDevice, st),
             "hipMemcpyAsync");
+    // symmetric products (exact arithmetic): G = Q Q^T, the Newton-Schulz
+    // Z^2 and Z Z^2 (polynomials in one symmetric Z commute), W sign(W)
+    auto symk = [](int kind) {
+      return kind == J_G || kind == J_NSY0 || kind == J_NSU0 || kind == J_NSY1 ||
+             kind == J_NSU1 || kind == J_S;
+    };
     auto gemm = [&](int kind, bool ta, bool tb) -> hipError_t {
       return gemm_f64(ta, tb, dj + (size_t)kind * NP, njob[kind], mx[kind][0], mx[kind][1], st,
-                      g_flops);
+                      g_flops, symk(kind) && mx[kind][0] == mx[kind][1]);
     };
     int max_s = 0, max_np = 0, maxK1 = 1;
     for (const Info& in : info) {

@@ -5,6 +5,13 @@
 // live in device memory, so a setup kernel may fill them and converged
 // problems drop out without a host round trip).
 //
+// Placement: a 1-D grid whose block b works on job (b % 8) + 8 k -- blocks
+// b and b + 8 share an XCD (blocks are dealt round-robin over the 8 XCDs), so
+// every tile of one job runs on one XCD and its operand panels are re-read
+// from that XCD's L2 instead of being fetched by all eight.
+// Symmetric jobs (SYM: D symmetric in exact arithmetic, square) compute only
+// the tiles on and above the diagonal and store each off-diagonal one twice.
+//
 // Tiling: a 64 x 64 (or 32 x 32) output tile per 256-thread workgroup, four
 // waves in a 2 x 2 arrangement, each wave 2 x 2 (1 x 1) MFMA 16x16 tiles; K staged through LDS in
 // steps of 16 with a register-prefetched double buffer (one barrier per step).
@@ -41,14 +48,28 @@ constexpr int kGemmKStep = 16;
 // TW = MFMA 16x16 tiles per wave per dimension: TW = 2 -> 64 x 64 output
 // tile per workgroup, TW = 1 -> 32 x 32 (less padding on the ADMM's 392- and
 // 196-sized products, but one accumulator per wave).
-template <bool TA, bool TB, int TW>
-__global__ void __launch_bounds__(256) gemm_f64_kernel(const GemmJob* __restrict__ jobs,
+template <bool TA, bool TB, int TW, bool SYM>
+__global__ void __launch_bounds__(256) gemm_f64_kernel(const GemmJob* __restrict__ jobs, int njobs,
+                                                          int tm, int tiles,
                                                           unsigned long long* flops) {
   constexpr int TILE = 32 * TW;
   constexpr int EPT = TILE / 16;  // operand elements each thread stages per K step
-  const GemmJob J = jobs[blockIdx.z];
+  const int blk = blockIdx.x;
+  const int slot = blk >> 3;
+  const int job = (blk & 7) + 8 * (slot / tiles);
+  if (job >= njobs) return;
+  int t = slot % tiles, bi, bj;
+  if (SYM) {  // upper-triangle tile t: row blocks bi <= bj
+    bj = 0;
+    while (t > bj) { t -= bj + 1; ++bj; }
+    bi = t;
+  } else {
+    bi = t % tm;
+    bj = t / tm;
+  }
+  const GemmJob J = jobs[job];
   if (J.skip && *J.skip) return;
-  const int m0 = blockIdx.x * TILE, n0 = blockIdx.y * TILE;
+  const int m0 = bi * TILE, n0 = bj * TILE;
   if (m0 >= J.m || n0 >= J.n) return;
   if (flops && threadIdx.x == 0)  // algorithmic flops of this tile (diagnostics)
     atomicAdd(flops, 2ull * (unsigned long long)min(TILE, J.m - m0) *
@@ -146,6 +167,7 @@ __global__ void __launch_bounds__(256) gemm_f64_kernel(const GemmJob* __restrict
           double v = alpha * acc[a][b][r];
           if (beta != 0.0) v += beta * J.C[gi + (size_t)gj * J.ldc];
           J.D[gi + (size_t)gj * J.ldd] = v;
+          if (SYM && bi != bj) J.D[gj + (size_t)gi * J.ldd] = v;
         }
       }
 }
@@ -163,24 +185,36 @@ inline int gemm_tile() {
 }
 
 // Host launcher: `jobs` is a device array of `njobs` descriptors whose m, n
-// are bounded by mmax, nmax.
+// are bounded by mmax, nmax. sym: every job's D is symmetric in exact
+// arithmetic (and square): upper-triangle tiles only, mirrored.
 inline hipError_t gemm_f64(bool ta, bool tb, const GemmJob* jobs, int njobs, int mmax, int nmax,
-                           hipStream_t s, unsigned long long* flops = nullptr) {
+                           hipStream_t s, unsigned long long* flops = nullptr, bool sym = false) {
   if (njobs <= 0 || mmax <= 0 || nmax <= 0) return hipSuccess;
   const int T = gemm_tile();
-  const dim3 grid((mmax + T - 1) / T, (nmax + T - 1) / T, njobs);
-#define ACL_GEMM_LAUNCH(TA_, TB_)                                                            \
-  do {                                                                                       \
-    if (T == 64)                                                                             \
-      hipLaunchKernelGGL((gemm_f64_kernel<TA_, TB_, 2>), grid, dim3(256), 0, s, jobs, flops); \
-    else                                                                                     \
-      hipLaunchKernelGGL((gemm_f64_kernel<TA_, TB_, 1>), grid, dim3(256), 0, s, jobs, flops); \
+  const int tm = (mmax + T - 1) / T, tn = (nmax + T - 1) / T;
+  if (sym && tm != tn) return hipErrorInvalidValue;
+  const int tiles = sym ? tm * (tm + 1) / 2 : tm * tn;
+  const dim3 grid(8 * ((njobs + 7) / 8) * tiles);
+#define ACL_GEMM_LAUNCH2(TA_, TB_, SYM_)                                                   \
+  do {                                                                                     \
+    if (T == 64)                                                                           \
+      hipLaunchKernelGGL((gemm_f64_kernel<TA_, TB_, 2, SYM_>), grid, dim3(256), 0, s, jobs, \
+                         njobs, tm, tiles, flops);                                         \
+    else                                                                                   \
+      hipLaunchKernelGGL((gemm_f64_kernel<TA_, TB_, 1, SYM_>), grid, dim3(256), 0, s, jobs, \
+                         njobs, tm, tiles, flops);                                         \
+  } while (0)
+#define ACL_GEMM_LAUNCH(TA_, TB_)                       \
+  do {                                                  \
+    if (sym) ACL_GEMM_LAUNCH2(TA_, TB_, true);          \
+    else ACL_GEMM_LAUNCH2(TA_, TB_, false);             \
   } while (0)
   if (!ta && !tb) ACL_GEMM_LAUNCH(false, false);
   else if (!ta && tb) ACL_GEMM_LAUNCH(false, true);
   else if (ta && !tb) ACL_GEMM_LAUNCH(true, false);
   else ACL_GEMM_LAUNCH(true, true);
 #undef ACL_GEMM_LAUNCH
+#undef ACL_GEMM_LAUNCH2
   return hipGetLastError();
 }
 
