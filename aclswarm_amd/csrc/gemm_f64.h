@@ -40,7 +40,7 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kGemmKStep = 16;
 #ifndef ACL_GEMM_TILE_DEFAULT
-#define ACL_GEMM_TILE_DEFAULT 64
+#define ACL_GEMM_TILE_DEFAULT 80
 #endif
 
 // op(A)[i][kk]: TA ? A[kk + i*lda] : A[i + kk*lda]
@@ -172,14 +172,145 @@ __global__ void __launch_bounds__(256) gemm_f64_kernel(const GemmJob* __restrict
       }
 }
 
-// Output tile per workgroup: 64 (default) or 32 (ACLSWARM_AMD_GEMM_TILE=32).
-// Measured on C5 (N=100, F=1024): 548 ms per batch with 64, 684 ms with 32
-// (the 32-tile wave holds one accumulator: less padding, but dependent MFMAs).
+// 80 x 80 output tile per 320-thread workgroup (five waves, wave w owns the
+// 16-row block strip w: one A operand and five B operands per MFMA step).
+// 80 = 5 x 16 fits the ADMM's 392-sized products with 2% padding (64-tiles
+// pad them to 448: 23% of the MFMA work on zeros).
+template <bool TA, bool TB, bool SYM>
+__global__ void __launch_bounds__(320) gemm80_f64_kernel(const GemmJob* __restrict__ jobs, int njobs,
+                                                           int tm, int tiles,
+                                                           unsigned long long* flops) {
+  constexpr int TILE = 80, NB = 5, EPT = 4;  // 2 x 80 x 16 operands / 320 threads = 4 + 4
+  const int blk = blockIdx.x;
+  const int slot = blk >> 3;
+  const int job = (blk & 7) + 8 * (slot / tiles);
+  if (job >= njobs) return;
+  int t = slot % tiles, bi, bj;
+  if (SYM) {
+    bj = 0;
+    while (t > bj) { t -= bj + 1; ++bj; }
+    bi = t;
+  } else {
+    bi = t % tm;
+    bj = t / tm;
+  }
+  const GemmJob J = jobs[job];
+  if (J.skip && *J.skip) return;
+  const int m0 = bi * TILE, n0 = bj * TILE;
+  if (m0 >= J.m || n0 >= J.n) return;
+  if (flops && threadIdx.x == 0)
+    atomicAdd(flops, 2ull * (unsigned long long)min(TILE, J.m - m0) *
+                         (unsigned long long)min(TILE, J.n - n0) * (unsigned long long)J.k);
+  // LDS images, conflict-free for the MFMA operand reads (ds_read_b64 lane
+  // groups 0-31 / 32-63, bank = dword mod 64) and the staging stores
+  // (ds_write_b64 groups of 16 contiguous lanes, bank = dword mod 32):
+  // an operand contiguous along i (j) in memory is staged k-major, rows of
+  // 80 doubles (two k rows of 16 doubles land on disjoint bank halves); one
+  // contiguous along k is staged i-major, rows of 18 doubles (16 i x 2 k in
+  // a read group cover all 64 banks once), so 16 lanes store one row.
+  constexpr bool AT = TA, BT = !TB;  // staged i-major (k contiguous in memory)
+  constexpr int KM = TILE, IM = 18;  // row strides (doubles)
+  constexpr int SZ = TILE * IM;      // >= kGemmKStep * KM
+  __shared__ double Ash[2][SZ];
+  __shared__ double Bsh[2][SZ];
+  auto a_at = [&](int buf, int kk, int i) -> double& {
+    return AT ? Ash[buf][i * IM + kk] : Ash[buf][kk * KM + i];
+  };
+  auto b_at = [&](int buf, int kk, int j) -> double& {
+    return BT ? Bsh[buf][j * IM + kk] : Bsh[buf][kk * KM + j];
+  };
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  double ra[EPT], rb[EPT];
+  // staging maps: the contiguous dimension along the threads
+  auto a_idx = [&](int r, int& i, int& kk) {
+    if (!TA) { i = tid % TILE; kk = tid / TILE + 4 * r; }
+    else     { kk = tid & 15; i = (tid >> 4) + 20 * r; }
+  };
+  auto b_idx = [&](int r, int& j, int& kb) {
+    if (TB) { j = tid % TILE; kb = tid / TILE + 4 * r; }
+    else    { kb = tid & 15; j = (tid >> 4) + 20 * r; }
+  };
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < EPT; ++r) {
+      int i, kk;
+      a_idx(r, i, kk);
+      const int gi = m0 + i, gk = k0 + kk;
+      ra[r] = (gi < J.m && gk < J.k)
+                  ? (TA ? J.A[gk + (size_t)gi * J.lda] : J.A[gi + (size_t)gk * J.lda])
+                  : 0.0;
+      int j, kb;
+      b_idx(r, j, kb);
+      const int gj = n0 + j, gkb = k0 + kb;
+      rb[r] = (gj < J.n && gkb < J.k)
+                  ? (TB ? J.B[gj + (size_t)gkb * J.ldb] : J.B[gkb + (size_t)gj * J.ldb])
+                  : 0.0;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < EPT; ++r) {
+      int i, kk;
+      a_idx(r, i, kk);
+      a_at(buf, kk, i) = ra[r];
+      int j, kb;
+      b_idx(r, j, kb);
+      b_at(buf, kb, j) = rb[r];
+    }
+  };
+  f64x4 acc[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[b] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const int nk = (J.k + kGemmKStep - 1) / kGemmKStep;
+  if (nk > 0) {
+    load(0);
+    store(0);
+    __syncthreads();
+  }
+  for (int kb = 0; kb < nk; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nk) load((kb + 1) * kGemmKStep);
+#pragma unroll
+    for (int k4 = 0; k4 < kGemmKStep; k4 += 4) {
+      const int kr = k4 + (lane >> 4);
+      const double av = a_at(cur, kr, wave * 16 + (lane & 15));
+      double bv[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) bv[b] = b_at(cur, kr, b * 16 + (lane & 15));
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(bv[b], av, acc[b], 0, 0, 0);
+    }
+    if (kb + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+  }
+  const double alpha = J.alpha, beta = J.beta;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gi = m0 + wave * 16 + (lane & 15);
+      const int gj = n0 + b * 16 + (lane >> 4) + 4 * r;
+      if (gi < J.m && gj < J.n) {
+        double v = alpha * acc[b][r];
+        if (beta != 0.0) v += beta * J.C[gi + (size_t)gj * J.ldc];
+        J.D[gi + (size_t)gj * J.ldd] = v;
+        if (SYM && bi != bj) J.D[gj + (size_t)gi * J.ldd] = v;
+      }
+    }
+}
+
+// Output tile per workgroup: 80 (default), 64 or 32 (ACLSWARM_AMD_GEMM_TILE).
+// Measured on C5 (N=100, F=1024) in round 1: 548 ms per batch with 64, 684 ms
+// with 32 (the 32-tile wave holds one accumulator: less padding, but
+// dependent MFMAs).
 inline int gemm_tile() {
   static int t = 0;
   if (!t) {
     const char* e = getenv("ACLSWARM_AMD_GEMM_TILE");
-    t = e ? (e[0] == '3' ? 32 : 64) : ACL_GEMM_TILE_DEFAULT;
+    t = e ? atoi(e) : ACL_GEMM_TILE_DEFAULT;
+    if (t != 32 && t != 64 && t != 80) t = ACL_GEMM_TILE_DEFAULT;
   }
   return t;
 }
@@ -197,7 +328,10 @@ inline hipError_t gemm_f64(bool ta, bool tb, const GemmJob* jobs, int njobs, int
   const dim3 grid(8 * ((njobs + 7) / 8) * tiles);
 #define ACL_GEMM_LAUNCH2(TA_, TB_, SYM_)                                                   \
   do {                                                                                     \
-    if (T == 64)                                                                           \
+    if (T == 80)                                                                           \
+      hipLaunchKernelGGL((gemm80_f64_kernel<TA_, TB_, SYM_>), grid, dim3(320), 0, s, jobs,  \
+                         njobs, tm, tiles, flops);                                         \
+    else if (T == 64)                                                                      \
       hipLaunchKernelGGL((gemm_f64_kernel<TA_, TB_, 2, SYM_>), grid, dim3(256), 0, s, jobs, \
                          njobs, tm, tiles, flops);                                         \
     else                                                                                   \

@@ -9,4 +9,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/kt_admm -o run --outp
     python3 scripts/admm_bench.py --reps 1 > gpurun_out/admm_prof/bench.json 2> gpurun_out/admm_prof/err.txt || { tail -20 gpurun_out/admm_prof/err.txt; exit 1; }
 f=$(find /tmp/kt_admm -name "*kernel_stats.csv" | head -1)
 cp "$f" gpurun_out/admm_prof/kernel_stats.csv
+t=$(find /tmp/kt_admm -name "*kernel_trace.csv" | head -1)
+gzip -c "$t" > gpurun_out/admm_prof/kernel_trace.csv.gz
 cut -d, -f1-4 gpurun_out/admm_prof/kernel_stats.csv | cut -c1-150 | head -16
