@@ -22,7 +22,7 @@ FLAG_CHANGED = 0x04
 FLAG_NONFINITE = 0x08
 FLAG_BAD_INPUT = 0x10
 FLAG_CA_ACTIVE = 0x20
-ABI_VERSION = 3  # include/aclswarm_amd.h ACL_ABI_VERSION
+ABI_VERSION = 4  # include/aclswarm_amd.h ACL_ABI_VERSION
 FLAG_FRAGILE = 0x40
 FRAGILE_MARGIN = 1e-6
 
@@ -33,7 +33,7 @@ STATUS_DTYPE = np.dtype([("flags", "<u4"), ("eff_rounds", "<u2"),
 # every symbol include/aclswarm_amd.h declares
 EXPORTS = (
     "acl_default_cntrl_gains", "acl_default_safety_params", "acl_default_admm_params",
-    "acl_formations_init", "acl_max_vehicles", "acl_abi_version", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_count_edges", "acl_pack_adjacency",
+    "acl_formations_init", "acl_max_vehicles", "acl_abi_version", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_swarm_stats", "acl_count_edges", "acl_pack_adjacency",
     "acl_pack_gains", "acl_gain_planes", "acl_pack_gains_planes", "acl_tile_gains", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
     "acl_control_batch", "acl_write_assignment_log", "acl_read_assignment_log",
     "acl_hungarian_batch",
@@ -169,6 +169,8 @@ def lib():
     L.acl_pack_gains_planes.argtypes = [I32, VP, VP, I32, VP]
     L.acl_pack_gains_planes.restype = ct.c_int
     L.acl_tile_gains.argtypes = [ct.POINTER(Formations), VP, VP]
+    L.acl_swarm_stats.argtypes = [VP, I32, VP, VP, VP]
+    L.acl_swarm_stats.restype = I32
     L.acl_tile_gains.restype = ct.c_int
     L.acl_admm_solve_batch.argtypes = [I32, I32, VP, VP, VP, VP, ct.POINTER(AdmmParams), VP]
     L.acl_admm_solve_batch.restype = ct.c_int

@@ -92,6 +92,69 @@ static int overlap_chunks() {
   }
   return k;
 }
+namespace acl_amd {
+// acl_swarm_stats: one workgroup strides over the records (1 MB at B = 65536:
+// microseconds), LDS accumulators, then one thread writes every output.
+constexpr int kStatsThreads = 1024, kStatsHist = 64, kStatsKeys = 11;
+__global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_status_t* st, int B,
+                                                              long long* counters, double* ext) {
+  __shared__ unsigned long long cnt[kStatsKeys + kStatsHist];
+  __shared__ unsigned emax, mmin;
+  const int tid = threadIdx.x;
+  for (int k = tid; k < kStatsKeys + kStatsHist; k += kStatsThreads) cnt[k] = 0ull;
+  if (tid == 0) {
+    emax = 0u;
+    mmin = 0x7F800000u;  // +inf: margins are non-negative floats (bits order as values)
+  }
+  __syncthreads();
+  unsigned long long c[kStatsKeys] = {};
+  unsigned em = 0u, mm = 0x7F800000u;
+  for (int b = tid; b < B; b += kStatsThreads) {
+    const acl_swarm_status_t s = st[b];
+    c[0] += 1;
+    const uint32_t bits[7] = {ACL_SWARM_VALID, ACL_SWARM_AGREE, ACL_SWARM_CHANGED,
+                              ACL_SWARM_NONFINITE, ACL_SWARM_BAD_INPUT, ACL_SWARM_CA_ACTIVE,
+                              ACL_SWARM_FRAGILE};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) c[1 + k] += (s.flags & bits[k]) ? 1 : 0;
+    c[8] += s.n_invalid;
+    c[9] += s.n_ca;
+    c[10] += s.eff_rounds;
+    atomicAdd(&cnt[kStatsKeys + (s.eff_rounds < kStatsHist - 1 ? s.eff_rounds : kStatsHist - 1)],
+              1ull);
+    em = s.eff_rounds > em ? s.eff_rounds : em;
+    const unsigned mb = __float_as_uint(s.margin);
+    mm = mb < mm ? mb : mm;
+  }
+#pragma unroll
+  for (int k = 0; k < kStatsKeys; ++k)
+    if (c[k]) atomicAdd(&cnt[k], c[k]);
+  atomicMax(&emax, em);
+  atomicMin(&mmin, mm);
+  __syncthreads();
+  for (int k = tid; k < kStatsKeys + kStatsHist; k += kStatsThreads)
+    counters[k] = (long long)cnt[k];
+  if (tid == 0) {
+    ext[0] = B > 0 ? (double)emax : 0.0;
+    ext[1] = B > 0 ? -(double)__uint_as_float(mmin) : -1.0;
+  }
+}
+}  // namespace acl_amd
+
+extern "C" acl_status_t acl_swarm_stats(const acl_swarm_status_t* status, int32_t B,
+                                        int64_t* counters, double* extrema, void* stream) {
+  using namespace acl_amd;
+  static_assert(kStatsKeys + kStatsHist == ACL_STATS_COUNTERS, "counter layout");
+  if (B < 0) return acl__set_error("acl_swarm_stats: B < 0");
+  if (!counters || !extrema || (B > 0 && !status))
+    return acl__set_error("acl_swarm_stats: null argument");
+  hipLaunchKernelGGL(stats_kernel, dim3(1), dim3(kStatsThreads), 0, (hipStream_t)stream, status, B,
+                     (long long*)counters, extrema);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
+  return ACL_OK;
+}
+
 static acl_status_t solve_overlapped(const acl_formations_t* F, const acl_solve_args_t* a,
                                      acl_amd::SolveParams P, hipStream_t s, int nchunk);
 

@@ -22,14 +22,38 @@ HIST_BINS = 64  # effective rounds 0..62, bin 63 = 63 or more
 def swarm_stats(status_u8):
     """[B][16] uint8 status records -> (int64 counters [len(STAT_KEYS) +
     HIST_BINS]: the STAT_KEYS counts then the eff_rounds histogram;
-    extrema f64 [2]: max eff_rounds, -(min margin)) on the device."""
+    extrema f64 [2]: max eff_rounds, -(min margin)) on the device. GPU
+    records: one launch of acl_swarm_stats; CPU records (the gloo tests):
+    the same reduction in torch."""
+    if status_u8.is_cuda:
+        return _swarm_stats_native(status_u8)
+    return swarm_stats_torch(status_u8)
+
+
+def _swarm_stats_native(status_u8):
+    from . import _lib
+    st = status_u8.contiguous()
+    dev = st.device
+    counters = torch.empty(len(STAT_KEYS) + HIST_BINS, dtype=torch.int64, device=dev)
+    ext = torch.empty(2, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    rc = _lib.lib().acl_swarm_stats(st.data_ptr(), st.shape[0], counters.data_ptr(),
+                                    ext.data_ptr(), stream)
+    _lib.check(rc)
+    return counters, ext
+
+
+def swarm_stats_torch(status_u8):
+    """The torch statement of acl_swarm_stats (CPU records, and the GPU
+    test's reference)."""
     s = status_u8.to(torch.int64)
     flags = s[:, 0] | (s[:, 1] << 8) | (s[:, 2] << 16) | (s[:, 3] << 24)
     eff = s[:, 4] | (s[:, 5] << 8)
     ninv = s[:, 8] | (s[:, 9] << 8)
     nca = s[:, 10] | (s[:, 11] << 8)
-    margin = status_u8[:, 12:16].contiguous().view(torch.float32).reshape(-1)
     dev = s.device
+    margin = (status_u8[:, 12:16].contiguous().view(torch.float32).reshape(-1)
+              if status_u8.shape[0] else torch.empty(0, dtype=torch.float32, device=dev))
     c = [torch.tensor(s.shape[0], device=dev, dtype=torch.int64)]
     c += [((flags & bit) != 0).sum() for bit in FLAG_BITS]
     c += [ninv.sum(), nca.sum(), eff.sum()]

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define ACL_ABI_VERSION 3
+#define ACL_ABI_VERSION 4
 
 typedef enum {
   ACL_OK = 0,
@@ -197,6 +197,21 @@ void acl_formations_init(acl_formations_t* F, int32_t n, int32_t n_formations);
  * every lane that has one, then edge (j, i) of every lane that has one
  * (diagonal tile: lanes r < c). Stream-ordered. */
 acl_status_t acl_tile_gains(const acl_formations_t* F, double* out, void* stream);
+
+/* ---- swarm statistics of a solve ---------------------------
+ * The convergence counters the multi-GPU gather all-reduces, computed from B
+ * status records in one launch on `stream` (device pointers, no sync):
+ *   counters[0 .. 10]  int64: B; the number of swarms with each of the
+ *       flags VALID, AGREE, CHANGED, NONFINITE, BAD_INPUT, CA_ACTIVE,
+ *       FRAGILE; the sums of n_invalid, n_ca and eff_rounds;
+ *   counters[11 .. 74] int64: histogram of eff_rounds (bin 63: 63 or more);
+ *   extrema[0..1]      f64: max eff_rounds, -(min margin) (0 and -1 for B = 0).
+ * The reference keeps no such statistics in the hot path (its supervisor
+ * logs convergence per trial, supervisor.py:297-348); the layout is the one
+ * aclswarm_amd/dist.py reduces across ranks. */
+#define ACL_STATS_COUNTERS 75
+acl_status_t acl_swarm_stats(const acl_swarm_status_t* status, int32_t B, int64_t* counters,
+                             double* extrema, void* stream);
 
 /* ---- the batched solve --------------------------------------------------
  * One "solve" = for one swarm of n vehicles:
