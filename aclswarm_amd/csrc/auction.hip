@@ -48,8 +48,9 @@
 
 namespace acl_amd {
 
-constexpr int kAB = 512;       // threads per swarm
-constexpr int kAW = kAB / 64;  // waves per swarm
+// threads per swarm (kernel template parameter kAB): 512 for n > 64, 256 for
+// 32 < n <= 64, 128 for n <= 32 -- a small swarm leaves most of a 512-thread
+// workgroup idle in every phase, and the CU holds more small swarms
 #ifndef ACL_AUCTION_LEVELS
 #define ACL_AUCTION_LEVELS 4   // price levels per dirty column before the exact scan
 #endif
@@ -333,8 +334,9 @@ __device__ __forceinline__ void runner_up_walk(int n, const unsigned (&key)[NC],
   }
 }
 
-template <int NC>
+template <int NC, int kAB>
 __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
+  constexpr int kAW = kAB / 64;  // waves per swarm
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const ALayout L = make_alayout(n);
@@ -997,17 +999,21 @@ hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream) {
   const ALayout L = make_alayout(P.n);
   static bool configured = false;
   if (!configured) {
-    for (const void* k : {(const void*)auction_kernel<1>, (const void*)auction_kernel<2>}) {
+    for (const void* k : {(const void*)auction_kernel<1, 128>, (const void*)auction_kernel<1, 256>,
+                          (const void*)auction_kernel<2, 512>}) {
       const hipError_t e =
           hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
     configured = true;
   }
-  if (P.n <= 64)
-    hipLaunchKernelGGL(auction_kernel<1>, dim3(nb), dim3(kAB), L.total, stream, P);
+  // (64 threads for n <= 32 measured no faster at C2: 0.091 vs 0.088 ms)
+  if (P.n <= 32)
+    hipLaunchKernelGGL((auction_kernel<1, 128>), dim3(nb), dim3(128), L.total, stream, P);
+  else if (P.n <= 64)
+    hipLaunchKernelGGL((auction_kernel<1, 256>), dim3(nb), dim3(256), L.total, stream, P);
   else
-    hipLaunchKernelGGL(auction_kernel<2>, dim3(nb), dim3(kAB), L.total, stream, P);
+    hipLaunchKernelGGL((auction_kernel<2, 512>), dim3(nb), dim3(512), L.total, stream, P);
   return hipGetLastError();
 }
 

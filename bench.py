@@ -378,7 +378,9 @@ def main():
     gain_sym = ("acl_amd::gain_pair_kernel<%s>" % ("true" if t_tile is not None else "false")
                 if w["planes"] == 5 and os.environ.get("ACLSWARM_AMD_GAIN_PAIR", "1") != "0"
                 else f"acl_amd::gain_kernel<{w['planes']}>")
-    auction_sym = ("acl_amd::auction_kernel<%d>" % (1 if n <= 64 else 2) if n <= 128
+    auction_sym = (("acl_amd::auction_kernel<1, 128>" if n <= 32 else
+                    "acl_amd::auction_kernel<1, 256>" if n <= 64 else
+                    "acl_amd::auction_kernel<2, 512>") if n <= 128
                    else "acl_amd::solve_wide_kernel")
     kern = {}
     for k, (name, sym) in enumerate((("auction", auction_sym), ("gain", gain_sym),
