@@ -940,6 +940,101 @@ __host__ __device__ inline int ca_wave_bytes(int n) {
   return cal16(n * 3 * 8) + cal16(4 * n * 8) + cal16(4 * n);
 }
 
+// Wave-parallel tail of collisionAvoidance for one vehicle whose sector
+// edges fit one wave (lane k < nslot holds slot k of caA / caS; sign 0 =
+// unused). Same results as the serial lane-0 path below: the edges sorted as
+// std::sort on (angle, sign) pairs (bitonic network on lanes; the order of a
+// sequence of keys is unique), the parenthesis-count union as a prefix sum of
+// the signs, a zone's start the edge after the previous zone's end, the
+// closest zone edge by lower_bound over the sorted, flattened zone edges.
+// Returns true when psi lies strictly inside a zone (cmd is then updated).
+__device__ __forceinline__ bool ca_resolve_wave(int lane, int nslot, const double* caA,
+                                                const signed char* caS, bool didWrap,
+                                                double& cmd0, double& cmd1, double& cmd2) {
+  double a = 0.0;
+  int sg = 0;
+  if (lane < nslot) {
+    a = caA[lane];
+    sg = caS[lane];
+  }
+  // sort key: the angle's total order (-0.0 as +0.0, so equal angles tie as
+  // in the double comparison), unused slots last
+  auto keyof = [](double x, int sgn) -> unsigned long long {
+    if (sgn == 0) return ~0ull;
+    const unsigned long long u = (unsigned long long)__double_as_longlong(x + 0.0);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+  };
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const double pa = __shfl_xor(a, j, 64);
+      const int ps = __shfl_xor(sg, j, 64);
+      const unsigned long long mk = keyof(a, sg), pk = keyof(pa, ps);
+      const bool pless = pk < mk || (pk == mk && ps < sg);
+      const bool mless = mk < pk || (mk == pk && sg < ps);
+      const bool take_min = ((lane & k) == 0) == ((lane & j) == 0);
+      if (take_min ? pless : mless) {
+        a = pa;
+        sg = ps;
+      }
+    }
+  }
+  // union: inclusive prefix count of the signs
+  int incl = sg;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  const int excl = incl - sg;
+  const bool isEnd = sg != 0 && incl == 0;
+  const unsigned long long endMask = __ballot(isEnd);
+  if (!endMask) return false;
+  // zone of an end lane e: from the lane after the previous end (or lane 0)
+  const unsigned long long below = endMask & ((1ull << lane) - 1ull);
+  const int sLane = below ? 64 - __clzll(below) : 0;
+  const double zs = __shfl(a, sLane, 64);
+  const double psi = atan2(cmd1, cmd0);
+  const bool inside = isEnd && psi > zs && psi < a;
+  if (!__any(inside)) return false;
+  // zone edges in order: every closed zone's start and end; +-pi dropped
+  // when some sector wrapped
+  const int lastEnd = 63 - __clzll(endMask);
+  const bool isStart = sg != 0 && excl == 0 && lane < lastEnd;
+  const bool keep = (isStart || isEnd) && !(didWrap && fabs(a) == kPi);
+  const unsigned long long km = __ballot(keep);
+  const int m = __popcll(km);
+  if (m == 0) {
+    cmd0 = cmd1 = 0.0;
+    cmd2 = 0.0;
+    return true;
+  }
+  const int it = __popcll(km & __ballot(keep && a < psi));  // std::lower_bound
+  auto nth = [&](int r) -> int {  // lane of the r-th kept edge
+    unsigned long long x = km;
+    for (int t = 0; t < r; ++t) x &= x - 1ull;
+    return __ffsll((long long)x) - 1;
+  };
+  int idx;
+  if (it == 0) idx = 0;
+  else if (it == m) idx = it - 1;
+  else {
+    const double lo = __shfl(a, nth(it - 1), 64), hi = __shfl(a, nth(it), 64);
+    idx = fabs(lo - psi) < fabs(hi - psi) ? it - 1 : it;
+  }
+  const double edge = __shfl(a, nth(idx), 64);
+  if (fabs(wrap_to_pi(edge - psi)) <= kPi / 2) {
+    const double umag = sqrt(cmd0 * cmd0 + cmd1 * cmd1);
+    cmd0 = umag * cos(edge);
+    cmd1 = umag * sin(edge);
+  } else {
+    cmd0 = cmd1 = 0.0;
+    cmd2 = 0.0;
+  }
+  return true;
+}
+
 __global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
@@ -1004,7 +1099,13 @@ __global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
         const int nslot = 4 * base;
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
-        if (lane == 0) {
+        // up to 16 close vehicles: the whole wave resolves the sectors; more
+        // (or a NaN angle) take the serial path
+        bool nanA = false;
+        if (nslot <= 64 && lane < nslot) nanA = caS[lane] != 0 && caA[lane] != caA[lane];
+        const bool par = nslot <= 64 && !__any(nanA);
+        if (par) modified = ca_resolve_wave(lane, nslot, caA, caS, didWrap, cmd0, cmd1, cmd2);
+        if (!par && lane == 0) {
           // compact + insertion sort by (angle, sign) = std::sort on pairs
           int ne = 0;
           for (int k = 0; k < nslot; ++k) {

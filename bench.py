@@ -247,6 +247,8 @@ def main():
     ap.add_argument("--no-tile-gains", action="store_true",
                     help="pair kernel reads the row-major records instead of the "
                          "tile-ordered copy made at formation setup (acl_tile_gains)")
+    ap.add_argument("--no-ca-probe", action="store_true",
+                    help="skip the crowded (collision-avoidance) probe reported beside the headline")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo rehearsal of the launch + gather path (no GPU, no solve)")
     args = ap.parse_args()
@@ -372,6 +374,45 @@ def main():
             setup["break_even_solves_per_formation"] = (
                 (t_tile / w["F"]) / (gain_s / B) if gain_s > 0 else None)
 
+    # collision-avoidance probe: the same swarms crowded (positions scaled by
+    # 0.3 about each swarm's centre, most vehicles inside the 1.5 m avoidance
+    # radius), so the sector algebra of Safety::collisionAvoidance
+    # (safety.cpp:412-541) runs for most vehicles; reported beside the
+    # headline, which is the reference's spacing (start.sh discs, no CA)
+    ca_probe = None
+    if not args.no_ca_probe:
+        qc = w["q"].clone()
+        cen = qc[:, :, :2].mean(dim=1, keepdim=True)
+        qc[:, :, :2] = cen + 0.3 * (qc[:, :, :2] - cen)
+        outc = {k: torch.empty_like(v) for k, v in out.items()}
+
+        def solve_c():
+            engine.solve(T, w["fidx"], qc, w["vel"], w["P_in"], early_exit=not args.full_rounds,
+                         out=outc, stream=stream.cuda_stream)
+        solve_c()
+        torch.cuda.synchronize()
+        lib.acl_internal_kernel_timing(1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(3):
+            solve_c()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        kms_c = (ctypes.c_double * 3)()
+        kcnt_c = (ctypes.c_int * 3)()
+        if lib.acl_internal_kernel_times(kms_c, kcnt_c) != 0:
+            raise RuntimeError("kernel timing failed")
+        lib.acl_internal_kernel_timing(0)
+        ms_c = e0.elapsed_time(e1) / 3
+        sc = D.stats_dict(*D.swarm_stats(outc["status"]))
+        ca_probe = {"what": "the benchmark's swarms with positions scaled by 0.3 about each "
+                            "swarm's centre (collision avoidance active)",
+                    "call_ms": ms_c, "value_1gpu": B / (ms_c * 1e-3),
+                    "kernel_ms": {k: kms_c[i] / max(kcnt_c[i], 1)
+                                  for i, k in enumerate(("auction", "gain", "ca"))},
+                    "ca_active_swarms": sc["ca_active"], "ca_vehicles": sc["ca_vehicles"]}
+        del outc, qc
+
     # algorithmic bytes per launch (every kernel is one launch over all B)
     a_all, g_all, s_all, e_avg = algorithmic_bytes(w, 0, B)
     per_launch = {"auction": a_all, "gain": g_all, "ca": s_all}
@@ -457,6 +498,7 @@ def main():
             "kernels": kern,
         },
         "setup": setup,
+        "ca_probe": ca_probe,
         "stats": stats,
         "gen_s": t_gen,
     }
