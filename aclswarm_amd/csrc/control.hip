@@ -157,13 +157,17 @@ __device__ void gain_epilogue(const CtlParams& P, int b, int n, const double* q,
 // the fast e (fused multiply-adds, one-step sqrt; error far below 1e-9 at the
 // configs' distances) is recomputed with correctly rounded square roots and
 // no contraction whenever it lies within 1e-9 of a threshold. Returns the
-// two gate decisions; gm takes the gate margin min(| |e| - thr | / thr).
+// two gate decisions; mxy / mz take min | |e| - thr | of each gate (the gate
+// margin min(| |e| - thr | / thr) is formed once per swarm by gate_margin_of:
+// division by a positive constant is monotone under rounding, so
+// fl(min x / thr) = min fl(x / thr) -- two divisions per swarm, not per edge).
 #define ACL_GATE_WINDOW 1e-9
+template <bool GM>
 __device__ __forceinline__ void gate_decide(const acl_cntrl_gains_t& g, double e_xy, double e_z,
                                             double q0, double q1, double q2, double Ni, double Nj,
                                             double Nzi, double Nzj, double pix, double piy,
                                             double piz, double pjx, double pjy, double pjz,
-                                            bool& gxy, bool& gz, double& gm) {
+                                            bool& gxy, bool& gz, double& mxy, double& mz) {
   double axy = fabs(e_xy), az = fabs(e_z);
   const double dxy = fabs(axy - g.e_xy_thr), dz = fabs(az - g.e_z_thr);
   if (dxy < ACL_GATE_WINDOW || dz < ACL_GATE_WINDOW) {
@@ -175,8 +179,14 @@ __device__ __forceinline__ void gate_decide(const acl_cntrl_gains_t& g, double e
   }
   gxy = axy > g.e_xy_thr;
   gz = az > g.e_z_thr;
-  const double mxy = fabs(axy - g.e_xy_thr) / g.e_xy_thr, mz = fabs(az - g.e_z_thr) / g.e_z_thr;
-  gm = fmin(gm, fmin(mxy, mz));
+  if (GM) {
+    mxy = fmin(mxy, fabs(axy - g.e_xy_thr));
+    mz = fmin(mz, fabs(az - g.e_z_thr));
+  }
+}
+
+__device__ __forceinline__ double gate_margin_of(const acl_cntrl_gains_t& g, double mxy, double mz) {
+  return fmin(mxy / g.e_xy_thr, mz / g.e_z_thr);
 }
 
 // per-swarm gate margin: wave minimum, then the block's minimum through LDS
@@ -189,7 +199,8 @@ __device__ __forceinline__ void gate_margin_reduce(unsigned long long* word, dou
 
 // NP = 9: general 3x3 gain blocks; NP = 5: the ADMM block structure, the four
 // structural zeros supplied as constants (acl_formations_t::gain_planes)
-template <int NP>
+// GM: the caller asked for the gate margin (acl_solve_args_t::gate_margin)
+template <int NP, bool GM>
 __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
@@ -268,7 +279,7 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
   const int E = __builtin_amdgcn_readfirstlane(rowpre[n * NW]);
   __shared__ unsigned long long gmw;
   if (tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
-  double gmin = __builtin_inf();
+  double gmxy = __builtin_inf(), gmz = __builtin_inf();
   const double* G = P.gains + NP * P.gain_off[f];
   // the formation's gains through one buffer resource (9 planes: plane k at
   // SGPR offset 8kE, one VGPR offset per lane; 5: one 40-byte record per
@@ -363,8 +374,8 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
         // the two gated atan terms, one after the other (register pressure)
         double Fxy = 0.0, Fz = 0.0;
         bool gxy, gz;
-        gate_decide(g, e_xy, e_z, q0, q1, q2, Ni, pn[2 * j], Nzi, pn[2 * j + 1], pix, piy, piz,
-                    pjx, pjy, pjz, gxy, gz, gmin);
+        gate_decide<GM>(g, e_xy, e_z, q0, q1, q2, Ni, pn[2 * j], Nzi, pn[2 * j + 1], pix, piy, piz,
+                    pjx, pjy, pjz, gxy, gz, gmxy, gmz);
 #pragma unroll 1
         for (int kk = 0; kk < 2; ++kk) {
           const bool on = kk ? gz : gxy;
@@ -416,9 +427,9 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }
-  if (P.gate_margin) gate_margin_reduce(&gmw, gmin);
+  if (GM) gate_margin_reduce(&gmw, gate_margin_of(g, gmxy, gmz));
   __syncthreads();
-  if (P.gate_margin && tid == 0) P.gate_margin[b] = __longlong_as_double((long long)gmw);
+  if (GM && tid == 0) P.gate_margin[b] = __longlong_as_double((long long)gmw);
   gain_epilogue(P, b, n, q, uo, tid);
 }
 
@@ -584,7 +595,7 @@ __host__ __device__ inline PairLayout make_pair_layout(int n) {
   return L;
 }
 
-template <bool kTiled>
+template <bool kTiled, bool GM>
 __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
@@ -664,7 +675,7 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
   const int E = __builtin_amdgcn_readfirstlane(rowpre[n * NW]);
   __shared__ unsigned long long gmw;
   if (tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
-  double gmin = __builtin_inf();
+  double gmxy = __builtin_inf(), gmz = __builtin_inf();
   const double* G = (tiled ? P.gains_tiled : P.gains) + 5 * P.gain_off[f];
   const __amdgpu_buffer_rsrc_t grs =
       __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 5 * E * 8, 0x00020000);
@@ -760,8 +771,8 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
       const double e_z = fabs(q2) - dz;
       double Fxy = 0.0, Fz = 0.0;
       bool gxy, gz;
-      gate_decide(g, e_xy, e_z, q0, q1, q2, pn[2 * i], pn[2 * j], pn[2 * i + 1], pn[2 * j + 1],
-                  pix, piy, piz, pjx, pjy, pjz, gxy, gz, gmin);
+      gate_decide<GM>(g, e_xy, e_z, q0, q1, q2, pn[2 * i], pn[2 * j], pn[2 * i + 1], pn[2 * j + 1],
+                  pix, piy, piz, pjx, pjy, pjz, gxy, gz, gmxy, gmz);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const bool on = kk ? gz : gxy;
@@ -820,9 +831,9 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
       Aji[k] = Bji[k];
     }
   }
-  if (P.gate_margin) gate_margin_reduce(&gmw, gmin);
+  if (GM) gate_margin_reduce(&gmw, gate_margin_of(g, gmxy, gmz));
   __syncthreads();
-  if (P.gate_margin && tid == 0) P.gate_margin[b] = __longlong_as_double((long long)gmw);
+  if (GM && tid == 0) P.gate_margin[b] = __longlong_as_double((long long)gmw);
   // u of the vehicle at row i: the four waves' sums in wave order, plus
   // kd (-vel) once per edge of row i (distcntrl.cpp:85-95)
   for (int i = tid; i < n; i += kCtlBlock) {
@@ -1264,25 +1275,36 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
       // for the swarms whose vehicles hold different assignments
       const PairLayout PL = make_pair_layout(P.n);
       const bool tiled = P.gains_tiled != nullptr && P.n <= kMaxN;
-      const void* kp = tiled ? (const void*)gain_pair_kernel<true>
-                             : (const void*)gain_pair_kernel<false>;
-      if (PL.total > 64 * 1024)
-        (void)hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, PL.total);
-      if (tiled)
-        hipLaunchKernelGGL(gain_pair_kernel<true>, dim3(nb), dim3(kCtlBlock), PL.total, stream, Q);
-      else
-        hipLaunchKernelGGL(gain_pair_kernel<false>, dim3(nb), dim3(kCtlBlock), PL.total, stream, Q);
+      const bool gm = P.gate_margin != nullptr;
+#define ACL_PAIR(T_, G_)                                                                     \
+  do {                                                                                       \
+    if (PL.total > 64 * 1024)                                                                \
+      (void)hipFuncSetAttribute((const void*)gain_pair_kernel<T_, G_>,                       \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, PL.total);       \
+    hipLaunchKernelGGL((gain_pair_kernel<T_, G_>), dim3(nb), dim3(kCtlBlock), PL.total, stream, Q); \
+  } while (0)
+      if (tiled && gm) ACL_PAIR(true, true);
+      else if (tiled) ACL_PAIR(true, false);
+      else if (gm) ACL_PAIR(false, true);
+      else ACL_PAIR(false, false);
+#undef ACL_PAIR
       if (P.all_uniform) return hipGetLastError();
       Q.only_nonuniform = 1;
     }
     const GainLayout L = make_gain_layout(P.n);
-    const void* k = P.gain_planes == 5 ? (const void*)gain_kernel<5> : (const void*)gain_kernel<9>;
-    if (L.total > 64 * 1024)
-      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, L.total);
-    if (P.gain_planes == 5)
-      hipLaunchKernelGGL(gain_kernel<5>, dim3(nb), dim3(kCtlBlock), L.total, stream, Q);
-    else
-      hipLaunchKernelGGL(gain_kernel<9>, dim3(nb), dim3(kCtlBlock), L.total, stream, Q);
+    const bool gm = P.gate_margin != nullptr;
+#define ACL_GAIN(NP_, G_)                                                                    \
+  do {                                                                                       \
+    if (L.total > 64 * 1024)                                                                 \
+      (void)hipFuncSetAttribute((const void*)gain_kernel<NP_, G_>,                           \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, L.total);        \
+    hipLaunchKernelGGL((gain_kernel<NP_, G_>), dim3(nb), dim3(kCtlBlock), L.total, stream, Q); \
+  } while (0)
+    if (P.gain_planes == 5 && gm) ACL_GAIN(5, true);
+    else if (P.gain_planes == 5) ACL_GAIN(5, false);
+    else if (gm) ACL_GAIN(9, true);
+    else ACL_GAIN(9, false);
+#undef ACL_GAIN
   } else {
     // a fixed grid striding over the device-side count of listed vehicles
     const int lds = kCaWaves * ca_wave_bytes(P.n);

@@ -416,9 +416,9 @@ def main():
     # algorithmic bytes per launch (every kernel is one launch over all B)
     a_all, g_all, s_all, e_avg = algorithmic_bytes(w, 0, B)
     per_launch = {"auction": a_all, "gain": g_all, "ca": s_all}
-    gain_sym = ("acl_amd::gain_pair_kernel<%s>" % ("true" if t_tile is not None else "false")
+    gain_sym = ("acl_amd::gain_pair_kernel<%s, false>" % ("true" if t_tile is not None else "false")
                 if w["planes"] == 5 and os.environ.get("ACLSWARM_AMD_GAIN_PAIR", "1") != "0"
-                else f"acl_amd::gain_kernel<{w['planes']}>")
+                else f"acl_amd::gain_kernel<{w['planes']}, false>")
     auction_sym = (("acl_amd::auction_kernel<1, 128>" if n <= 32 else
                     "acl_amd::auction_kernel<1, 256>" if n <= 64 else
                     "acl_amd::auction_kernel<2, 512>") if n <= 128
