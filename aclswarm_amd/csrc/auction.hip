@@ -98,7 +98,7 @@ __host__ __device__ inline ALayout make_alayout(int n) {
   return L;
 }
 
-enum { A_NITEMS = 2 };
+enum { A_NITEMS = 2, A_RCH = 3 /* [2]: a column changed in a round of that parity */ };
 
 // diagnostic builds (-DACL_AUCTION_STOP=k): the kernel returns after phase
 // k, for per-phase instruction counts (scripts/auction_phase_pmc.sh)
@@ -820,7 +820,8 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         }
         // the scan read the column: rewrite it only now
         __builtin_amdgcn_wave_barrier();
-        unsigned long long ch = 0ull;
+        unsigned long long ch = 0ull, mixed = 0ull;
+        const int nw0 = __builtin_amdgcn_readfirstlane(nw[0]);  // vehicle 0's new entry
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           if (okv[c]) T[rowa[c] + j] = (unsigned char)nw[c];
@@ -828,8 +829,16 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           const unsigned long long ob = __ballot(okv[c] && wu[c] == u && nw[c] != u);
           if (ob && lane == 0) atomicOr(&obm[2 * par + c], ob);  // outbid (auctioneer.cpp:502)
           ch |= __ballot(nw[c] != wu[c]);
+          mixed |= __ballot(okv[c] && nw[c] != nw0);
         }
-        if (ch && lane == 0) atomicOr(&dmask[2 * npar + (j >> 6)], 1ull << (j & 63));
+        // A column left holding one `who` everywhere is a fixed point (every
+        // neighbourhood sees one (price, who)) with no runner-up: it is not
+        // dirty next round unless a re-select writes it (which marks it).
+        // The change itself still counts for eff_rounds.
+        if (ch && lane == 0) {
+          misc[A_RCH + par] = 1;
+          if (mixed || nonfinite) atomicOr(&dmask[2 * npar + (j >> 6)], 1ull << (j & 63));
+        }
       }
     }
     {
@@ -846,6 +855,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         dmask[2 * par + 1] = 0ull;
         obm[2 * npar] = 0ull;   // round r+1's outbid mask
         obm[2 * npar + 1] = 0ull;
+        misc[A_RCH + npar] = 0;  // round r+1's change flag (round r-1's was read)
       }
       int base = 0;
 #pragma unroll
@@ -867,9 +877,14 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       }
     }
     __syncthreads();
-    const bool changed = (dmask[2 * npar] | dmask[2 * npar + 1]) != 0ull;
-    if (changed) eff = r;
-    else if (P.early_exit) break;  // fixed point
+    // a re-select always changes an entry; columns that changed but became
+    // uniform are not in the next mask (above)
+    const bool next = (dmask[2 * npar] | dmask[2 * npar + 1]) != 0ull;
+    if (next || misc[A_RCH + par]) eff = r;
+    // no dirty column and no re-select: round r+1 changes nothing, so round
+    // r's table is the fixed point every later round repeats (SURVEY App.
+    // A.5) -- with or without early_exit, the outcome of all 2N rounds
+    if (!next) break;
   }
   stamp_phase(P, b, tid, 4);
   ACL_AUCTION_STOP_AT(5);
