@@ -65,7 +65,7 @@ struct ALayout {
   int C, pq, adjF, items;
   int A, p, qf, out;
   int T, TS;
-  int vadj, Pin, Ptin, itm, valid, H, misc, total;
+  int vadj, Pin, Ptin, itm, valid, H, misc, dummy, total;
 };
 
 __host__ __device__ inline ALayout make_alayout(int n) {
@@ -94,6 +94,7 @@ __host__ __device__ inline ALayout make_alayout(int n) {
   L.valid = o; o = a16(o + n);
   L.H = o;     o = a16(o + 16 * 8);  // dmask[2][2], obm[2][2], seen[2]
   L.misc = o;  o = a16(o + 16 * 4);
+  L.dummy = o; o = a16(o + 64);      // write-back target of the lanes past n
   L.total = o;
   return L;
 }
@@ -167,6 +168,41 @@ __device__ __forceinline__ void stamp_phase(const SolveParams& P, int b, int tid
   if (P.stamps && tid == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
 }
 
+// diagnostic builds (-DACL_AUCTION_PROF=1): s_memtime cycles of the CBAA
+// column step's sections, summed over a swarm's waves into stamps[b][7..15]
+// (scripts/phase_profile.py; each mark waits for the wave's LDS operations,
+// so the split is indicative)
+#ifndef ACL_AUCTION_PROF
+#define ACL_AUCTION_PROF 0
+#endif
+enum { PS_L0, PS_LV, PS_MB, PS_WALK, PS_SCAN, PS_WB, PS_SEL, PS_BAR, PS_N };
+struct SecProf {
+  unsigned long long acc[PS_N], last;
+  unsigned cols, walks, scans;
+  __device__ void start() {
+    if (ACL_AUCTION_PROF) {
+      for (int k = 0; k < PS_N; ++k) acc[k] = 0;
+      cols = walks = scans = 0;
+      last = __builtin_amdgcn_s_memtime();
+    }
+  }
+  __device__ void mark(int k) {
+    if (ACL_AUCTION_PROF) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc[k] += t - last;
+      last = t;
+    }
+  }
+  __device__ void flush(const SolveParams& P, int b, int lane) {
+    if (ACL_AUCTION_PROF && P.stamps && lane == 0) {
+      unsigned long long* s = P.stamps + (size_t)b * 16 + 7;
+      for (int k = 0; k < PS_N; ++k) atomicAdd(s + k, acc[k]);
+      atomicAdd(s + PS_N, (unsigned long long)cols | ((unsigned long long)walks << 21) |
+                               ((unsigned long long)scans << 42));
+    }
+  }
+};
+
 // diagnostic builds (-DACL_AUCTION_NO_MARGIN): the CBAA rounds skip the
 // decision-margin bookkeeping (a cost measurement only; margins then wrong)
 #ifndef ACL_AUCTION_NO_MARGIN
@@ -179,6 +215,16 @@ __device__ __forceinline__ double margin_gap_pair(float hi, float lo) {
   m.hi = hi;
   m.lo = lo;
   return margin_gap(m);
+}
+
+// margin_track (common.h) of a per-lane pair where `act`, branch-free: the
+// kernel is bound by the CU's scalar pipe, and a divergent branch costs three
+// scalar instructions (exec save, branch, restore) where selects cost none
+__device__ __forceinline__ void margin_track_sel(MarginPair& m, float hi, float lo, bool act) {
+  const bool eq = act && lo == hi;
+  const bool up = act && lo < hi && (double)lo * (double)m.hi > (double)m.lo * (double)hi;
+  m.hi = eq ? 1.0f : (up ? hi : m.hi);
+  m.lo = eq ? 1.0f : (up ? lo : m.lo);
 }
 
 // margin_track on a wave-uniform pair, branch-free (selects)
@@ -234,13 +280,15 @@ __device__ __forceinline__ int wave_select(int n, int TS, int v, int lane, const
   const float cmax = __uint_as_float(M);
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
+    // the selected task vs its price; an eligible task that lost vs the
+    // maximum; a task that would win if it became eligible vs its price
     const int j = lane + 64 * c;
-    if (oth[c]) {
-      if (j == js) margin_track(m, cv[c], pr[c]);
-      else if (key[c] != 0u) margin_track(m, cmax, cv[c]);
-      else if (cv[c] > 0.0f && (js < 0 || cv[c] > cmax || (cv[c] == cmax && j < js)))
-        margin_track(m, pr[c], cv[c]);
-    }
+    const bool isjs = oth[c] && j == js;
+    const bool elig = oth[c] && !isjs && key[c] != 0u;
+    const bool near = oth[c] && !isjs && key[c] == 0u && cv[c] > 0.0f &&
+                      (js < 0 || cv[c] > cmax || (cv[c] == cmax && j < js));
+    margin_track_sel(m, isjs ? cv[c] : (elig ? cmax : pr[c]), isjs ? pr[c] : cv[c],
+                     isjs || elig || near);
   }
   return js;
 }
@@ -603,12 +651,6 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   }
   __syncthreads();  // region A (p, qf, out) is dead from here: T overlays it
   const bool nonfinite = misc[M_NONFIN] != 0;
-  {
-    // reset (auctioneer.cpp:448-465): every entry `none`
-    const unsigned fill = (unsigned)n * 0x01010101u;
-    unsigned* T32 = reinterpret_cast<unsigned*>(T);
-    for (int k = tid; k < n * TS / 4; k += kAB) T32[k] = fill;
-  }
   stamp_phase(P, b, tid, 3);
   ACL_AUCTION_STOP_AT(3);
 
@@ -616,7 +658,14 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   unsigned long long* dmask = H;      // [2 parities][2 words]
   unsigned long long* obm = H + 4;    // [2][2]
   // round 0: the START bid, select from the zero table (start, auctioneer.cpp:105)
+  // Each row is reset (auctioneer.cpp:448-465: every entry `none`) by the
+  // wave that then places that vehicle's START bid in it: one wave's LDS
+  // operations complete in order, so no reset store of another wave can land
+  // on a bid (a reset by all threads before the bids, without a barrier
+  // between, could: a latent race that surfaced as lost bids).
+  const unsigned fill = (unsigned)n * 0x01010101u;
   for (int v = wave; v < n; v += kAW) {
+    if (lane < TS / 4) reinterpret_cast<unsigned*>(T + v * TS)[lane] = fill;
     const int task = wave_select<NC>(n, TS, v, lane, C, T, true, mp);
     if (task >= 0 && lane == 0) {
       T[v * TS + task] = (unsigned char)v;
@@ -640,6 +689,8 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   // the wave's uniform margin pair over the level-resolved evaluations
   float uhi = 1.0f, ulo = 0.0f;
   int eff = 0;
+  SecProf sp;
+  sp.start();
   const int max_rounds = 2 * n;  // cbaa_max_iter_ = n * diameter (:50-51)
   for (int r = 1; r <= max_rounds; ++r) {
     const int par = r & 1, npar = par ^ 1;
@@ -702,7 +753,19 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         unsigned long long tie = 0ull;
 #pragma unroll
         for (int c = 0; c < NC; ++c) tie |= h[c] & __ballot(wu[c] != wk);
-        if (full && !tie && !nonfinite) continue;
+        if (ACL_AUCTION_PROF) sp.cols++;
+#ifdef ACL_CAL_VALU
+        // calibration builds: 20 independent VALU (or SALU) instructions per column
+        { int dmy; asm volatile(".rept 20\n\tv_mov_b32 %0, 0\n\t.endr" : "=v"(dmy)); }
+#endif
+#ifdef ACL_CAL_SALU
+        { int dmy; asm volatile(".rept 20\n\ts_mov_b32 %0, 0\n\t.endr" : "=s"(dmy)); }
+#endif
+        if (full && !tie && !nonfinite) {
+          sp.mark(PS_L0);
+          continue;
+        }
+        sp.mark(PS_L0);
         // winners, level by level. Per-vehicle state as lane masks: U = not
         // yet resolved, Nd = exact scan. Each resolving level's successor
         // bounds the decision gap of the vehicles it resolved (their
@@ -768,6 +831,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
             for (int c = 0; c < NC; ++c) tie |= h[c] & __ballot(wu[c] != wk);
           }
         }
+        sp.mark(PS_LV);
         if (!ACL_AUCTION_NO_MARGIN && kres != 0u && cum < n) {  // the resolving level's successor
           const unsigned Mn = level_key<NC>(key, kres);
           margin_track_u(bhi, blo, __uint_as_float(kres - 1u), __uint_as_float(Mn - 1u));
@@ -775,9 +839,15 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         // the exact runner-ups only where the bound could lower the wave's
         // running minimum (an evaluation skipped here has a gap >= the bound
         // >= a gap already tracked, so the minimum is unchanged)
-        if (!ACL_AUCTION_NO_MARGIN && (double)blo * (double)uhi > (double)ulo * (double)bhi &&
-            margin_gap_pair(bhi, blo) < Gpub)
+        const bool walk = !ACL_AUCTION_NO_MARGIN &&
+                          (double)blo * (double)uhi > (double)ulo * (double)bhi &&
+                          margin_gap_pair(bhi, blo) < Gpub;
+        sp.mark(PS_MB);
+        if (walk) {
           runner_up_walk<NC>(n, key, k1, Nd, vm, uhi, ulo);
+          if (ACL_AUCTION_PROF) sp.walks++;
+          sp.mark(PS_WALK);
+        }
         // the exact ordered scan (ascending vehid, strict >) for ties, NaN
         // prices and vehicles the levels did not resolve; the runner-up is the
         // best price of another `who` (entries of one `who` share its price)
@@ -788,6 +858,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           scan |= Nd[c];
         }
         if (scan) {
+          if (ACL_AUCTION_PROF) sp.scans++;
 #pragma unroll
           for (int c = 0; c < NC; ++c) {
             if (lanebit(Nd[c])) {
@@ -818,13 +889,15 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
             }
           }
         }
+        sp.mark(PS_SCAN);
         // the scan read the column: rewrite it only now
         __builtin_amdgcn_wave_barrier();
         unsigned long long ch = 0ull, mixed = 0ull;
         const int nw0 = __builtin_amdgcn_readfirstlane(nw[0]);  // vehicle 0's new entry
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-          if (okv[c]) T[rowa[c] + j] = (unsigned char)nw[c];
+          // (lanes past n store to a dummy row: no branch, see margin_track_sel)
+          smem[okv[c] ? L.T + rowa[c] + j : L.dummy + lane] = (unsigned char)nw[c];
           const int u = lane + 64 * c;
           const unsigned long long ob = __ballot(okv[c] && wu[c] == u && nw[c] != u);
           if (ob && lane == 0) atomicOr(&obm[2 * par + c], ob);  // outbid (auctioneer.cpp:502)
@@ -839,6 +912,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           misc[A_RCH + par] = 1;
           if (mixed || nonfinite) atomicOr(&dmask[2 * npar + (j >> 6)], 1ull << (j & 63));
         }
+        sp.mark(PS_WB);
       }
     }
     {
@@ -847,7 +921,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       const double gl = margin_gap(mp), gu = margin_gap_pair(uhi, ulo);
       block_min_gap(margw, gl < gu ? gl : gu);
     }
+    sp.mark(PS_WB);
     __syncthreads();
+    sp.mark(PS_BAR);
     // outbid vehicles re-select on their updated rows (auctioneer.cpp:224)
     {
       if (tid == 0) {
@@ -877,6 +953,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       }
     }
     __syncthreads();
+    sp.mark(PS_SEL);
     // a re-select always changes an entry; columns that changed but became
     // uniform are not in the next mask (above)
     const bool next = (dmask[2 * npar] | dmask[2 * npar + 1]) != 0ull;
@@ -886,6 +963,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     // A.5) -- with or without early_exit, the outcome of all 2N rounds
     if (!next) break;
   }
+  sp.flush(P, b, lane);
   stamp_phase(P, b, tid, 4);
   ACL_AUCTION_STOP_AT(5);
   {  // swarm margin: every lane's pair and the wave's level pair (the

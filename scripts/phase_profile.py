@@ -42,12 +42,19 @@ tot = d.sum(1)
 print(f"per-swarm cycles: mean {tot.mean():.0f}  median {np.median(tot):.0f}")
 for k, nm in enumerate(NAMES):
     print(f"  {nm:16s} mean {d[:, k].mean():10.0f}  share {d[:, k].sum() / tot.sum() * 100:5.1f}%")
-# alignment sub-phases: stamps 8 (pass 1 sums) and 9 (pass 2 cross sums)
-a1 = s[:, 8] - s[:, 1]
-a2 = s[:, 9] - s[:, 8]
-a3 = s[:, 2] - s[:, 9]
-for nm, x in (("  align pass 1", a1), ("  align pass 2", a2), ("  align finish", a3)):
-    print(f"  {nm:16s} mean {x.mean():10.0f}")
-sub = s[:, 10:14]
-for k, nm in enumerate(["  cbaa columns", "  cbaa selects", "  #dirty cols", "  #outbid"]):
-    print(f"  {nm:16s} mean {sub[:, k].mean():10.0f}")
+# CBAA column-step sections (a -DACL_AUCTION_PROF=1 build): cycles summed
+# over a swarm's waves, and the counts of evaluated columns, walks and scans
+sec = st.cpu().numpy()[:, 7:16].astype(np.uint64)
+if sec[:, :8].any():
+    SN = ["level 0", "levels", "margin bound", "runner-up walk", "exact scan", "write-back",
+          "selects+barrier", "column barrier"]
+    tot8 = sec[:, :8].astype(np.float64).sum()
+    for k, nm in enumerate(SN):
+        x = sec[:, k].astype(np.float64)
+        print(f"  cbaa {nm:16s} wave-cycles/swarm {x.mean():10.0f}  share {x.sum() / tot8 * 100:5.1f}%")
+    cnt = sec[:, 8]
+    cols = (cnt & np.uint64((1 << 21) - 1)).astype(np.float64)
+    walks = ((cnt >> np.uint64(21)) & np.uint64((1 << 21) - 1)).astype(np.float64)
+    scans = (cnt >> np.uint64(42)).astype(np.float64)
+    print(f"  per swarm: columns evaluated {cols.mean():.1f}, runner-up walks {walks.mean():.1f}, "
+          f"exact scans {scans.mean():.1f}")
