@@ -235,6 +235,14 @@ __device__ __forceinline__ void margin_track_u(float& hi, float& lo, float h, fl
   lo = tie ? 1.0f : (up ? l : lo);
 }
 
+// a per-lane flag held as a VGPR integer (0 or 1)
+__device__ __forceinline__ unsigned vflag(bool x) {
+  unsigned v = x ? 1u : 0u;
+  asm volatile("" : "+v"(v));
+  return v;
+}
+enum { FL_OB = 0, FL_DIRTY = 2, FL_CH = 4 };
+
 __device__ __forceinline__ bool lanebit(unsigned long long m) {
   return __builtin_amdgcn_inverse_ballot_w64(m);
 }
@@ -689,6 +697,11 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   // the wave's uniform margin pair over the level-resolved evaluations
   float uhi = 1.0f, ulo = 0.0f;
   int eff = 0;
+  // per-lane flags (FL_*) published once per wave and phase instead of
+  // atomics per column and per re-select: FL_OB << c = vehicle lane + 64 c
+  // outbid, FL_DIRTY << w = column 64 w + lane dirty next round, FL_CH = a
+  // column changed this round
+  unsigned fl = 0u;
   SecProf sp;
   sp.start();
   const int max_rounds = 2 * n;  // cbaa_max_iter_ = n * diameter (:50-51)
@@ -735,19 +748,14 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           key[c] = entry_key(C, n, wu[c], j) & okk[c];
           nw[c] = wu[c];
         }
-        // level 0: the column's highest price key, its holders and `who`.
-        // A column whose every entry is that one (price, who) is a fixed
-        // point with no runner-up: nothing to do (a third of the dirty
-        // columns: the round after the last vehicles adopted an entry).
+        // level 0: the column's highest price key, its holders and `who`
         unsigned M0 = level_key<NC>(key, 0xFFFFFFFFu);
         unsigned long long h[NC];
         int cum = 0;
-        bool full = true;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           h[c] = __ballot(key[c] == M0);
           cum += __popcll(h[c]);
-          full = full && h[c] == okm[c];
         }
         int wk = first_who<NC>(h, wu);
         unsigned long long tie = 0ull;
@@ -761,10 +769,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
 #ifdef ACL_CAL_SALU
         { int dmy; asm volatile(".rept 20\n\ts_mov_b32 %0, 0\n\t.endr" : "=s"(dmy)); }
 #endif
-        if (full && !tie && !nonfinite) {
-          sp.mark(PS_L0);
-          continue;
-        }
+        // (no fast exit for a column holding one (price, who) everywhere: the
+        // uniform-column rule below keeps such columns out of the dirty set,
+        // so the test cost more than it saved; the levels resolve it exactly)
         sp.mark(PS_L0);
         // winners, level by level. Per-vehicle state as lane masks: U = not
         // yet resolved, Nd = exact scan. Each resolving level's successor
@@ -899,8 +906,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           // (lanes past n store to a dummy row: no branch, see margin_track_sel)
           smem[okv[c] ? L.T + rowa[c] + j : L.dummy + lane] = (unsigned char)nw[c];
           const int u = lane + 64 * c;
-          const unsigned long long ob = __ballot(okv[c] && wu[c] == u && nw[c] != u);
-          if (ob && lane == 0) atomicOr(&obm[2 * par + c], ob);  // outbid (auctioneer.cpp:502)
+          fl |= (vflag(okv[c]) & vflag(wu[c] == u) & vflag(nw[c] != u)) << c;
           ch |= __ballot(nw[c] != wu[c]);
           mixed |= __ballot(okv[c] && nw[c] != nw0);
         }
@@ -908,12 +914,17 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         // neighbourhood sees one (price, who)) with no runner-up: it is not
         // dirty next round unless a re-select writes it (which marks it).
         // The change itself still counts for eff_rounds.
-        if (ch && lane == 0) {
-          misc[A_RCH + par] = 1;
-          if (mixed || nonfinite) atomicOr(&dmask[2 * npar + (j >> 6)], 1ull << (j & 63));
+        if (ch) {
+          fl |= 1u << FL_CH;
+          if (mixed || nonfinite) fl |= vflag(lane == (j & 63)) << (FL_DIRTY + (j >> 6));
         }
         sp.mark(PS_WB);
       }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {  // publish the outbid vehicles
+      const unsigned long long ob = __ballot((fl >> c) & 1u);
+      if (ob && lane == 0) atomicOr(&obm[2 * par + c], ob);
     }
     {
       // publish this wave's smallest gap so far (its lanes' select and scan
@@ -945,13 +956,18 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           const int v = 64 * c + __ffsll((long long)mv) - 1;
           mv &= mv - 1;
           const int task = wave_select<NC>(n, TS, v, lane, C, T, false, mp);
-          if (task >= 0 && lane == 0) {
-            T[v * TS + task] = (unsigned char)v;
-            atomicOr(&dmask[2 * npar + (task >> 6)], 1ull << (task & 63));
-          }
+          smem[(task >= 0 && lane == 0) ? L.T + v * TS + task : L.dummy + lane] = (unsigned char)v;
+          fl |= (vflag(task >= 0) & vflag(lane == (task & 63))) << (FL_DIRTY + (task >> 6));
         }
       }
     }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {  // publish next round's dirty columns
+      const unsigned long long dm = __ballot((fl >> (FL_DIRTY + c)) & 1u);
+      if (dm && lane == 0) atomicOr(&dmask[2 * npar + c], dm);
+    }
+    if (__any((fl >> FL_CH) & 1u) && lane == 0) misc[A_RCH + par] = 1;
+    fl = 0u;
     __syncthreads();
     sp.mark(PS_SEL);
     // a re-select always changes an entry; columns that changed but became

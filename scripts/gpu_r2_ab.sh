@@ -9,4 +9,4 @@ if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_ab.log 2>&1 || { echo "parity failed"; grep -E "FAIL|Error|error" gpurun_out/pytest_ab.log | head -20; tail -40 gpurun_out/pytest_ab.log; exit 1; }
   tail -3 gpurun_out/pytest_ab.log
 fi
-[ $# -gt 0 ] && scripts/gpu_auction_ab.sh "$@"
+if [ $# -gt 0 ]; then scripts/gpu_auction_ab.sh "$@"; fi
