@@ -641,8 +641,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
       const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
       const double dx = qv[0] - ax, dy = qv[1] - ay, dz = qv[2] - az;
-      const double nrm = sqrt((dx * dx + dy * dy) + dz * dz);
-      const float c = (float)(1.0 / (nrm + 1e-8));
+      const float c = acl_price((dx * dx + dy * dy) + dz * dz);  // bit-exact, see common.h
       C[v * n + j] = c;
       nonfin |= (c != c);
     }
@@ -1104,6 +1103,16 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   stamp_phase(P, b, tid, 6);
 }
 
+// test hook: acl_price (fast path) and the IEEE expression for m squared
+// distances (tests/test_gpu_prices.py)
+__global__ void price_sweep_kernel(const double* x, float* fast, float* ieee, int m) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) {
+    fast[i] = acl_price(x[i]);
+    ieee[i] = (float)(1.0 / (sqrt(x[i]) + 1e-8));
+  }
+}
+
 hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream) {
   const ALayout L = make_alayout(P.n);
   static bool configured = false;
@@ -1127,3 +1136,10 @@ hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream) {
 }
 
 }  // namespace acl_amd
+
+extern "C" int acl_internal_price_sweep(const double* x, float* fast, float* ieee, int m) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(acl_amd::price_sweep_kernel, dim3((m + 255) / 256), dim3(256), 0, 0, x, fast,
+                     ieee, m);
+  return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}

@@ -279,6 +279,25 @@ __device__ __forceinline__ double acl_atan_k32(double x, const double* tab) {
   return (ax == __builtin_inf()) ? copysign(1.57079632679489655800e+00, x) : copysign(res, x);
 }
 
+// getPrice (auctioneer.cpp:546-549) from the squared distance x:
+// (float)(1.0 / (sqrt(x) + 1e-8)) with IEEE sqrt and division, bit for bit.
+// The fast path computes y = 1 / (sqrt(x) + 1e-8) with sqrt_nr and div_nr
+// (a few ulp of the exact double in all) and rounds it to float; that float
+// is the exact one unless a float rounding boundary (a midpoint between two
+// floats) lies within the error: the 29 mantissa bits the float drops are
+// then within 1024 ulp of their midpoint 2^28, and those lanes (about 4e-6
+// of them) -- and every x outside [1e-200, 1e60] (zero, subnormal results,
+// float underflow, inf, NaN) -- take the IEEE expression. `tests/
+// test_gpu_prices.py` sweeps it against the IEEE expression on the GPU.
+__device__ __forceinline__ float acl_price(double x) {
+  const double y = div_nr(1.0, sqrt_nr(x) + 1e-8);
+  const unsigned r = (unsigned)((unsigned long long)__double_as_longlong(y) & ((1ull << 29) - 1ull));
+  const bool fast = x > 1e-200 && x < 1e60 && (r - (1u << 28) + 1024u) > 2048u;
+  float c = (float)y;
+  if (!fast) c = (float)(1.0 / (sqrt(x) + 1e-8));
+  return c;
+}
+
 __device__ __forceinline__ double wrap_to_pi(double a) {  // utils.h:275-280
   if (a > kPi) return a - 2 * kPi;
   if (a < -kPi) return a + 2 * kPi;

@@ -344,8 +344,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
           const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
           const double dx = qv[0] - ax, dy = qv[1] - ay, dz = qv[2] - az;
-          const double nrm = sqrt((dx * dx + dy * dy) + dz * dz);
-          const float cpr = (float)(1.0 / (nrm + 1e-8));
+          const float cpr = acl_price((dx * dx + dy * dy) + dz * dz);  // bit-exact (common.h)
           tile[vv * 65 + jj] = cpr;
           C[(size_t)v * n + j] = cpr;
           nonfin |= (cpr != cpr);
