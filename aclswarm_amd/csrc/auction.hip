@@ -431,9 +431,25 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   stamp_phase(P, b, tid, 0);
 
   // ---------------- phase 0: load ------------------------------------------
+  // Every global read of the phase is issued up front (one HBM round trip,
+  // not three): thread v < n (n <= kAB) holds P_in[v] and q[v] in registers
+  // until the permutation check can run.
+  const bool hv = tid < n;
+  unsigned pvr = 0u;
+  double qx = 0.0, qy = 0.0, qz = 0.0;
+  if (hv) {
+    pvr = P.P_in[(size_t)b * n + tid];
+    const double* qv = P.q + ((size_t)b * n + tid) * 3;
+    qx = qv[0]; qy = qv[1]; qz = qv[2];
+  }
   {
     const double* gp = P.p + (size_t)f * n * 3;
-    for (int k = tid; k < 3 * n; k += kAB) p[k] = gp[k];
+    for (int k = tid; k < 3 * n; k += kAB) {
+      const double x = gp[k];
+      p[k] = x;
+      const int j = k / 3, comp = k - 3 * j;
+      if (comp < 2) pq[4 * j + comp] = x;  // pq[j] = {p_j.xy, qf_j.xy}
+    }
     const uint64_t* ga = P.adj + (size_t)f * n * NC;
     for (int k = tid; k < 2 * n; k += kAB) {
       const int i = k >> 1, w = k & 1;
@@ -455,8 +471,10 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     if (fbad) misc[M_BAD] = 1;
     *margw = (unsigned long long)__double_as_longlong(1.0);
   }
-  for (int v = tid; v < n; v += kAB) {
-    const unsigned pv = P.P_in[(size_t)b * n + v];
+  if (hv) {
+    // the permutation check; q in formation order: qf[P_in[v]] = q[v]
+    const int v = tid;
+    const unsigned pv = pvr;
     Pin[v] = (unsigned char)pv;
     if (pv >= (unsigned)n) {
       misc[M_BAD] = 1;
@@ -464,6 +482,8 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       const unsigned long long bit = 1ull << (pv & 63);
       if (atomicOr(&H[8 + (pv >> 6)], bit) & bit) misc[M_BAD] = 1;  // not a permutation
       Ptin[pv] = (unsigned char)v;
+      qf[3 * pv] = qx; qf[3 * pv + 1] = qy; qf[3 * pv + 2] = qz;
+      pq[4 * pv + 2] = qx; pq[4 * pv + 3] = qy;
     }
   }
   __syncthreads();
@@ -488,17 +508,6 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       P.status[b] = st;
     }
     return;
-  }
-  // q in formation order: qf[j] = q[Pt[j]]; pq[j] = {p_j.xy, qf_j.xy}
-  {
-    const double* gq = P.q + (size_t)b * n * 3;
-    for (int j = tid; j < n; j += kAB) {
-      const double* qv = gq + 3 * Ptin[j];
-      const double x = qv[0], y = qv[1], z = qv[2];
-      qf[3 * j] = x; qf[3 * j + 1] = y; qf[3 * j + 2] = z;
-      double* o = pq + 4 * j;
-      o[0] = p[3 * j]; o[1] = p[3 * j + 1]; o[2] = x; o[3] = y;
-    }
   }
   // closed neighbourhoods in vehicle space (bidIterComplete, auctioneer.cpp:
   // 419-437): u ~ v iff u == v or adj(P[v], P[u])
