@@ -12,9 +12,11 @@
 // Symmetric jobs (SYM: D symmetric in exact arithmetic, square) compute only
 // the tiles on and above the diagonal and store each off-diagonal one twice.
 //
-// Tiling: a 64 x 64 (or 32 x 32) output tile per 256-thread workgroup, four
-// waves in a 2 x 2 arrangement, each wave 2 x 2 (1 x 1) MFMA 16x16 tiles; K staged through LDS in
-// steps of 16 with a register-prefetched double buffer (one barrier per step).
+// Tiling (default): an 80 x 80 output tile per 256-thread workgroup, one wave
+// per SIMD, 25 MFMA 16x16 blocks split evenly over the four waves
+// (gemm80w4_f64_kernel); alternatives 64 x 64 / 32 x 32 (four waves in a 2 x 2
+// arrangement) and the 80 tile on five waves. K staged through LDS in steps of
+// 16 with a register-prefetched double buffer (one barrier per step).
 // The MFMA is issued with the operands swapped (it computes the tile of D^T),
 // so the accumulator's lane index runs along D's rows and every epilogue
 // load/store is a contiguous 128-byte column segment.
@@ -40,7 +42,7 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kGemmKStep = 16;
 #ifndef ACL_GEMM_TILE_DEFAULT
-#define ACL_GEMM_TILE_DEFAULT 80
+#define ACL_GEMM_TILE_DEFAULT 80  // the four-wave 80 tile
 #endif
 
 // op(A)[i][kk]: TA ? A[kk + i*lda] : A[i + kk*lda]
@@ -301,16 +303,171 @@ __global__ void __launch_bounds__(320) gemm80_f64_kernel(const GemmJob* __restri
     }
 }
 
-// Output tile per workgroup: 80 (default), 64 or 32 (ACLSWARM_AMD_GEMM_TILE).
-// Measured on C5 (N=100, F=1024) in round 1: 548 ms per batch with 64, 684 ms
-// with 32 (the 32-tile wave holds one accumulator: less padding, but
-// dependent MFMAs).
+// The 80 x 80 tile with four waves (256 threads), one per SIMD: five waves
+// put two of a workgroup's MFMA streams on one SIMD. Wave w owns row strip w
+// (five blocks), block (4, w) of strip 4, and block (4, 4) for the k rows of
+// its own k4 step (k4 = w in every K step of 16): 25 MFMAs per wave per K
+// step. The four partial (4, 4) accumulators are summed through LDS in wave
+// order after the K loop.
+template <bool TA, bool TB, bool SYM>
+__global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __restrict__ jobs,
+                                                            int njobs, int tm, int tiles,
+                                                            unsigned long long* flops) {
+  constexpr int TILE = 80, NB = 5, EPT = 5;  // 80 x 16 operands / 256 threads = 5
+  const int blk = blockIdx.x;
+  const int slot = blk >> 3;
+  const int job = (blk & 7) + 8 * (slot / tiles);
+  if (job >= njobs) return;
+  int t = slot % tiles, bi, bj;
+  if (SYM) {
+    bj = 0;
+    while (t > bj) { t -= bj + 1; ++bj; }
+    bi = t;
+  } else {
+    bi = t % tm;
+    bj = t / tm;
+  }
+  const GemmJob J = jobs[job];
+  if (J.skip && *J.skip) return;
+  const int m0 = bi * TILE, n0 = bj * TILE;
+  if (m0 >= J.m || n0 >= J.n) return;
+  if (flops && threadIdx.x == 0)
+    atomicAdd(flops, 2ull * (unsigned long long)min(TILE, J.m - m0) *
+                         (unsigned long long)min(TILE, J.n - n0) * (unsigned long long)J.k);
+  constexpr bool AT = TA, BT = !TB;  // staged i-major (k contiguous in memory)
+  constexpr int KM = TILE, IM = 18;
+  constexpr int SZ = TILE * IM;
+  __shared__ double Ash[2][SZ];
+  __shared__ double Bsh[2][SZ];
+  auto a_at = [&](int buf, int kk, int i) -> double& {
+    return AT ? Ash[buf][i * IM + kk] : Ash[buf][kk * KM + i];
+  };
+  auto b_at = [&](int buf, int kk, int j) -> double& {
+    return BT ? Bsh[buf][j * IM + kk] : Bsh[buf][kk * KM + j];
+  };
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  double ra[EPT], rb[EPT];
+  auto a_idx = [&](int r, int& i, int& kk) {
+    const int e = tid + 256 * r;
+    if (!TA) { i = e % TILE; kk = e / TILE; }
+    else     { kk = e & 15; i = e >> 4; }
+  };
+  auto b_idx = [&](int r, int& j, int& kb) {
+    const int e = tid + 256 * r;
+    if (TB) { j = e % TILE; kb = e / TILE; }
+    else    { kb = e & 15; j = e >> 4; }
+  };
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < EPT; ++r) {
+      int i, kk;
+      a_idx(r, i, kk);
+      const int gi = m0 + i, gk = k0 + kk;
+      ra[r] = (gi < J.m && gk < J.k)
+                  ? (TA ? J.A[gk + (size_t)gi * J.lda] : J.A[gi + (size_t)gk * J.lda])
+                  : 0.0;
+      int j, kb;
+      b_idx(r, j, kb);
+      const int gj = n0 + j, gkb = k0 + kb;
+      rb[r] = (gj < J.n && gkb < J.k)
+                  ? (TB ? J.B[gj + (size_t)gkb * J.ldb] : J.B[gkb + (size_t)gj * J.ldb])
+                  : 0.0;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < EPT; ++r) {
+      int i, kk;
+      a_idx(r, i, kk);
+      a_at(buf, kk, i) = ra[r];
+      int j, kb;
+      b_idx(r, j, kb);
+      b_at(buf, kb, j) = rb[r];
+    }
+  };
+  f64x4 acc[NB], acc4w = f64x4{0.0, 0.0, 0.0, 0.0}, acc44 = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[b] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const int nk = (J.k + kGemmKStep - 1) / kGemmKStep;
+  if (nk > 0) {
+    load(0);
+    store(0);
+    __syncthreads();
+  }
+  for (int kb = 0; kb < nk; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nk) load((kb + 1) * kGemmKStep);
+#pragma unroll
+    for (int k4 = 0; k4 < kGemmKStep; k4 += 4) {
+      const int kr = k4 + (lane >> 4);
+      const double av = a_at(cur, kr, wave * 16 + (lane & 15));
+      const double a4 = a_at(cur, kr, 4 * 16 + (lane & 15));
+      double bv[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) bv[b] = b_at(cur, kr, b * 16 + (lane & 15));
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(bv[b], av, acc[b], 0, 0, 0);
+      // block (4, w): B column block w (a wave-uniform index: select, no
+      // dynamic register indexing)
+      double bw = bv[0];
+#pragma unroll
+      for (int b = 1; b < 4; ++b) bw = wave == b ? bv[b] : bw;
+      acc4w = __builtin_amdgcn_mfma_f64_16x16x4f64(bw, a4, acc4w, 0, 0, 0);
+      if (k4 == 4 * wave)  // block (4, 4) on this wave's k4 step
+        acc44 = __builtin_amdgcn_mfma_f64_16x16x4f64(bv[4], a4, acc44, 0, 0, 0);
+    }
+    if (kb + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+  }
+  // (4, 4): the four partial sums through LDS (the A buffer is free), added in
+  // wave order
+  double* red = &Ash[0][0];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[(wave * 4 + r) * 64 + lane] = acc44[r];
+  __syncthreads();
+  const double alpha = J.alpha, beta = J.beta;
+  auto put = [&](int si, int cb, int r, double a) {
+    const int gi = m0 + si * 16 + (lane & 15);
+    const int gj = n0 + cb * 16 + (lane >> 4) + 4 * r;
+    if (gi < J.m && gj < J.n) {
+      double v = alpha * a;
+      if (beta != 0.0) v += beta * J.C[gi + (size_t)gj * J.ldc];
+      J.D[gi + (size_t)gj * J.ldd] = v;
+      if (SYM && bi != bj) J.D[gj + (size_t)gi * J.ldd] = v;
+    }
+  };
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) put(wave, b, r, acc[b][r]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) put(4, wave, r, acc4w[r]);
+  if (wave == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double x = red[(0 * 4 + r) * 64 + lane];
+      x += red[(1 * 4 + r) * 64 + lane];
+      x += red[(2 * 4 + r) * 64 + lane];
+      x += red[(3 * 4 + r) * 64 + lane];
+      put(4, 4, r, x);
+    }
+  }
+}
+
+// Output tile per workgroup (ACLSWARM_AMD_GEMM_TILE): 80 (default: four
+// waves, gemm80w4_f64_kernel), 85 (the 80 tile on five waves,
+// gemm80_f64_kernel), 64 or 32. Measured on C5 (N=100, F=1024): 80 on four
+// waves 278 ms per batch, on five 325 ms, 64 338 ms.
+// Round 1 (before the symmetric products): 64 548 ms, 32 684 ms (the
+// 32-tile wave holds one accumulator: less padding, but dependent MFMAs).
 inline int gemm_tile() {
   static int t = 0;
   if (!t) {
     const char* e = getenv("ACLSWARM_AMD_GEMM_TILE");
     t = e ? atoi(e) : ACL_GEMM_TILE_DEFAULT;
-    if (t != 32 && t != 64 && t != 80) t = ACL_GEMM_TILE_DEFAULT;
+    if (t != 32 && t != 64 && t != 80 && t != 85) t = ACL_GEMM_TILE_DEFAULT;
   }
   return t;
 }
@@ -321,14 +478,17 @@ inline int gemm_tile() {
 inline hipError_t gemm_f64(bool ta, bool tb, const GemmJob* jobs, int njobs, int mmax, int nmax,
                            hipStream_t s, unsigned long long* flops = nullptr, bool sym = false) {
   if (njobs <= 0 || mmax <= 0 || nmax <= 0) return hipSuccess;
-  const int T = gemm_tile();
+  const int TT = gemm_tile(), T = TT == 85 ? 80 : TT;
   const int tm = (mmax + T - 1) / T, tn = (nmax + T - 1) / T;
   if (sym && tm != tn) return hipErrorInvalidValue;
   const int tiles = sym ? tm * (tm + 1) / 2 : tm * tn;
   const dim3 grid(8 * ((njobs + 7) / 8) * tiles);
 #define ACL_GEMM_LAUNCH2(TA_, TB_, SYM_)                                                   \
   do {                                                                                     \
-    if (T == 80)                                                                           \
+    if (TT == 80)                                                                          \
+      hipLaunchKernelGGL((gemm80w4_f64_kernel<TA_, TB_, SYM_>), grid, dim3(256), 0, s, jobs, \
+                         njobs, tm, tiles, flops);                                         \
+    else if (TT == 85)                                                                     \
       hipLaunchKernelGGL((gemm80_f64_kernel<TA_, TB_, SYM_>), grid, dim3(320), 0, s, jobs,  \
                          njobs, tm, tiles, flops);                                         \
     else if (T == 64)                                                                      \
