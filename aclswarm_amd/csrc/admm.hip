@@ -364,10 +364,17 @@ __global__ void __launch_bounds__(kT) chol_kernel(const Part* parts) {
     if (!kp && tid == 0) L[k + (size_t)k * K1] = 0.0;
     __syncthreads();
     if (kp) {
-      for (int j = k + 1; j < K1; ++j) {
+      // trailing update, every (i, j), k < j <= i, in one parallel pass (each
+      // element still takes its updates in k order: the same roundings as a
+      // column-by-column sweep, without its K1^2 / 2 serial steps)
+      const int m = K1 - k - 1;
+      for (int e = tid; e < m * m; e += kT) {
+        const int jj = e / m, ii = e - jj * m;
+        if (ii < jj) continue;
+        const int j = k + 1 + jj, i = k + 1 + ii;
         const double ljk = L[j + (size_t)k * K1];
         if (ljk == 0.0) continue;
-        for (int i = j + tid; i < K1; i += kT) L[i + (size_t)j * K1] -= L[i + (size_t)k * K1] * ljk;
+        L[i + (size_t)j * K1] -= L[i + (size_t)k * K1] * ljk;
       }
     }
     __syncthreads();
