@@ -879,6 +879,9 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       mx[kind][0] = std::max(mx[kind][0], j.m);
       mx[kind][1] = std::max(mx[kind][1], j.n);
     };
+    // the default GEMM kernel (the four-wave 80 tile) fuses nserr_kernel's
+    // |Y - I|_F^2 into the epilogue of the Newton-Schulz product Y = Z^2
+    const bool fuse_err = gemm_tile() == 80;
     for (int p = 0; p < NP; ++p) {
       const Part& P = hp[p];
       const int s = P.s, K = P.K, K1 = K + 1, np = P.np, n2 = 2 * s;
@@ -895,9 +898,11 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       add(J_GINV, {P.Gam, P.Gam, nullptr, P.Ginv, K1, K1, K1, K1, K1, K1, K1, 1.0, 0.0, nullptr});
       add(J_T, {P.Qa, P.Qbc, nullptr, P.T, s, s, K, std::max(K, 1), std::max(K, 1), s, s, 1.0, 0.0, nullptr});
       add(J_YK, {P.Qa, P.Pm, nullptr, P.Yk, K, s, s, std::max(K, 1), s, std::max(K, 1), std::max(K, 1), 1.0, 0.0, nullptr});
-      add(J_NSY0, {P.N0, P.N0, nullptr, P.Y, n2, n2, n2, n2, n2, n2, n2, 1.0, 0.0, nsd});
+      // (err2: the default GEMM kernel accumulates |Y - I|_F^2, nserr_kernel's sum)
+      double* e2 = fuse_err ? &P.sc->err2 : nullptr;
+      add(J_NSY0, {P.N0, P.N0, nullptr, P.Y, n2, n2, n2, n2, n2, n2, n2, 1.0, 0.0, nsd, e2});
       add(J_NSU0, {P.N0, P.Y, P.N0, P.N1, n2, n2, n2, n2, n2, n2, n2, -0.5, 1.5, nsd});
-      add(J_NSY1, {P.N1, P.N1, nullptr, P.Y, n2, n2, n2, n2, n2, n2, n2, 1.0, 0.0, nsd});
+      add(J_NSY1, {P.N1, P.N1, nullptr, P.Y, n2, n2, n2, n2, n2, n2, n2, 1.0, 0.0, nsd, e2});
       add(J_NSU1, {P.N1, P.Y, P.N1, P.N0, n2, n2, n2, n2, n2, n2, n2, -0.5, 1.5, nsd});
       add(J_S, {P.W, P.N0, P.W, P.Sr, n2, n2, n2, n2, n2, n2, n2, 0.5, 0.5, inact});
       add(J_A1, {P.Q, P.Sr, nullptr, P.A1, np, s, s, np, s, np, np, 1.0, 0.0, nullptr});
@@ -957,8 +962,9 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       for (int it = 0; it < kNsMax; ++it) {
         const bool odd = it & 1;
         ACL_HIP(gemm(odd ? J_NSY1 : J_NSY0, false, false), "gemm NS");
-        hipLaunchKernelGGL(nserr_kernel, dim3(std::min(grid1((long long)n2max * n2max), 64), NP),
-                           dim3(kT), 0, st, dp);
+        if (!fuse_err)
+          hipLaunchKernelGGL(nserr_kernel, dim3(std::min(grid1((long long)n2max * n2max), 64), NP),
+                             dim3(kT), 0, st, dp);
         ACL_HIP(gemm(odd ? J_NSU1 : J_NSU0, false, false), "gemm NS");
         hipLaunchKernelGGL(nsstep_kernel, dim3(1), dim3(1024), 0, st, dp, NP,
                            it == kNsMax - 1 ? 1 : 0, X.d_cnt);

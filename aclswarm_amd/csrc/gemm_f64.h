@@ -36,6 +36,7 @@ struct GemmJob {
   int lda, ldb, ldc, ldd;
   double alpha, beta;
   const int* skip;  // job skipped when non-NULL and *skip != 0
+  double* err2;     // non-NULL (default kernel only): += |D - I|_F^2 of the stored D
 };
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -428,6 +429,7 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
   for (int r = 0; r < 4; ++r) red[(wave * 4 + r) * 64 + lane] = acc44[r];
   __syncthreads();
   const double alpha = J.alpha, beta = J.beta;
+  double e2 = 0.0;  // |D - I|_F^2 of this wave's stored elements (J.err2)
   auto put = [&](int si, int cb, int r, double a) {
     const int gi = m0 + si * 16 + (lane & 15);
     const int gj = n0 + cb * 16 + (lane >> 4) + 4 * r;
@@ -436,6 +438,8 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
       if (beta != 0.0) v += beta * J.C[gi + (size_t)gj * J.ldc];
       J.D[gi + (size_t)gj * J.ldd] = v;
       if (SYM && bi != bj) J.D[gj + (size_t)gi * J.ldd] = v;
+      const double d = v - (gi == gj ? 1.0 : 0.0);
+      e2 += (SYM && bi != bj) ? 2.0 * (d * d) : d * d;
     }
   };
 #pragma unroll
@@ -453,6 +457,10 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
       x += red[(3 * 4 + r) * 64 + lane];
       put(4, 4, r, x);
     }
+  }
+  if (J.err2) {  // the Newton-Schulz error of Y = Z^2, fused (no pass over Y)
+    for (int o = 32; o > 0; o >>= 1) e2 += __shfl_xor(e2, o, 64);
+    if (lane == 0) atomicAdd(J.err2, e2);
   }
 }
 
