@@ -56,6 +56,8 @@ struct Info {  // written by basis_kernel
 struct Scal {
   double trM11, c0, nrm, err2, diff, tr22;
   int active, inactive, ns_done, ns_final, ns_upd, ns_fail, itr, pad;
+  int skip_s0, skip_s1;  // which S product runs: the sign is in N0 (even updates) or N1
+  int pad2[2];
 };
 
 struct Part {
@@ -619,13 +621,18 @@ __global__ void __launch_bounds__(1024) nsstep_kernel(const Part* parts, int npa
   if (threadIdx.x == 0) *remaining = cnt;
 }
 
-// the sign lives in N0 after an even number of updates, N1 after an odd one
-__global__ void __launch_bounds__(kT) nscopy_kernel(const Part* parts) {
-  const Part& P = parts[blockIdx.y];
-  if (!P.sc->active || !(P.sc->ns_upd & 1)) return;
-  const int n2 = 2 * P.s;
-  for (int e = blockIdx.x * kT + threadIdx.x; e < n2 * n2; e += gridDim.x * kT) P.N0[e] = P.N1[e];
+// the sign lives in N0 after an even number of updates, N1 after an odd one:
+// the S product of each part reads the one that holds it (two job lists,
+// each skipping the other parity's parts) instead of a copy N1 -> N0
+__global__ void __launch_bounds__(1024) nsparity_kernel(const Part* parts, int nparts) {
+  for (int p = threadIdx.x; p < nparts; p += blockDim.x) {
+    Scal& sc = *parts[p].sc;
+    const int odd = sc.ns_upd & 1;
+    sc.skip_s0 = (!sc.active || odd) ? 1 : 0;
+    sc.skip_s1 = (!sc.active || !odd) ? 1 : 0;
+  }
 }
+
 
 // S = sym(Sr), Sr = (W + W sign)/2 from the GEMM; X = (S - W)/mu;
 // sum |X_old - X|, tr X22.
@@ -869,7 +876,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     // ---- GEMM job lists
     enum {
       J_G, J_PRE1, J_PRE2, J_PIM1, J_PIM2, J_GINV, J_T, J_YK, J_NSY0, J_NSU0, J_NSY1, J_NSU1,
-      J_S, J_A1, J_AP, J_COUNT
+      J_S, J_S1, J_A1, J_AP, J_COUNT
     };
     std::vector<GemmJob> jobs((size_t)J_COUNT * NP);
     std::vector<int> njob(J_COUNT, 0);
@@ -885,7 +892,6 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     for (int p = 0; p < NP; ++p) {
       const Part& P = hp[p];
       const int s = P.s, K = P.K, K1 = K + 1, np = P.np, n2 = 2 * s;
-      const int* inact = &P.sc->inactive;
       const int* nsd = &P.sc->ns_done;
       add(J_G, {P.Q, P.Q, nullptr, P.G, np, np, s, np, np, np, np, 1.0, 0.0, nullptr});
       if (P.st) {
@@ -904,7 +910,8 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       add(J_NSU0, {P.N0, P.Y, P.N0, P.N1, n2, n2, n2, n2, n2, n2, n2, -0.5, 1.5, nsd});
       add(J_NSY1, {P.N1, P.N1, nullptr, P.Y, n2, n2, n2, n2, n2, n2, n2, 1.0, 0.0, nsd, e2});
       add(J_NSU1, {P.N1, P.Y, P.N1, P.N0, n2, n2, n2, n2, n2, n2, n2, -0.5, 1.5, nsd});
-      add(J_S, {P.W, P.N0, P.W, P.Sr, n2, n2, n2, n2, n2, n2, n2, 0.5, 0.5, inact});
+      add(J_S, {P.W, P.N0, P.W, P.Sr, n2, n2, n2, n2, n2, n2, n2, 0.5, 0.5, &P.sc->skip_s0});
+      add(J_S1, {P.W, P.N1, P.W, P.Sr, n2, n2, n2, n2, n2, n2, n2, 0.5, 0.5, &P.sc->skip_s1});
       add(J_A1, {P.Q, P.Sr, nullptr, P.A1, np, s, s, np, s, np, np, 1.0, 0.0, nullptr});
       add(J_AP, {P.A1, P.Q, nullptr, P.Ap, np, np, s, np, np, np, np, -1.0, 0.0, nullptr});
     }
@@ -920,7 +927,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     // Z^2 and Z Z^2 (polynomials in one symmetric Z commute), W sign(W)
     auto symk = [](int kind) {
       return kind == J_G || kind == J_NSY0 || kind == J_NSU0 || kind == J_NSY1 ||
-             kind == J_NSU1 || kind == J_S;
+             kind == J_NSU1 || kind == J_S || kind == J_S1;
     };
     auto gemm = [&](int kind, bool ta, bool tb) -> hipError_t {
       return gemm_f64(ta, tb, dj + (size_t)kind * NP, njob[kind], mx[kind][0], mx[kind][1], st,
@@ -975,8 +982,9 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
           if (*X.h_cnt == 0) break;
         }
       }
-      hipLaunchKernelGGL(nscopy_kernel, gW, dim3(kT), 0, st, dp);
+      hipLaunchKernelGGL(nsparity_kernel, dim3(1), dim3(1024), 0, st, dp, NP);
       ACL_HIP(gemm(J_S, false, false), "gemm S");
+      ACL_HIP(gemm(J_S1, false, false), "gemm S");
       hipLaunchKernelGGL(post_kernel, dim3(std::min(grid1((long long)n2max * n2max), 64), NP),
                          dim3(kT), 0, st, dp, mu);
       hipLaunchKernelGGL(check_kernel, dim3(1), dim3(1024), 0, st, dp, NP, prm.thresh,
