@@ -527,9 +527,13 @@ __global__ void __launch_bounds__(kT) w_kernel(const Part* parts, double mu) {
     }
     return w;
   };
+  // raw(j, i) == raw(i, j) bit for bit: S, Pm, hb and combine are symmetric
+  // element for element (each is built from symmetric operands by the same
+  // operations in the same order, or as 0.5 (a + b) of a transposed pair),
+  // so sym(raw) = 0.5 (x + x) = x exactly -- no transposed (uncoalesced) reads
   for (int e = blockIdx.x * kT + threadIdx.x; e < n2 * n2; e += gridDim.x * kT) {
     const int i = e % n2, j = e / n2;
-    P.W[e] = 0.5 * (raw(i, j) + raw(j, i));
+    P.W[e] = raw(i, j);
   }
 }
 
