@@ -640,7 +640,11 @@ __global__ void __launch_bounds__(1024) nsparity_kernel(const Part* parts, int n
 
 // S = sym(Sr), Sr = (W + W sign)/2 from the GEMM; X = (S - W)/mu;
 // sum |X_old - X|, tr X22.
-__global__ void __launch_bounds__(kT) post_kernel(const Part* parts, double mu) {
+// Sr comes from the symmetric GEMM path: a tile off the diagonal (tile size
+// `tile`) is stored mirrored, so there Sr_ji == Sr_ij and sym(Sr) = Sr bit for
+// bit; only the diagonal tiles (both triangles computed) need the transposed
+// read.
+__global__ void __launch_bounds__(kT) post_kernel(const Part* parts, double mu, int tile) {
   const Part& P = parts[blockIdx.y];
   if (!P.sc->active) return;
   const int s = P.s, n2 = 2 * s;
@@ -649,7 +653,8 @@ __global__ void __launch_bounds__(kT) post_kernel(const Part* parts, double mu) 
   const double imu = 1.0 / mu;
   for (int e = blockIdx.x * kT + threadIdx.x; e < n2 * n2; e += gridDim.x * kT) {
     const int i = e % n2, j = e / n2;
-    const double Sv = 0.5 * (P.Sr[e] + P.Sr[j + (size_t)i * n2]);
+    const double Sv = (i / tile != j / tile) ? P.Sr[e]
+                                             : 0.5 * (P.Sr[e] + P.Sr[j + (size_t)i * n2]);
     const double Xn = (Sv - P.W[e]) * imu;
     dsum += fabs(P.X[e] - Xn);
     if (i == j && i >= s) tr += Xn;
@@ -990,7 +995,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       ACL_HIP(gemm(J_S, false, false), "gemm S");
       ACL_HIP(gemm(J_S1, false, false), "gemm S");
       hipLaunchKernelGGL(post_kernel, dim3(std::min(grid1((long long)n2max * n2max), 64), NP),
-                         dim3(kT), 0, st, dp, mu);
+                         dim3(kT), 0, st, dp, mu, symk(J_S) ? gemm_tile_size() : (1 << 30));
       hipLaunchKernelGGL(check_kernel, dim3(1), dim3(1024), 0, st, dp, NP, prm.thresh,
                          prm.threshTr, X.d_cnt + 1);
       ACL_HIP(hipGetLastError(), "iteration kernels");

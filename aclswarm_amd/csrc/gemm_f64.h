@@ -480,6 +480,10 @@ inline int gemm_tile() {
   return t;
 }
 
+// output tile edge of the configured kernel (the symmetric path mirrors the
+// tiles off the diagonal: post-processing may rely on that)
+inline int gemm_tile_size() { return gemm_tile() == 85 ? 80 : gemm_tile(); }
+
 // Host launcher: `jobs` is a device array of `njobs` descriptors whose m, n
 // are bounded by mmax, nmax. sym: every job's D is symmetric in exact
 // arithmetic (and square): upper-triangle tiles only, mirrored.
