@@ -27,6 +27,8 @@
 
 namespace acl_amd {
 
+enum { W_RCH = 3 /* misc[3..4]: a column changed in a round of that parity */ };
+
 constexpr int kWBlock = 1024;
 constexpr int kWWaves = kWBlock / 64;
 constexpr int kWMaxW = kMaxNWide / 64;  // 64-bit words per bitmask row
@@ -498,7 +500,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           }
         }
         __builtin_amdgcn_wave_barrier();
-        bool ch = false;
+        bool ch = false, mx = false;
+        const unsigned nw0 = (unsigned)__builtin_amdgcn_readfirstlane((int)nw[0]);  // vehicle 0
 #pragma unroll
         for (int c = 0; c < kWMaxW; ++c) {
           const int u = lane + 64 * c;
@@ -508,9 +511,16 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
               __ballot(ok && wu[c] == (unsigned)u && nw[c] != (unsigned)u);
           if (ob && lane == 0) atomicOr(&obm[par * NW + c], ob);  // outbid (:502)
           ch |= nw[c] != wu[c];
+          mx |= ok && nw[c] != nw0;
         }
-        if (__ballot(ch) != 0ull && lane == 0)
-          atomicOr(&dmask[npar * NW + (j >> 6)], 1ull << (j & 63));
+        // a column left holding one `who` everywhere is a fixed point with no
+        // runner-up: not dirty next round unless a re-select writes it (as in
+        // auction.hip); the change still counts for eff_rounds
+        const bool anych = __ballot(ch) != 0ull, anymx = __ballot(mx) != 0ull;
+        if (anych && lane == 0) {
+          misc[W_RCH + par] = 1;
+          if (anymx || nonfinite) atomicOr(&dmask[npar * NW + (j >> 6)], 1ull << (j & 63));
+        }
       }
     }
     __syncthreads();
@@ -518,6 +528,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       dmask[par * NW + tid] = 0ull;
       obm[npar * NW + tid] = 0ull;
     }
+    if (tid == 0) misc[W_RCH + npar] = 0;  // round r+1's change flag (round r-1's was read)
     {
       int idx2 = 0;
       for (int w = 0; w < NW; ++w) {
@@ -535,10 +546,12 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       }
     }
     __syncthreads();
-    bool changed = false;
-    for (int w = 0; w < NW; ++w) changed |= dmask[npar * NW + w] != 0ull;
-    if (changed) eff = r;
-    else if (P.early_exit) break;
+    bool next = false;
+    for (int w = 0; w < NW; ++w) next |= dmask[npar * NW + w] != 0ull;
+    if (next || misc[W_RCH + par]) eff = r;
+    // no dirty column and no re-select: round r+1 changes nothing (the
+    // fixed point every later round repeats, with or without early_exit)
+    if (!next) break;
   }
 
   // swarm margin: min over every thread's CBAA pair and alignment gaps
