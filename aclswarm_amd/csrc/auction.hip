@@ -217,16 +217,6 @@ __device__ __forceinline__ double margin_gap_pair(float hi, float lo) {
   return margin_gap(m);
 }
 
-// margin_track (common.h) of a per-lane pair where `act`, branch-free: the
-// kernel is bound by the CU's scalar pipe, and a divergent branch costs three
-// scalar instructions (exec save, branch, restore) where selects cost none
-__device__ __forceinline__ void margin_track_sel(MarginPair& m, float hi, float lo, bool act) {
-  const bool eq = act && lo == hi;
-  const bool up = act && lo < hi && (double)lo * (double)m.hi > (double)m.lo * (double)hi;
-  m.hi = eq ? 1.0f : (up ? hi : m.hi);
-  m.lo = eq ? 1.0f : (up ? lo : m.lo);
-}
-
 // margin_track on a wave-uniform pair, branch-free (selects)
 __device__ __forceinline__ void margin_track_u(float& hi, float& lo, float h, float l) {
   const bool tie = l == h;

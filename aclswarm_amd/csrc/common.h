@@ -336,6 +336,16 @@ __device__ __forceinline__ void margin_track(MarginPair& m, float hi, float lo) 
   }
 }
 
+// margin_track of a per-lane pair where `act`, branch-free: the
+// kernel is bound by the CU's scalar pipe, and a divergent branch costs three
+// scalar instructions (exec save, branch, restore) where selects cost none
+__device__ __forceinline__ void margin_track_sel(MarginPair& m, float hi, float lo, bool act) {
+  const bool eq = act && lo == hi;
+  const bool up = act && lo < hi && (double)lo * (double)m.hi > (double)m.lo * (double)hi;
+  m.hi = eq ? 1.0f : (up ? hi : m.hi);
+  m.lo = eq ? 1.0f : (up ? lo : m.lo);
+}
+
 // gap of a tracked pair: (hi - lo) / hi in double (hi - lo exact there), 1
 // when lo < 2^-28 hi; monotone in the ratio, so min over gaps = gap of the
 // max-ratio pair

@@ -104,12 +104,16 @@ __device__ int wide_select(int n, int NW, int v, int lane, const float* C, const
   const float cmax = __uint_as_float(M);
 #pragma unroll
   for (int c = 0; c < kWMaxW; ++c) {
+    // branch-free (margin_track_sel, common.h): the selected task vs its
+    // price; an eligible task that lost vs the maximum; a task that would
+    // win if it became eligible vs its price
     const int j = lane + 64 * c;
-    if (!other[c]) continue;
-    if (j == js) margin_track(m, cvs[c], prs[c]);
-    else if (key[c] != 0u) margin_track(m, cmax, cvs[c]);
-    else if (cvs[c] > 0.0f && (js < 0 || cvs[c] > cmax || (cvs[c] == cmax && j < js)))
-      margin_track(m, prs[c], cvs[c]);
+    const bool isjs = other[c] && j == js;
+    const bool elig = other[c] && !isjs && key[c] != 0u;
+    const bool near = other[c] && !isjs && key[c] == 0u && cvs[c] > 0.0f &&
+                      (js < 0 || cvs[c] > cmax || (cvs[c] == cmax && j < js));
+    margin_track_sel(m, isjs ? cvs[c] : (elig ? cmax : prs[c]), isjs ? prs[c] : cvs[c],
+                     isjs || elig || near);
   }
   return js;
 }
