@@ -225,12 +225,6 @@ __device__ __forceinline__ void margin_track_u(float& hi, float& lo, float h, fl
   lo = tie ? 1.0f : (up ? l : lo);
 }
 
-// a per-lane flag held as a VGPR integer (0 or 1)
-__device__ __forceinline__ unsigned vflag(bool x) {
-  unsigned v = x ? 1u : 0u;
-  asm volatile("" : "+v"(v));
-  return v;
-}
 enum { FL_OB = 0, FL_DIRTY = 2, FL_CH = 4 };
 
 __device__ __forceinline__ bool lanebit(unsigned long long m) {

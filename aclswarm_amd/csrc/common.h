@@ -336,6 +336,16 @@ __device__ __forceinline__ void margin_track(MarginPair& m, float hi, float lo) 
   }
 }
 
+// a per-lane flag held as a VGPR integer (0 or 1), combined with bitwise
+// vector operations (the compiler would keep a divergent bool as an SGPR
+// lane mask combined by scalar instructions; the auction kernels are bound
+// by the CU's scalar pipe)
+__device__ __forceinline__ unsigned vflag(bool x) {
+  unsigned v = x ? 1u : 0u;
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // margin_track of a per-lane pair where `act`, branch-free: the
 // kernel is bound by the CU's scalar pipe, and a divergent branch costs three
 // scalar instructions (exec save, branch, restore) where selects cost none

@@ -380,6 +380,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   }
   __syncthreads();
   int eff = 0;
+  unsigned obf = 0u;  // per-lane outbid bits (bit c: vehicle lane + 64 c), one round
   const int max_rounds = 2 * n;
   for (int r = 1; r <= max_rounds; ++r) {
     const int par = r & 1, npar = par ^ 1;
@@ -511,9 +512,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           const int u = lane + 64 * c;
           const bool ok = c < NW && u < n;
           if (ok) T[(size_t)j * n + u] = (uint16_t)nw[c];
-          const unsigned long long ob =
-              __ballot(ok && wu[c] == (unsigned)u && nw[c] != (unsigned)u);
-          if (ob && lane == 0) atomicOr(&obm[par * NW + c], ob);  // outbid (:502)
+          // outbid (:502): a per-lane bit, published once per wave and round
+          obf |= (vflag(ok) & vflag(wu[c] == (unsigned)u) & vflag(nw[c] != (unsigned)u)) << c;
           ch |= nw[c] != wu[c];
           mx |= ok && nw[c] != nw0;
         }
@@ -527,6 +527,12 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         }
       }
     }
+#pragma unroll
+    for (int c = 0; c < kWMaxW; ++c) {
+      const unsigned long long ob = __ballot((obf >> c) & 1u);
+      if (ob && lane == 0) atomicOr(&obm[par * NW + c], ob);
+    }
+    obf = 0u;
     __syncthreads();
     if (tid < NW) {
       dmask[par * NW + tid] = 0ull;
