@@ -247,6 +247,9 @@ def main():
     ap.add_argument("--no-tile-gains", action="store_true",
                     help="pair kernel reads the row-major records instead of the "
                          "tile-ordered copy made at formation setup (acl_tile_gains)")
+    ap.add_argument("--graph", action="store_true",
+                    help="time the step (solve + device-side stats) as one captured HIP graph "
+                         "replayed per step (launch-bound configurations such as C2; one GPU)")
     ap.add_argument("--no-ca-probe", action="store_true",
                     help="skip the crowded (collision-avoidance) probe reported beside the headline")
     ap.add_argument("--dry-run", action="store_true",
@@ -342,6 +345,35 @@ def main():
     if lib.acl_internal_kernel_times(kms, kcnt) != 0:
         raise RuntimeError("kernel timing failed")
     lib.acl_internal_kernel_timing(0)
+    if args.graph and world == 1:
+        # the same step captured once into a HIP graph and replayed: the
+        # per-kernel times above come from the eager pass, the step time from
+        # the replays (no host launch overhead between the step's kernels)
+        gs = torch.cuda.Stream()  # (capture needs a non-default stream)
+        gs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(gs):  # one eager step on the capture stream first
+            engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], early_exit=not args.full_rounds,
+                         out=out, stream=gs.cuda_stream)
+            D.gather_results(out["P_out"], out["status"])
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=gs):
+            engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], early_exit=not args.full_rounds,
+                         out=out, stream=gs.cuda_stream)
+            gres = D.gather_results(out["P_out"], out["status"])
+        with torch.cuda.stream(gs):
+            graph.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(gs):
+            for k in range(args.steps):
+                evs[k][0].record(gs)
+                graph.replay()
+                evs[k][1].record(gs)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+        call_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        res = gres
     dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
@@ -476,6 +508,8 @@ def main():
             "edges_per_formation_avg": e_avg,
             "cbaa": "all 2N rounds" if args.full_rounds else "exact fixed-point exit",
             "parallelism": f"swarm-sharded x{world}",
+            "launch": ("one captured HIP graph per step (solve + device-side stats), replayed"
+                       if args.graph and world == 1 else "eager launches on one stream"),
             "gains": ("synthetic ADMM-structured blocks [a b 0; c d 0; 0 0 e] "
                       "(solver.cpp:49-77), 5-entry records = 40 B/edge" if w["planes"] == 5 else
                       "synthetic random 3x3 blocks, 9 planes = 72 B/edge"),

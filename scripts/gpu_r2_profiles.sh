@@ -12,9 +12,9 @@ mkdir -p $O
 case $CFG in
   c3) AARGS="--B 65536 --n 100" ;;
   c4) AARGS="--B 2048 --n 500 --L 90" ;;
-  c2) AARGS="--B 4096 --n 20 --L 15 --complete" ;;
+  c2) AARGS="--B 4096 --n 20 --L 15 --complete"; GRAPH=--graph ;;  # launch-bound: graph replay
 esac
-[ -n "$SKIP_BENCH" ] || timeout -k 10 600 python3 bench.py --config $CFG > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
+[ -n "$SKIP_BENCH" ] || timeout -k 10 600 python3 bench.py --config $CFG $GRAPH > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
 cat $O/bench.json
 rm -rf /tmp/kt_$CFG
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/kt_$CFG -o run --output-format csv -- \
