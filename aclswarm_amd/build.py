@@ -22,13 +22,50 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
          "-fPIC", "-shared", "-Wall", "-Wno-unused-function"]
 
 
+OBJ = os.path.join(ROOT, "build", "obj")
+
+
+def _headers():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hs.append(os.path.join(ROOT, "include", "aclswarm_amd.h"))
+    return hs
+
+
 def _stale():
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
-    deps.append(os.path.join(HERE, "..", "include", "aclswarm_amd.h"))
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + _headers()
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _compile_objects(force, verbose, extra=()):
+    """One hipcc per translation unit, in parallel (each TU launches its own
+    kernels: no relocatable device code); an object is rebuilt when its
+    source or any header is newer."""
+    from concurrent.futures import ThreadPoolExecutor
+    os.makedirs(OBJ, exist_ok=True)
+    hdr_t = max(os.path.getmtime(h) for h in _headers() if os.path.exists(h))
+    jobs, objs = [], []
+    for src in SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(OBJ, src + ".o")
+        objs.append(obj)
+        if (force or not os.path.exists(obj) or os.path.getmtime(obj) < max(
+                os.path.getmtime(path), hdr_t)):
+            flags = [f for f in FLAGS if f != "-shared"] + list(extra)
+            jobs.append([HIPCC] + flags + ["-c", path, "-o", obj + ".tmp"])
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+        os.replace(cmd[-1], cmd[-1][:-4])
+
+    with ThreadPoolExecutor(workers) as ex:
+        list(ex.map(run, jobs))
+    return objs
 
 
 def build_driver(force=False, verbose=False):
@@ -53,7 +90,8 @@ def build(force=False, verbose=False):
         build_driver(force, verbose)
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [HIPCC] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", OUT + ".tmp"]
+    objs = _compile_objects(force, verbose)
+    cmd = [HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared"] + objs + ["-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -968,8 +968,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     if (next || misc[A_RCH + par]) eff = r;
     // no dirty column and no re-select: round r+1 changes nothing, so round
     // r's table is the fixed point every later round repeats (SURVEY App.
-    // A.5) -- with or without early_exit, the outcome of all 2N rounds
-    if (!next) break;
+    // A.5): the outcome of all 2N rounds. early_exit = 0 still iterates the
+    // remaining (empty) rounds, the reference's literal schedule.
+    if (!next && P.early_exit) break;
   }
   sp.flush(P, b, lane);
   stamp_phase(P, b, tid, 4);
@@ -1108,16 +1109,17 @@ __global__ void price_sweep_kernel(const double* x, float* fast, float* ieee, in
 
 hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream) {
   const ALayout L = make_alayout(P.n);
-  static bool configured = false;
-  if (!configured) {
+  static PerDeviceOnce once;
+  const hipError_t ea = once.run([] {
     for (const void* k : {(const void*)auction_kernel<1, 128>, (const void*)auction_kernel<1, 256>,
                           (const void*)auction_kernel<2, 512>}) {
       const hipError_t e =
           hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
-    configured = true;
-  }
+    return hipSuccess;
+  });
+  if (ea != hipSuccess) return ea;
   // (64 threads for n <= 32 measured no faster at C2: 0.091 vs 0.088 ms)
   if (P.n <= 32)
     hipLaunchKernelGGL((auction_kernel<1, 128>), dim3(nb), dim3(128), L.total, stream, P);

@@ -229,6 +229,10 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
   if (tid < ACL_ATAB_N) atab[tid] = kAtanTab[tid / 6][tid % 6];
 #endif
 
+  // the gate-margin word: set before the barriers below, so that every
+  // wave's atomicMin after the edge loop follows it
+  __shared__ unsigned long long gmw;
+  if (GM && tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
   const int f = P.fidx[b];
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
   const bool uniform = P.wsMode[b] == 0;
@@ -277,8 +281,6 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
   __syncthreads();
 
   const int E = __builtin_amdgcn_readfirstlane(rowpre[n * NW]);
-  __shared__ unsigned long long gmw;
-  if (tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
   double gmxy = __builtin_inf(), gmz = __builtin_inf();
   const double* G = P.gains + NP * P.gain_off[f];
   // the formation's gains through one buffer resource (9 planes: plane k at
@@ -623,6 +625,8 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
 #else
   if (tid < ACL_ATAB_N) atab[tid] = kAtanTab[tid / 6][tid % 6];
 #endif
+  __shared__ unsigned long long gmw;  // gate margin: set before the barriers below
+  if (GM && tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
   const int f = P.fidx[b];
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
   {
@@ -673,8 +677,6 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
   __syncthreads();
 
   const int E = __builtin_amdgcn_readfirstlane(rowpre[n * NW]);
-  __shared__ unsigned long long gmw;
-  if (tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
   double gmxy = __builtin_inf(), gmz = __builtin_inf();
   const double* G = (tiled ? P.gains_tiled : P.gains) + 5 * P.gain_off[f];
   const __amdgpu_buffer_rsrc_t grs =
@@ -1255,22 +1257,17 @@ hipError_t launch_control_prep(const CtlParams& P, const uint16_t* Pgiven, int n
   return hipGetLastError();
 }
 
-// ACLSWARM_AMD_GAIN_PAIR=0 selects the directed walk (gain_kernel) for every
-// swarm (diagnostic A/B switch; read once).
-static bool gain_pair_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("ACLSWARM_AMD_GAIN_PAIR");
-    on = (e && e[0] == '0') ? 0 : 1;
-  }
-  return on != 0;
-}
+// ACL_GAIN_PAIR=0 (diagnostic builds only) selects the directed walk
+// (gain_kernel) for every swarm
+#ifndef ACL_GAIN_PAIR
+#define ACL_GAIN_PAIR 1
+#endif
 
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream) {
   if (which == 0) {
     CtlParams Q = P;
     Q.only_nonuniform = 0;
-    if (P.gain_planes == 5 && gain_pair_enabled()) {
+    if (P.gain_planes == 5 && ACL_GAIN_PAIR) {
       // uniform swarms: one evaluation per undirected edge; then gain_kernel
       // for the swarms whose vehicles hold different assignments
       const PairLayout PL = make_pair_layout(P.n);

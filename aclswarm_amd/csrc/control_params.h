@@ -6,9 +6,33 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/aclswarm_amd.h"
 
 namespace acl_amd {
+
+// One-time per-device setup (kernel attributes such as the 160 KiB dynamic
+// LDS limit are per device): f() runs once for each device it is called on,
+// under a mutex; a failure is returned and retried on the next call.
+class PerDeviceOnce {
+ public:
+  template <class F>
+  hipError_t run(F&& f) {
+    int d = 0;
+    hipError_t e = hipGetDevice(&d);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(m_);
+    if (d >= 0 && d < 64 && ((done_ >> d) & 1ull)) return hipSuccess;
+    e = f();
+    if (e == hipSuccess && d >= 0 && d < 64) done_ |= 1ull << d;
+    return e;
+  }
+
+ private:
+  std::mutex m_;
+  unsigned long long done_ = 0ull;
+};
 
 constexpr int kMaxN = 128;      // LDS-resident auction kernel (auction.hip)
 constexpr int kMaxNWide = 512;  // tables-in-HBM auction kernel (solve_wide.hip)

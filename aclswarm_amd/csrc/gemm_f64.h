@@ -464,25 +464,19 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
   }
 }
 
-// Output tile per workgroup (ACLSWARM_AMD_GEMM_TILE): 80 (default: four
-// waves, gemm80w4_f64_kernel), 85 (the 80 tile on five waves,
-// gemm80_f64_kernel), 64 or 32. Measured on C5 (N=100, F=1024): 80 on four
-// waves 278 ms per batch, on five 325 ms, 64 338 ms.
+// Output tile per workgroup (build-time ACL_GEMM_TILE_DEFAULT, diagnostic
+// builds only): 80 (default: four waves, gemm80w4_f64_kernel), 85 (the 80
+// tile on five waves, gemm80_f64_kernel), 64 or 32. Measured on C5 (N=100,
+// F=1024): 80 on four waves 278 ms per batch, on five 325 ms, 64 338 ms.
 // Round 1 (before the symmetric products): 64 548 ms, 32 684 ms (the
 // 32-tile wave holds one accumulator: less padding, but dependent MFMAs).
-inline int gemm_tile() {
-  static int t = 0;
-  if (!t) {
-    const char* e = getenv("ACLSWARM_AMD_GEMM_TILE");
-    t = e ? atoi(e) : ACL_GEMM_TILE_DEFAULT;
-    if (t != 32 && t != 64 && t != 80 && t != 85) t = ACL_GEMM_TILE_DEFAULT;
-  }
-  return t;
-}
+constexpr int gemm_tile() { return ACL_GEMM_TILE_DEFAULT; }
+static_assert(gemm_tile() == 32 || gemm_tile() == 64 || gemm_tile() == 80 || gemm_tile() == 85,
+              "ACL_GEMM_TILE_DEFAULT");
 
 // output tile edge of the configured kernel (the symmetric path mirrors the
 // tiles off the diagonal: post-processing may rely on that)
-inline int gemm_tile_size() { return gemm_tile() == 85 ? 80 : gemm_tile(); }
+constexpr int gemm_tile_size() { return gemm_tile() == 85 ? 80 : gemm_tile(); }
 
 // Host launcher: `jobs` is a device array of `njobs` descriptors whose m, n
 // are bounded by mmax, nmax. sym: every job's D is symmetric in exact

@@ -79,19 +79,6 @@ extern "C" int acl_internal_kernel_times(double* ms, int* count) {
   return 0;
 }
 
-// ACLSWARM_AMD_OVERLAP=k (experiment, read once): the batch in k chunks,
-// chunk i's gain kernel on a second stream after chunk i's auction, so the
-// HBM-bound gain stream fills CUs the issue-bound auction leaves idle at its
-// chunk tails; the caller's stream waits for the second one at the end.
-static int overlap_chunks() {
-  static int k = -1;
-  if (k < 0) {
-    const char* e = getenv("ACLSWARM_AMD_OVERLAP");
-    k = e ? atoi(e) : 0;
-    if (k < 0 || k > 64) k = 0;
-  }
-  return k;
-}
 namespace acl_amd {
 // acl_swarm_stats: one workgroup strides over the records (1 MB at B = 65536:
 // microseconds), LDS accumulators, then one thread writes every output.
@@ -155,9 +142,6 @@ extern "C" acl_status_t acl_swarm_stats(const acl_swarm_status_t* status, int32_
   return ACL_OK;
 }
 
-static acl_status_t solve_overlapped(const acl_formations_t* F, const acl_solve_args_t* a,
-                                     acl_amd::SolveParams P, hipStream_t s, int nchunk);
-
 extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_solve_args_t* a,
                                         void* stream) {
   using namespace acl_amd;
@@ -188,9 +172,6 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   P.gate_margin = a->do_control ? a->gate_margin : nullptr;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
-  const int nchunk = overlap_chunks();
-  if (nchunk > 1 && a->do_control && n <= kMaxN && a->B >= 2 * nchunk)
-    return solve_overlapped(F, a, P, s, nchunk);
   kt_record(0, 0, s);
   if (n <= kMaxN) {
     e = launch_auction(P, a->B, s);
@@ -296,65 +277,6 @@ extern "C" acl_status_t acl_tile_gains(const acl_formations_t* F, double* out, v
   if (out == F->gains) return acl__set_error("acl_tile_gains: out aliases gains");
   const hipError_t e = launch_tile_gains(F->n, F->n_formations, F->adj, F->gains, F->gain_off,
                                          out, (hipStream_t)stream);
-  if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
-  return ACL_OK;
-}
-
-static acl_status_t solve_overlapped(const acl_formations_t* F, const acl_solve_args_t* a,
-                                     acl_amd::SolveParams P, hipStream_t s, int nchunk) {
-  using namespace acl_amd;
-  static hipStream_t s2 = nullptr;
-  static hipEvent_t ev[65];
-  if (!s2) {
-    if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess)
-      return acl__set_error("hipStreamCreate failed");
-    for (int i = 0; i < 65; ++i)
-      if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
-        return acl__set_error("hipEventCreate failed");
-  }
-  const int n = F->n, B = a->B;
-  CtlParams C;
-  C.n = n; C.B = B; C.b0 = 0;
-  C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
-  C.gain_planes = F->gain_planes == 5 ? 5 : 9;
-  C.gains_tiled = (C.gain_planes == 5) ? F->gains_tiled : nullptr;
-  C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P_out;
-  C.status = a->status;
-  C.u = a->u ? a->u : reinterpret_cast<double*>(P.ws + P.W.u);
-  C.u_safe = a->u_safe; C.ca_flag = a->ca_flag;
-  C.wsPt = reinterpret_cast<const uint16_t*>(P.ws + P.W.pt);
-  C.wsMode = P.ws + P.W.mode;
-  C.wsRows = reinterpret_cast<const uint16_t*>(P.ws + P.W.rows);
-  C.ca_list = reinterpret_cast<unsigned*>(P.ws + P.W.calist);
-  C.ca_count = reinterpret_cast<unsigned*>(P.ws + P.W.cacount);
-  C.g = a->cntrl; C.s = a->safety;
-  C.only_nonuniform = 0;
-  C.all_uniform = 0;
-  C.F = F->n_formations;
-  C.gate_margin = a->gate_margin;
-  if (hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
-    return acl__set_error("hipMemsetAsync failed");
-  // s2 starts after everything the caller queued before this call
-  if (hipEventRecord(ev[64], s) != hipSuccess || hipStreamWaitEvent(s2, ev[64], 0) != hipSuccess)
-    return acl__set_error("hipEventRecord failed");
-  const int per = (B + nchunk - 1) / nchunk;
-  for (int i = 0; i < nchunk; ++i) {
-    const int b0 = i * per, nb = (B - b0 < per) ? B - b0 : per;
-    if (nb <= 0) break;
-    SolveParams Pi = P;
-    Pi.b0 = b0;
-    hipError_t e = launch_auction(Pi, nb, s);
-    if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
-    if (hipEventRecord(ev[i], s) != hipSuccess || hipStreamWaitEvent(s2, ev[i], 0) != hipSuccess)
-      return acl__set_error("hipEventRecord failed");
-    CtlParams Ci = C;
-    Ci.b0 = b0;
-    e = launch_control(Ci, nb, 0, s2);
-    if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
-  }
-  if (hipEventRecord(ev[64], s2) != hipSuccess || hipStreamWaitEvent(s, ev[64], 0) != hipSuccess)
-    return acl__set_error("hipEventRecord failed");
-  const hipError_t e = launch_control(C, B, 1, s);  // collision avoidance over the whole list
   if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
   return ACL_OK;
 }

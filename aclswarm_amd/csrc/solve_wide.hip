@@ -560,8 +560,9 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     for (int w = 0; w < NW; ++w) next |= dmask[npar * NW + w] != 0ull;
     if (next || misc[W_RCH + par]) eff = r;
     // no dirty column and no re-select: round r+1 changes nothing (the
-    // fixed point every later round repeats, with or without early_exit)
-    if (!next) break;
+    // fixed point every later round repeats); early_exit = 0 iterates the
+    // remaining (empty) rounds, the reference's literal schedule
+    if (!next && P.early_exit) break;
   }
 
   // swarm margin: min over every thread's CBAA pair and alignment gaps
@@ -653,14 +654,12 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
 
 hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream) {
   const WLayout L = make_wlayout(P.n);
-  static bool configured = false;
-  if (!configured) {
-    const hipError_t e = hipFuncSetAttribute((const void*)solve_wide_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             160 * 1024);
-    if (e != hipSuccess) return e;
-    configured = true;
-  }
+  static PerDeviceOnce once;
+  const hipError_t e = once.run([] {
+    return hipFuncSetAttribute((const void*)solve_wide_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(solve_wide_kernel, dim3(nb), dim3(kWBlock), L.total, stream, P);
   return hipGetLastError();
 }

@@ -210,10 +210,12 @@ def admm_design(pts, adj, params=None, stream=None):
     return out.transpose(1, 2), iters
 
 
-def control(table, fidx, q, vel, P, cntrl=None, safety=None, stream=None):
+def control(table, fidx, q, vel, P, cntrl=None, safety=None, want_gate_margin=False,
+            stream=None):
     """acl_control_batch: DistCntrl::compute + Safety for B swarms with given
     assignments P [B][n] (int16 holding uint16 bits). Returns u, u_safe,
-    ca_flag, status (device tensors)."""
+    ca_flag, status and, if requested (as in solve), gate_margin [B] f64
+    (device tensors)."""
     lib = L.lib()
     B, n = int(q.shape[0]), table.n
     dev = q.device
@@ -222,14 +224,15 @@ def control(table, fidx, q, vel, P, cntrl=None, safety=None, stream=None):
         "u_safe": torch.empty((B, n, 3), dtype=torch.float64, device=dev),
         "ca_flag": torch.empty((B, n), dtype=torch.uint8, device=dev),
         "status": torch.empty((B, 16), dtype=torch.uint8, device=dev),
-        "gate_margin": torch.empty(B, dtype=torch.float64, device=dev),
     }
+    if want_gate_margin:
+        out["gate_margin"] = torch.empty(B, dtype=torch.float64, device=dev)
     a = L.ControlArgs()
     a.B = B
     a.fidx = fidx.data_ptr(); a.q = q.data_ptr(); a.vel = vel.data_ptr(); a.P = P.data_ptr()
     a.u = out["u"].data_ptr(); a.u_safe = out["u_safe"].data_ptr()
     a.ca_flag = out["ca_flag"].data_ptr(); a.status = out["status"].data_ptr()
-    a.gate_margin = out["gate_margin"].data_ptr()
+    a.gate_margin = out["gate_margin"].data_ptr() if want_gate_margin else None
     a.workspace = workspace(n, B, dev).data_ptr()
     a.cntrl = cntrl or L.default_gains()
     a.safety = safety or L.default_safety()

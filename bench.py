@@ -16,7 +16,9 @@ rank solves its own B swarms (weak scaling, no exchange during the solve);
 launched directly with N > 1, this script starts the N ranks itself (child
 processes, before anything touches a GPU) and exits with rank 0's status.
 --config c2 / c4 run the other single-GPU shards (simform20 complete,
-B=4096; simform500, B=2048 per GPU = C4's 16384 over 8 GPUs).
+B=4096; simform500, B=2048 per GPU = C4's 16384 over 8 GPUs); --config c5
+the batched ADMM gain design (N=100, F=1024 formations per GPU, MFMA
+roofline, CPU restatement baseline).
 --dry-run exercises the launch + gather path on the CPU (gloo, synthetic
 outputs, no solve) for the multi-process tests.
 
@@ -46,7 +48,12 @@ CONFIGS = {
     "c4": dict(n=500, B=2048, L=90.0, complete=False,
                name="simform500_nc (config C4 shard: 2048 of 16384 swarms per GPU): "
                     "noncomplete random formation graphs, u16 vehicle indices"),
+    "c5": dict(n=100, B=1024, L=40.0, complete=False,
+               name="batched ADMM formation-gain design (config C5): N=100, F=1024 "
+                    "simform100 noncomplete formations per GPU"),
 }
+METRIC_C5 = "batched ADMM formation-gain designs/sec (N=100, F=1024); % fp64 MFMA roofline"
+FP64_MATRIX_PEAK_TF = 78.6  # MI355X fp64 matrix, AMD spec (the microarch guide has no fp64 row)
 
 
 def _free_port():
@@ -180,6 +187,127 @@ def cpu_baseline(w, out, budget_s, nthreads):
     }
 
 
+def cpu_baseline_admm(pts, adj, G, its, budget_s):
+    """The build's CPU ADMM restatement (oracle/admm_oracle.py: the
+    codegen's algebra, eigh-based PSD projection) on a bounded sample of the
+    same formations, one BLAS thread; checks the sample's gains and iteration
+    counts against the GPU."""
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import admm_oracle as AO
+
+    def note(msg):
+        print(f"[bench] cpu_baseline: {msg}", file=sys.stderr, flush=True)
+
+    F = pts.shape[0]
+    res, t = [], 0.0
+    with threadpool_limits(1):
+        for f in range(F):
+            note(f"ADMM formation {f} on 1 thread")
+            t0 = time.perf_counter()
+            A, it = AO.design_3d(pts[f].cpu().numpy(), adj[f].cpu().numpy())
+            t += time.perf_counter() - t0
+            res.append((A, it))
+            if t > budget_s:
+                break
+    S = len(res)
+    Gs = G[:S].cpu().numpy()
+    err = max(float(np.abs(Gs[k] - res[k][0]).max() / max(np.abs(res[k][0]).max(), 1e-300))
+              for k in range(S))
+    it_ok = all(tuple(int(x) for x in its[k].tolist()) == tuple(res[k][1]) for k in range(S))
+    return {"value": S / t, "unit": "formations/s", "cores": 1, "kind": "port",
+            "sample": f"the first {S} of the benchmark's formations (n={pts.shape[1]}) on one "
+                      "thread; CPU restatement oracle/admm_oracle.py (the codegen's ADMM "
+                      "algebra with a dense eigh PSD projection)",
+            "reference_codegen_s_per_formation": 41.9,
+            "parity_sample": {"formations": S, "gains_max_rel_err": err,
+                              "iterations_equal": it_ok}}
+
+
+def bench_c5(args, world, rank, local):
+    """Config C5: one step = one acl_admm_solve_batch over F formations per
+    GPU (formations shard across ranks; weak scaling)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from aclswarm_amd import _lib as L
+    from aclswarm_amd import engine, workload
+    cfg = CONFIGS["c5"]
+    n, F = cfg["n"], (args.B or cfg["B"])
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    pts, adjb = workload.reference_formations(F, n, cfg["L"], cfg["complete"], rank * F, dev)
+    adj = adjb.to(torch.float64)
+    torch.cuda.synchronize()
+    lib = L.lib()
+    # GEMM flops of one batch, counted on the device in an untimed pass
+    counter = torch.zeros(1, dtype=torch.int64, device=dev)
+    lib.acl_internal_admm_flop_counter(ctypes.c_void_p(counter.data_ptr()))
+    G, its = engine.admm_design(pts, adj)
+    torch.cuda.synchronize()
+    lib.acl_internal_admm_flop_counter(ctypes.c_void_p(0))
+    flops = float(counter.item())
+    for _ in range(max(0, args.warmup - 1)):
+        G, its = engine.admm_design(pts, adj)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        G, its = engine.admm_design(pts, adj)
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    batch_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt_max = float(dt_t.item())
+    itn = its.cpu()
+    ach = flops / (batch_ms * 1e-3) / 1e12
+    line = {
+        "metric": METRIC_C5, "value": world * F / dt_max, "unit": "formations/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt_max * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": cfg["name"],
+                   "formations": "the reference generator (generate_random_formation.py:59-80, "
+                                 f"L={cfg['L']:g}, h=2, min_dist=2, fc=False) after "
+                                 f"np.random.seed(s), s = {rank * F}..{rank * F + F - 1} per rank",
+                   "n": n, "F_per_gpu": F, "F_total": world * F,
+                   "parallelism": f"formation-sharded x{world}"},
+        "roofline": {"bound": "mfma", "scope": "batch",
+                     "what": "the batch's fp64 GEMM flops (counted per tile on the device, "
+                             "symmetric products as upper-triangle tiles) / batch time",
+                     "achieved": ach, "peak": FP64_MATRIX_PEAK_TF, "unit": "TFLOP/s",
+                     "frac": ach / FP64_MATRIX_PEAK_TF, "traffic": None,
+                     "gemm_flops_per_batch": flops, "batch_ms_events": batch_ms},
+        "iters_xy": {int(k): int(v) for k, v in zip(*torch.unique(itn[:, 0], return_counts=True))},
+        "iters_z": {int(k): int(v) for k, v in zip(*torch.unique(itn[:, 1], return_counts=True))},
+        "finite": bool(torch.isfinite(G).all().item()),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_admm(pts, adj, G, its, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
 def dry_run(args, world, rank):
     """CPU/gloo rehearsal of the multi-rank path: synthetic outputs of the
     configured shard size, the same gather and max-over-ranks timing; no
@@ -267,6 +395,8 @@ def main():
         return 2
     if args.dry_run:
         return dry_run(args, world, rank)
+    if args.config == "c5":
+        return bench_c5(args, world, rank, local)
 
     import numpy as np
     import torch
@@ -449,7 +579,7 @@ def main():
     a_all, g_all, s_all, e_avg = algorithmic_bytes(w, 0, B)
     per_launch = {"auction": a_all, "gain": g_all, "ca": s_all}
     gain_sym = ("acl_amd::gain_pair_kernel<%s, false>" % ("true" if t_tile is not None else "false")
-                if w["planes"] == 5 and os.environ.get("ACLSWARM_AMD_GAIN_PAIR", "1") != "0"
+                if w["planes"] == 5
                 else f"acl_amd::gain_kernel<{w['planes']}, false>")
     auction_sym = (("acl_amd::auction_kernel<1, 128>" if n <= 32 else
                     "acl_amd::auction_kernel<1, 256>" if n <= 64 else
@@ -482,6 +612,9 @@ def main():
                                            "ports": ports, "source": isrc}
     pipe_bytes = a_all + g_all + s_all
     pipe_ach = pipe_bytes / (call_ms * 1e-3) / 1e9
+    tr = [kern[k]["traffic"] for k in ("auction", "gain")]
+    pipe_traffic = sum(tr) if all(x is not None for x in tr) else None
+    pipe_traffic_src = kern["gain"]["traffic_source"] if pipe_traffic is not None else None
     gk = kern["gain"]
     line = {
         "metric": METRIC,
@@ -517,18 +650,21 @@ def main():
                             if t_tile is not None else "row-major records"),
         },
         "roofline": {
-            "bound": "hbm", "scope": "kernel", "kernel": gk["kernel"],
-            "achieved": gk["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": gk["frac"], "traffic": gk["traffic"], "traffic_source": gk["traffic_source"],
-            "avg_launch_ms": gk["avg_launch_ms"], "bytes_per_launch": gk["bytes_per_launch"],
-            "pipeline": {"what": "whole acl_solve_batch call (auction, gain, ca kernels): "
-                                 "algorithmic bytes / call time",
-                         "call_ms": call_ms, "bytes": pipe_bytes,
-                         "achieved_GBs": pipe_ach, "frac": pipe_ach / HBM_PEAK_GBS},
-            "note": "scope=kernel: the kernel that carries the HBM stream (the gain "
-                    "stream, nearly all algorithmic bytes); the auction kernel is "
-                    "LDS/VALU/SALU-issue bound (kernels.auction.issue); the whole "
-                    "call's HBM fraction is `pipeline.frac`",
+            "bound": "hbm", "scope": "pipeline",
+            "what": "whole acl_solve_batch call (every kernel of the solve): algorithmic "
+                    "bytes (SURVEY.md 8d, `kernels.*.bytes_per_launch`) / call time "
+                    "(HIP events on the solve's stream)",
+            "achieved": pipe_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": pipe_ach / HBM_PEAK_GBS,
+            "traffic": pipe_traffic, "traffic_source": pipe_traffic_src,
+            "call_ms": call_ms, "bytes_per_call": pipe_bytes,
+            "gain_kernel": {"kernel": gk["kernel"], "achieved": gk["achieved_GBs"],
+                            "frac": gk["frac"], "avg_launch_ms": gk["avg_launch_ms"],
+                            "bytes_per_launch": gk["bytes_per_launch"],
+                            "traffic": gk["traffic"], "traffic_source": gk["traffic_source"]},
+            "note": "frac is the whole call's HBM fraction (the north-star quantity); the "
+                    "gain stream carries nearly all algorithmic bytes (`gain_kernel`); the "
+                    "auction is LDS/VALU/SALU-issue bound (kernels.auction.issue)",
             "kernels": kern,
         },
         "setup": setup,

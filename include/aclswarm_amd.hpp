@@ -10,11 +10,17 @@
  *   admm::Solver      lib/admm/include/admm/        admm::Solver    -> acl_admm_solve_batch (F = 1)
  *                     solver.h:16-60
  *
- * Layouts are the reference's (column-major Eigen storage): PtsMat n x 3 f64,
- * AdjMat n x n u8, GainMat 3n x 3n f64, AssignmentPerm indices() (vehicle ->
- * formation point, u8). Every method takes plain pointers in those layouts;
- * when <Eigen/Dense> is available the Eigen-typed overloads with the
- * reference's exact signatures are compiled too (ACLSWARM_AMD_HAVE_EIGEN).
+ * Types are the reference's (utils.h:25-30): vehidx_t, GainMat, AdjMat,
+ * PtsMat, AssignmentVec, AssignmentPerm, and the methods carry the
+ * reference's exact signatures (getAssignment() returns an AssignmentPerm
+ * whose indices()(v) is vehicle v's formation point, DistCntrl::Formation
+ * holds AdjMat / GainMat / PtsMat / MatrixXd, compute returns a Vector3d).
+ * With <Eigen/Dense> they ARE the Eigen types (ACLSWARM_AMD_HAVE_EIGEN);
+ * without it a small in-tree column-major matrix and permutation
+ * (namespace mini below) provide the calls the reference's caller makes on
+ * them: .indices()(v), .transpose(), .data(), (i, j), .cast<T>(), .rows(),
+ * .cols(), .size(), isApprox, Map<const AssignmentVec>(ptr, n). Plain-pointer
+ * forms in the column-major layouts stay available under *ColMajor names.
  *
  * Semantics that differ from the reference, by design:
  *  - Auctioneer. In the reference every vehicle's object exchanges CBAA bids
@@ -51,6 +57,7 @@
 #include <cmath>
 #include <cstring>
 #include <functional>
+#include <algorithm>
 #include <iostream>
 #include <memory>
 #include <mutex>
@@ -72,6 +79,147 @@ namespace aclswarm {
 namespace amd {
 
 using vehidx_t = uint8_t;  // utils.h:25
+
+#ifndef ACLSWARM_AMD_HAVE_EIGEN
+// ----------------------------------------------------------------------------
+// Minimal stand-ins for the Eigen types of utils.h:25-30 when Eigen is absent:
+// column-major dense storage and a permutation with Eigen's conventions
+// (indices()(v) = the image of v; transpose() = the inverse).
+// ----------------------------------------------------------------------------
+namespace mini {
+
+template <class T>
+class Matrix {
+ public:
+  Matrix() = default;
+  Matrix(int rows, int cols) : r_(rows), c_(cols), d_((size_t)rows * cols, T()) {}
+  int rows() const { return r_; }
+  int cols() const { return c_; }
+  int size() const { return r_ * c_; }
+  T* data() { return d_.data(); }
+  const T* data() const { return d_.data(); }
+  T& operator()(int i, int j) { return d_[(size_t)j * r_ + i]; }
+  const T& operator()(int i, int j) const { return d_[(size_t)j * r_ + i]; }
+  T& operator()(int i) { return d_[(size_t)i]; }  // vectors (and linear index)
+  const T& operator()(int i) const { return d_[(size_t)i]; }
+  void resize(int rows, int cols) {
+    r_ = rows;
+    c_ = cols;
+    d_.assign((size_t)rows * cols, T());
+  }
+  void setZero() { std::fill(d_.begin(), d_.end(), T()); }
+  Matrix transpose() const {
+    Matrix t(c_, r_);
+    for (int j = 0; j < c_; ++j)
+      for (int i = 0; i < r_; ++i) t(j, i) = (*this)(i, j);
+    return t;
+  }
+  template <class U>
+  Matrix<U> cast() const {
+    Matrix<U> m(r_, c_);
+    for (int k = 0; k < size(); ++k) m.data()[k] = static_cast<U>(d_[(size_t)k]);
+    return m;
+  }
+  // exact equality stands in for Eigen's fuzzy compare (index vectors)
+  bool isApprox(const Matrix& o) const { return r_ == o.r_ && c_ == o.c_ && d_ == o.d_; }
+  bool operator==(const Matrix& o) const { return isApprox(o); }
+  static Matrix Zero(int rows, int cols) { return Matrix(rows, cols); }
+
+ private:
+  int r_ = 0, c_ = 0;
+  std::vector<T> d_;
+};
+
+// Eigen::Map<const AssignmentVec>(ptr, n): a read-only view copied on use
+template <class M>
+class Map;
+template <class T>
+class Map<const Matrix<T>> {
+ public:
+  Map(const T* p, size_t n) : p_(p), n_((int)n) {}
+  const T* data() const { return p_; }
+  int size() const { return n_; }
+
+ private:
+  const T* p_;
+  int n_;
+};
+
+class PermutationMatrix {
+ public:
+  using IndicesType = Matrix<vehidx_t>;
+  PermutationMatrix() = default;
+  explicit PermutationMatrix(int n) { setIdentity(n); }
+  explicit PermutationMatrix(const IndicesType& idx) : idx_(idx) {}
+  explicit PermutationMatrix(const Map<const IndicesType>& m) : idx_(m.size(), 1) {
+    for (int k = 0; k < m.size(); ++k) idx_(k) = m.data()[k];
+  }
+  void setIdentity(int n) {
+    idx_.resize(n, 1);
+    for (int k = 0; k < n; ++k) idx_(k) = (vehidx_t)k;
+  }
+  int size() const { return idx_.size(); }
+  int rows() const { return idx_.size(); }
+  int cols() const { return idx_.size(); }
+  IndicesType& indices() { return idx_; }
+  const IndicesType& indices() const { return idx_; }
+  PermutationMatrix transpose() const {  // the inverse
+    PermutationMatrix t(size());
+    for (int k = 0; k < size(); ++k) t.idx_(idx_(k)) = (vehidx_t)k;
+    return t;
+  }
+  PermutationMatrix inverse() const { return transpose(); }
+
+ private:
+  IndicesType idx_;
+};
+
+class Vector3d {
+ public:
+  Vector3d() : v_{0.0, 0.0, 0.0} {}
+  Vector3d(double x, double y, double z) : v_{x, y, z} {}
+  static Vector3d Zero() { return Vector3d(); }
+  double* data() { return v_; }
+  const double* data() const { return v_; }
+  double& operator()(int i) { return v_[i]; }
+  double operator()(int i) const { return v_[i]; }
+  double& x() { return v_[0]; }
+  double& y() { return v_[1]; }
+  double& z() { return v_[2]; }
+  double x() const { return v_[0]; }
+  double y() const { return v_[1]; }
+  double z() const { return v_[2]; }
+  int size() const { return 3; }
+
+ private:
+  double v_[3];
+};
+
+}  // namespace mini
+
+using GainMat = mini::Matrix<double>;
+using AdjMat = mini::Matrix<vehidx_t>;
+using PtsMat = mini::Matrix<double>;
+using AssignmentVec = mini::Matrix<vehidx_t>;
+using AssignmentPerm = mini::PermutationMatrix;
+using MatrixXd = mini::Matrix<double>;
+using Matrix3Xd = mini::Matrix<double>;
+using Vector3d = mini::Vector3d;
+template <class M>
+using Map = mini::Map<M>;
+#else
+// utils.h:25-30 exactly
+using GainMat = Eigen::MatrixXd;
+using AdjMat = Eigen::Matrix<vehidx_t, Eigen::Dynamic, Eigen::Dynamic>;
+using PtsMat = Eigen::Matrix<double, Eigen::Dynamic, 3>;
+using AssignmentVec = Eigen::Matrix<vehidx_t, Eigen::Dynamic, 1>;
+using AssignmentPerm = Eigen::PermutationMatrix<Eigen::Dynamic, Eigen::Dynamic, vehidx_t>;
+using MatrixXd = Eigen::MatrixXd;
+using Matrix3Xd = Eigen::Matrix<double, 3, Eigen::Dynamic>;
+using Vector3d = Eigen::Vector3d;
+template <class M>
+using Map = Eigen::Map<M>;
+#endif
 
 /* C callback of the new-assignment event: P (vehicle -> formation point). */
 typedef void (*acl_new_assignment_fn)(void* user, const vehidx_t* P, int32_t n);
@@ -176,13 +324,18 @@ inline std::vector<double> rows_xyz(int n, const double* colmajor) {
 
 class Auctioneer {
  public:
+  using AssignmentPerm = amd::AssignmentPerm;
+  using PtsMat = amd::PtsMat;
+  using AdjMat = amd::AdjMat;
   /* auctioneer.h:31-34 */
   struct Bid {
     std::vector<float> price;
     std::vector<int> who;
   };
+  using BidPtr = std::shared_ptr<Bid>;
   using BidConstPtr = std::shared_ptr<const Bid>;
 
+  /* auctioneer.cpp:13-22: assignment initialised to identity */
   Auctioneer(vehidx_t vehid, uint8_t n, bool verbose = false)
       : n_(n), vehid_(vehid), verbose_(verbose) {
     if (n_ < 1 || vehid_ >= n_) throw std::runtime_error("Auctioneer: vehid >= n");
@@ -191,13 +344,16 @@ class Auctioneer {
     for (int i = 0; i < n_; ++i) P_[i] = Pt_[i] = (vehidx_t)i;
   }
 
-  void setNewAssignmentHandler(std::function<void(const std::vector<vehidx_t>&)> f) {
+  /* auctioneer.h:59: the handler gets P (vehicle -> formation point) */
+  void setNewAssignmentHandler(std::function<void(const AssignmentPerm&)> f) {
     handler_ = std::move(f);
   }
   /* C callback form: f(user, P, n). */
   void setNewAssignmentHandler(acl_new_assignment_fn f, void* user) {
     if (!f) { handler_ = nullptr; return; }
-    handler_ = [f, user](const std::vector<vehidx_t>& P) { f(user, P.data(), (int32_t)P.size()); };
+    handler_ = [f, user](const AssignmentPerm& P) {
+      f(user, P.indices().data(), (int32_t)P.indices().size());
+    };
   }
   /* Stored, never invoked: bids do not leave the GPU (see file header). */
   void setSendBidHandler(std::function<void(uint32_t, uint32_t, const BidConstPtr&)> f) {
@@ -205,18 +361,29 @@ class Auctioneer {
   }
 
   /* auctioneer.cpp:42-61: new formation; assignment reset to identity and the
-   * next auction's result is adopted unconditionally. p column-major n x 3,
-   * adjmat column-major n x n. */
-  void setFormation(const double* p_colmajor, const uint8_t* adj_colmajor) {
+   * next auction's result is adopted unconditionally. */
+  void setFormation(const PtsMat& p, const AdjMat& adjmat) {
+    if (p.rows() != n_ || p.cols() != 3 || adjmat.rows() != n_ || adjmat.cols() != n_)
+      throw std::runtime_error("Auctioneer::setFormation: sizes do not match n");
+    setFormationColMajor(p.data(), adjmat.data());
+  }
+  /* p column-major n x 3, adjmat column-major n x n */
+  void setFormationColMajor(const double* p_colmajor, const uint8_t* adj_colmajor) {
     form_.upload(n_, p_colmajor, adj_colmajor, nullptr);
     auction_open_ = false;
     formation_just_received_ = true;
     for (int i = 0; i < n_; ++i) P_[i] = Pt_[i] = (vehidx_t)i;
   }
 
-  /* auctioneer.cpp:78-125 + 245-306: run the auction on snapshot q (column-
-   * major n x 3) to consensus and adopt this vehicle's result. */
-  void start(const double* q_colmajor) {
+  /* auctioneer.cpp:78-125 + 245-306: run the auction on snapshot q to
+   * consensus and adopt this vehicle's result. */
+  void start(const PtsMat& q) {
+    if (q.rows() != n_ || q.cols() != 3)
+      throw std::runtime_error("Auctioneer::start: q is not n x 3");
+    startColMajor(q.data());
+  }
+  /* q column-major n x 3 */
+  void startColMajor(const double* q_colmajor) {
     std::lock_guard<std::mutex> lock(auction_mtx_);
     if (form_.n != n_) throw std::runtime_error("Auctioneer::start before setFormation");
     auction_open_ = true;
@@ -273,10 +440,16 @@ class Auctioneer {
     invalid_assignment_ = false;
   }
 
-  /* P: vehicle -> formation point; Pt: formation point -> vehicle. */
-  std::vector<vehidx_t> getAssignment() const { return P_; }
-  std::vector<vehidx_t> getInvAssignment() const { return Pt_; }
-  void setAssignment(const vehidx_t* P) {
+  /* auctioneer.h:103-104: P (vehicle -> formation point), Pt = P^-1 */
+  AssignmentPerm getAssignment() const { return toPerm(P_); }
+  AssignmentPerm getInvAssignment() const { return toPerm(Pt_); }
+  /* auctioneer.h:107: the "backdoor" override, Pt = P^T */
+  void setAssignment(const AssignmentPerm& P) { setAssignmentIndices(P.indices().data()); }
+
+  /* the same as plain index vectors */
+  const std::vector<vehidx_t>& getAssignmentIndices() const { return P_; }
+  const std::vector<vehidx_t>& getInvAssignmentIndices() const { return Pt_; }
+  void setAssignmentIndices(const vehidx_t* P) {
     for (int i = 0; i < n_; ++i) {
       P_[i] = P[i];
       Pt_[P[i]] = (vehidx_t)i;
@@ -287,35 +460,13 @@ class Auctioneer {
   bool didConvergeOnInvalidAssignment() const { return invalid_assignment_; }
   int auctionId() const { return auctionid_; }
 
-#ifdef ACLSWARM_AMD_HAVE_EIGEN
-  using PtsMat = Eigen::Matrix<double, Eigen::Dynamic, 3>;
-  using AdjMat = Eigen::Matrix<vehidx_t, Eigen::Dynamic, Eigen::Dynamic>;
-  using AssignmentPerm = Eigen::PermutationMatrix<Eigen::Dynamic, Eigen::Dynamic, vehidx_t>;
-  void setNewAssignmentHandler(std::function<void(const AssignmentPerm&)> f) {
-    if (!f) { handler_ = nullptr; return; }
-    handler_ = [f](const std::vector<vehidx_t>& P) {
-      AssignmentPerm perm((int)P.size());
-      for (size_t i = 0; i < P.size(); ++i) perm.indices()(i) = P[i];
-      f(perm);
-    };
-  }
-  void setFormation(const PtsMat& p, const AdjMat& adjmat) {
-    setFormation(p.data(), adjmat.data());
-  }
-  void start(const PtsMat& q) { start(q.data()); }
-  AssignmentPerm getAssignmentPerm() const { return toPerm(P_); }
-  AssignmentPerm getInvAssignmentPerm() const { return toPerm(Pt_); }
-  void setAssignment(const AssignmentPerm& P) { setAssignment(P.indices().data()); }
-
  private:
   static AssignmentPerm toPerm(const std::vector<vehidx_t>& v) {
     AssignmentPerm perm((int)v.size());
-    for (size_t i = 0; i < v.size(); ++i) perm.indices()(i) = v[i];
+    for (size_t i = 0; i < v.size(); ++i) perm.indices()((int)i) = v[i];
     return perm;
   }
-#endif
 
- private:
   /* auctioneer.cpp:250-295 (adoption) and 310-321 (shouldUseAssignment). */
   void finish(const std::vector<uint16_t>& who) {
     const int n = n_;
@@ -342,7 +493,7 @@ class Auctioneer {
     if (!use) return;
     P_ = newP;
     Pt_ = newPt;
-    if (handler_) handler_(P_);
+    if (handler_) handler_(toPerm(P_));
   }
 
   int n_;
@@ -354,7 +505,7 @@ class Auctioneer {
   bool invalid_assignment_ = false;
   bool formation_just_received_ = false;
   std::mutex queue_mtx_, auction_mtx_;
-  std::function<void(const std::vector<vehidx_t>&)> handler_;
+  std::function<void(const AssignmentPerm&)> handler_;
   std::function<void(uint32_t, uint32_t, const BidConstPtr&)> send_bid_;
   detail::DeviceFormation form_;
   detail::DeviceBuffer d_q_, d_pin_, d_fidx_, d_pout_, d_status_, d_who_, d_ws_;
@@ -366,16 +517,18 @@ class Auctioneer {
 
 class DistCntrl {
  public:
-  /* distcntrl.h:26-34, plain layouts: adjmat column-major n x n u8, gains
-   * column-major 3n x 3n, qdes column-major n x 3; dstar_* column-major n x n
-   * (filled by setFormation as the reference does). */
+  using AssignmentPerm = amd::AssignmentPerm;
+  using PtsMat = amd::PtsMat;
+
+  /* distcntrl.h:26-34 (column-major Eigen storage); dstar_* are filled by
+   * setFormation as the reference does */
   struct Formation {
     std::string name;
-    std::vector<uint8_t> adjmat;
-    std::vector<double> gains;
-    std::vector<double> qdes;
-    std::vector<double> dstar_xy;
-    std::vector<double> dstar_z;
+    AdjMat adjmat;   // n x n
+    GainMat gains;   // 3n x 3n
+    PtsMat qdes;     // n x 3
+    MatrixXd dstar_xy;
+    MatrixXd dstar_z;
   };
 
   /* distcntrl.h:36-45 */
@@ -399,23 +552,34 @@ class DistCntrl {
    * (utils::pdistmat, utils.h:137-147) and uploads it. */
   void setFormation(const std::shared_ptr<Formation>& f) {
     const int n = n_;
-    if (!f || (int)f->qdes.size() != 3 * n || (int)f->adjmat.size() != n * n ||
-        f->gains.size() != (size_t)9 * n * n)
+    if (!f || f->qdes.rows() != n || f->qdes.cols() != 3 || f->adjmat.rows() != n ||
+        f->adjmat.cols() != n || f->gains.rows() != 3 * n || f->gains.cols() != 3 * n)
       throw std::runtime_error("DistCntrl::setFormation: formation sizes do not match n");
     formation_ = f;
-    pdist(f->qdes.data(), 0, 2, f->dstar_xy);
-    pdist(f->qdes.data(), 2, 3, f->dstar_z);
+    f->dstar_xy.resize(n, n);
+    f->dstar_z.resize(n, n);
+    pdist(f->qdes.data(), 0, 2, f->dstar_xy.data());
+    pdist(f->qdes.data(), 2, 3, f->dstar_z.data());
     form_.upload(n, f->qdes.data(), f->adjmat.data(), f->gains.data());
   }
 
-  /* distcntrl.cpp:38-41; P: vehicle -> formation point. */
-  void setAssignment(const vehidx_t* P) {
+  /* distcntrl.cpp:39-42; P: vehicle -> formation point. */
+  void setAssignment(const AssignmentPerm& P) { setAssignmentIndices(P.indices().data()); }
+  void setAssignmentIndices(const vehidx_t* P) {
     for (int i = 0; i < n_; ++i) P_[i] = P[i];
   }
 
   /* distcntrl.cpp:46-102: u for this vehicle from the snapshot q_veh
-   * (column-major n x 3, vehicle space) and its velocity vel[3]. */
-  void compute(const double* q_veh_colmajor, const double vel[3], double u[3]) {
+   * (vehicle space, n x 3) and its velocity. */
+  Vector3d compute(const PtsMat& q_veh, const Vector3d vel) {
+    if (q_veh.rows() != n_ || q_veh.cols() != 3)
+      throw std::runtime_error("DistCntrl::compute: q_veh is not n x 3");
+    Vector3d u;
+    computeColMajor(q_veh.data(), vel.data(), u.data());
+    return u;
+  }
+  /* q_veh column-major n x 3, vel[3] -> u[3] */
+  void computeColMajor(const double* q_veh_colmajor, const double vel[3], double u[3]) {
     if (!formation_) throw std::runtime_error("DistCntrl::compute before setFormation");
     const int n = n_;
     const std::vector<double> q = detail::rows_xyz(n, q_veh_colmajor);
@@ -449,26 +613,15 @@ class DistCntrl {
     detail::check(acl_stream_synchronize(nullptr));
   }
 
-#ifdef ACLSWARM_AMD_HAVE_EIGEN
-  using PtsMat = Eigen::Matrix<double, Eigen::Dynamic, 3>;
-  using AssignmentPerm = Eigen::PermutationMatrix<Eigen::Dynamic, Eigen::Dynamic, vehidx_t>;
-  void setAssignment(const AssignmentPerm& P) { setAssignment(P.indices().data()); }
-  Eigen::Vector3d compute(const PtsMat& q_veh, const Eigen::Vector3d vel) {
-    Eigen::Vector3d u;
-    compute(q_veh.data(), vel.data(), u.data());
-    return u;
-  }
-#endif
-
  private:
   // squareform(pdist(M)) over columns [c0, c1) of the n x 3 matrix, by the
-  // reference's |x|^2 + |y|^2 - 2 x'y identity (utils.h:140-146)
-  void pdist(const double* M, int c0, int c1, std::vector<double>& D) const {
+  // reference's |x|^2 + |y|^2 - 2 x'y identity (utils.h:140-146); D is n x n
+  // column-major
+  void pdist(const double* M, int c0, int c1, double* D) const {
     const int n = n_;
     std::vector<double> N(n, 0.0);
     for (int i = 0; i < n; ++i)
       for (int c = c0; c < c1; ++c) N[i] += M[(size_t)c * n + i] * M[(size_t)c * n + i];
-    D.assign((size_t)n * n, 0.0);
     for (int j = 0; j < n; ++j)
       for (int i = 0; i < n; ++i) {
         double dot = 0.0;
@@ -509,9 +662,19 @@ class Solver {
   Solver() : Solver(Params()) {}
   explicit Solver(const Params& params) : params_(params) {}
 
-  /* Gains for n points: pts column-major 3 x n, adj column-major n x n f64,
-   * gains out column-major 3n x 3n. */
-  void solve(int n, const double* pts_3xn, const double* adj_nxn, double* gains_out) {
+  /* solver.h:38: gains (3n x 3n) for the points (3 x n) and adjacency (n x n) */
+  MatrixXd solve(const Matrix3Xd& pts, const MatrixXd& adj) {
+    const int n = (int)pts.cols();
+    if (pts.rows() != 3 || adj.rows() != n || adj.cols() != n)
+      throw std::runtime_error("admm::Solver::solve: pts must be 3 x n and adj n x n");
+    MatrixXd A(3 * n, 3 * n);
+    solveColMajor(n, pts.data(), adj.data(), A.data());
+    return A;
+  }
+
+  /* pts column-major 3 x n, adj column-major n x n f64, gains out
+   * column-major 3n x 3n */
+  void solveColMajor(int n, const double* pts_3xn, const double* adj_nxn, double* gains_out) {
     if (n < 1) throw std::runtime_error("admm::Solver::solve: n < 1");
     acl_admm_params_t p;
     acl_default_admm_params(&p);
@@ -540,16 +703,6 @@ class Solver {
    * PSD projection's sign iteration did not converge (aclswarm_amd.h). */
   int iterations2d() const { return iters_[0]; }
   int iterations1d() const { return iters_[1]; }
-
-#ifdef ACLSWARM_AMD_HAVE_EIGEN
-  Eigen::MatrixXd solve(const Eigen::Matrix<double, 3, Eigen::Dynamic>& pts,
-                        const Eigen::MatrixXd& adj) {
-    const int n = (int)pts.cols();
-    Eigen::MatrixXd A(3 * n, 3 * n);
-    solve(n, pts.data(), adj.data(), A.data());
-    return A;
-  }
-#endif
 
  private:
   Params params_;

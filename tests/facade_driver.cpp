@@ -15,6 +15,7 @@
 //         f64 u[n][3]; i32 iters[2]; f64 A[9m^2] (column-major)
 #include <stdio.h>
 
+#include <functional>
 #include <memory>
 #include <vector>
 
@@ -31,9 +32,73 @@ static void wr(FILE* f, const T* p, size_t n) {
   if (n && fwrite(p, sizeof(T), n, f) != n) throw std::runtime_error("short write");
 }
 
-static void on_assignment(void* user, const amd::vehidx_t*, int32_t) {
-  ++*static_cast<int*>(user);
-}
+// A stand-in for CoordinationROS (coordination_ros.h/.cpp) holding the
+// facade objects under the reference's member names and using them with the
+// reference's own expressions (cited line by line), so this file compiles
+// only if the facade keeps the reference's types and signatures.
+struct Coordination {
+  amd::vehidx_t vehid_;
+  uint8_t n_;
+  std::unique_ptr<amd::Auctioneer> auctioneer_;
+  std::unique_ptr<amd::DistCntrl> controller_;
+  std::unique_ptr<amd::admm::Solver> admm_;
+  std::shared_ptr<amd::DistCntrl::Formation> formation_;
+  amd::AssignmentPerm Pcentral_;
+  int handler_calls = 0;
+  std::vector<amd::vehidx_t> neighbours;  // vehicles connectToNeighbors found
+
+  Coordination(amd::vehidx_t vehid, uint8_t n) : vehid_(vehid), n_(n) {
+    // coordination_ros.cpp:176-178
+    admm_.reset(new amd::admm::Solver());
+    controller_.reset(new amd::DistCntrl(vehid_, n_));
+    auctioneer_.reset(new amd::Auctioneer(vehid_, n_, false));
+    // coordination_ros.cpp:184-188 (std::bind of the member callbacks)
+    namespace ph = std::placeholders;
+    auctioneer_->setNewAssignmentHandler(
+        std::bind(&Coordination::newAssignmentCb, this, ph::_1));
+    auctioneer_->setSendBidHandler(
+        [](uint32_t, uint32_t, const amd::Auctioneer::BidConstPtr&) {});
+  }
+
+  // coordination_ros.cpp:110-129 (formationCb); gains solved only when none
+  // were given
+  void formationCb(std::shared_ptr<amd::DistCntrl::Formation> f) {
+    formation_ = std::move(f);
+    if (formation_->gains.size() == 0) {
+      formation_->gains = admm_->solve(formation_->qdes.transpose(),
+                                       formation_->adjmat.cast<double>());
+    }
+    controller_->setFormation(formation_);
+    auctioneer_->setFormation(formation_->qdes, formation_->adjmat);
+    connectToNeighbors();
+  }
+
+  // coordination_ros.cpp:272-279 (centralAssignmentCb)
+  bool centralAssignmentCb(const std::vector<uint8_t>& data) {
+    Pcentral_ = amd::AssignmentPerm(amd::Map<const amd::AssignmentVec>(data.data(),
+                                                                       data.size()));
+    bool assignment_changed =
+        !(Pcentral_.indices().isApprox(auctioneer_->getAssignment().indices()));
+    return assignment_changed;
+  }
+
+  // coordination_ros.cpp:283-290 (newAssignmentCb)
+  void newAssignmentCb(const amd::AssignmentPerm& P) {
+    controller_->setAssignment(P);
+    ++handler_calls;
+    connectToNeighbors();
+  }
+
+  // coordination_ros.cpp:392-410 (connectToNeighbors)
+  void connectToNeighbors() {
+    neighbours.clear();
+    const auto i = auctioneer_->getAssignment().indices()(vehid_);
+    for (size_t j = 0; j < n_; ++j) {
+      const auto j_vehid = auctioneer_->getInvAssignment().indices()(j);
+      if (formation_->adjmat(i, j)) neighbours.push_back(j_vehid);
+    }
+  }
+};
 
 extern "C" int facade_run(const char* in_path, const char* out_path) {
   try {
@@ -41,78 +106,92 @@ extern "C" int facade_run(const char* in_path, const char* out_path) {
     if (!in) throw std::runtime_error("cannot open input");
     int32_t n = 0, m = 0;
     rd(in, &n, 1);
-    std::vector<double> p(3 * n), gains((size_t)9 * n * n), q(3 * n), vel(3 * n);
-    std::vector<uint8_t> adj((size_t)n * n), Pin(n);
-    rd(in, p.data(), p.size());
-    rd(in, adj.data(), adj.size());
-    rd(in, gains.data(), gains.size());
-    rd(in, q.data(), q.size());
+    amd::PtsMat p(n, 3), q(n, 3);
+    amd::AdjMat adj(n, n);
+    amd::GainMat gains(3 * n, 3 * n);
+    std::vector<double> vel(3 * n);
+    std::vector<uint8_t> Pin(n);
+    rd(in, p.data(), (size_t)3 * n);
+    rd(in, adj.data(), (size_t)n * n);
+    rd(in, gains.data(), (size_t)9 * n * n);
+    rd(in, q.data(), (size_t)3 * n);
     rd(in, vel.data(), vel.size());
     rd(in, Pin.data(), Pin.size());
     rd(in, &m, 1);
-    std::vector<double> pts(3 * m), adjf((size_t)m * m);
-    rd(in, pts.data(), pts.size());
-    rd(in, adjf.data(), adjf.size());
+    amd::Matrix3Xd pts(3, m);
+    amd::MatrixXd adjf(m, m);
+    rd(in, pts.data(), (size_t)3 * m);
+    rd(in, adjf.data(), (size_t)m * m);
     fclose(in);
 
     FILE* out = fopen(out_path, "wb");
     if (!out) throw std::runtime_error("cannot open output");
 
-    // auction: every vehicle's Auctioneer on the same snapshot
-    std::vector<std::vector<amd::vehidx_t>> Pveh(n);
+    // auction: every vehicle's objects on the same snapshot, the formation
+    // with its given gains (no ADMM solve inside formationCb)
+    std::vector<std::unique_ptr<Coordination>> veh;
     for (int v = 0; v < n; ++v) {
-      amd::Auctioneer auc((amd::vehidx_t)v, (uint8_t)n);
-      int calls = 0;
-      auc.setNewAssignmentHandler(&on_assignment, &calls);
-      auc.setFormation(p.data(), adj.data());
-      auc.setAssignment(Pin.data());
-      auc.start(q.data());
-      if (!auc.isIdle()) throw std::runtime_error("auction still open after start");
-      Pveh[v] = auc.getAssignment();
-      const std::vector<amd::vehidx_t> Pt = auc.getInvAssignment();
+      veh.emplace_back(new Coordination((amd::vehidx_t)v, (uint8_t)n));
+      Coordination& c = *veh.back();
+      auto f = std::make_shared<amd::DistCntrl::Formation>();
+      f->name = "facade";
+      f->adjmat = adj;
+      f->gains = gains;
+      f->qdes = p;
+      c.formationCb(f);
+      if (f->dstar_xy.rows() != n || f->dstar_z.cols() != n)
+        throw std::runtime_error("setFormation did not fill dstar");
+      // the caller's starting assignment through the backdoor (auctioneer.h:107)
+      amd::AssignmentPerm P0(amd::Map<const amd::AssignmentVec>(Pin.data(), Pin.size()));
+      c.auctioneer_->setAssignment(P0);
+      c.controller_->setAssignment(P0);
+      if (c.centralAssignmentCb(Pin)) throw std::runtime_error("isApprox after setAssignment");
+      c.auctioneer_->start(q);
+      if (!c.auctioneer_->isIdle()) throw std::runtime_error("auction still open after start");
+      const amd::AssignmentPerm P = c.auctioneer_->getAssignment();
+      const amd::AssignmentPerm Pt = c.auctioneer_->getInvAssignment();
       for (int i = 0; i < n; ++i)
-        if (Pt[Pveh[v][i]] != i) throw std::runtime_error("getInvAssignment is not P^-1");
-      const uint8_t inv = auc.didConvergeOnInvalidAssignment() ? 1 : 0;
-      const uint8_t nc = (uint8_t)calls;
-      wr(out, Pveh[v].data(), n);
+        if (Pt.indices()(P.indices()(i)) != i) throw std::runtime_error("getInvAssignment is not P^-1");
+      const amd::AssignmentPerm Pt2 = P.transpose();
+      if (!Pt2.indices().isApprox(Pt.indices())) throw std::runtime_error("P.transpose() != Pt");
+      // connectToNeighbors: the neighbours of this vehicle's formation point
+      const int i = P.indices()(v);
+      size_t deg = 0;
+      for (int j = 0; j < n; ++j) deg += adj(i, j) ? 1 : 0;
+      if (c.neighbours.size() != deg) throw std::runtime_error("connectToNeighbors");
+      const uint8_t inv = c.auctioneer_->didConvergeOnInvalidAssignment() ? 1 : 0;
+      const uint8_t nc = (uint8_t)c.handler_calls;
+      std::vector<uint8_t> Pv(n);
+      for (int k = 0; k < n; ++k) Pv[k] = P.indices()(k);
+      wr(out, Pv.data(), n);
       wr(out, &inv, 1);
       wr(out, &nc, 1);
     }
 
-    // control: each vehicle's DistCntrl with the assignment it adopted
-    auto form = std::make_shared<amd::DistCntrl::Formation>();
-    form->name = "facade";
-    form->adjmat = adj;
-    form->gains = gains;
-    form->qdes = p;
-    amd::DistCntrl::Gains g{};
-    {
-      acl_cntrl_gains_t d;
-      acl_default_cntrl_gains(&d);
-      g = {d.K1_xy, d.K2_xy, d.K1_z, d.K2_z, d.e_xy_thr, d.e_z_thr, d.kp, d.kd};
-    }
+    // control: each vehicle's DistCntrl with the assignment its handler set
+    // (coordination_ros.cpp:370-378: u = controller_->compute(q_veh, vel))
     for (int v = 0; v < n; ++v) {
-      amd::DistCntrl ctl((amd::vehidx_t)v, (uint8_t)n);
-      ctl.setGains(g);
-      ctl.setFormation(form);
-      ctl.setAssignment(Pveh[v].data());
-      double u[3];
-      ctl.compute(q.data(), &vel[3 * v], u);
-      wr(out, u, 3);
+      const amd::Vector3d vv(vel[3 * v], vel[3 * v + 1], vel[3 * v + 2]);
+      const amd::Vector3d u = veh[v]->controller_->compute(q, vv);
+      wr(out, u.data(), 3);
     }
-    if (form->dstar_xy.size() != (size_t)n * n) throw std::runtime_error("dstar not filled");
 
-    // ADMM gain design
+    // ADMM gain design: the formationCb path with no gains given
     int32_t its[2] = {0, 0};
-    std::vector<double> A((size_t)9 * m * m);
+    amd::MatrixXd A(3 * m, 3 * m);
     if (m > 0) {
-      amd::admm::Solver solver;
-      solver.solve(m, pts.data(), adjf.data(), A.data());
-      its[0] = solver.iterations2d();
-      its[1] = solver.iterations1d();
+      Coordination c(0, (uint8_t)m);
+      auto f = std::make_shared<amd::DistCntrl::Formation>();
+      f->name = "admm";
+      f->qdes = pts.transpose();
+      f->adjmat = adjf.cast<amd::vehidx_t>();
+      c.formationCb(f);
+      A = f->gains;
+      its[0] = c.admm_->iterations2d();
+      its[1] = c.admm_->iterations1d();
     }
     wr(out, its, 2);
-    wr(out, A.data(), A.size());
+    wr(out, A.data(), (size_t)9 * m * m);
     fclose(out);
   } catch (const std::exception& e) {
     fprintf(stderr, "facade_driver: %s\n", e.what());

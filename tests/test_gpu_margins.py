@@ -120,7 +120,8 @@ def test_gates_near_threshold(cuda, planes):
     assert T.gain_planes == planes
     fidx = np.arange(B, dtype=np.int32)
     out = engine.control(T, torch.from_numpy(fidx).to(dev), torch.from_numpy(q).to(dev),
-                         torch.from_numpy(vel).to(dev), torch.from_numpy(P.view(np.int16)).to(dev))
+                         torch.from_numpy(vel).to(dev), torch.from_numpy(P.view(np.int16)).to(dev),
+                         want_gate_margin=True)
     torch.cuda.synchronize()
     u = out["u"].cpu().numpy()
     gm = out["gate_margin"].cpu().numpy()
