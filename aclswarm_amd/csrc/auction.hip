@@ -43,6 +43,7 @@
 
 #include "../../include/aclswarm_amd.h"
 #include "common.h"
+#include "control_dev.h"
 #include "control_params.h"
 #include "umeyama_dev.h"
 
@@ -374,7 +375,10 @@ __device__ __forceinline__ void runner_up_walk(int n, const unsigned (&key)[NC],
   }
 }
 
-template <int NC, int kAB>
+// FUSE: phase 5, the control law of a swarm whose vehicles all adopted one
+// assignment, runs in this workgroup right after its auction (see below);
+// GM: the fused phase also reports the gate margin.
+template <int NC, int kAB, bool FUSE, bool GM>
 __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   constexpr int kAW = kAB / 64;  // waves per swarm
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1062,10 +1066,12 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   // Each vehicle's adopted inverse assignment (formation point -> vehicle):
   // one shared row when every vehicle adopts the same one (all tables valid
   // and identical, or none valid), else one row per vehicle.
+  const int ninv = misc[M_NINV];
+  const bool allvalid = ninv == 0;
+  const bool uniform = (allvalid && misc[M_AGREE]) || ninv == n;
+  // this thread's entry of the shared row (fused control phase)
+  const int ptv = (uniform && tid < n) ? (allvalid ? T[tid] : Ptin[tid]) : 0;
   {
-    const int ninv = misc[M_NINV];
-    const bool allvalid = ninv == 0;
-    const bool uniform = (allvalid && misc[M_AGREE]) || ninv == n;
     uint16_t* wsPt = reinterpret_cast<uint16_t*>(P.ws + P.W.pt) + (size_t)b * n;
     if (tid == 0) P.ws[P.W.mode + b] = uniform ? 0 : 1;
     if (uniform) {
@@ -1095,6 +1101,23 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     }
   }
   stamp_phase(P, b, tid, 6);
+
+  // ---------------- phase 5: control (FUSE) ---------------------------------
+  // DistCntrl::compute (distcntrl.cpp:46-102), saturation and the first
+  // collision test of a swarm whose vehicles all adopted one assignment, by
+  // this workgroup's waves once its own auction is done: the swarm's gain
+  // stream (the call's HBM bytes) overlaps the auctions of the co-resident
+  // swarms (scalar/LDS-issue bound) instead of following all of them in a
+  // second launch. LDS: every auction table is dead after the barrier; the
+  // pair layout starts at 0. Swarms with per-vehicle rows (mode 1) are left
+  // to gain_kernel (launch_control which = 2).
+  if constexpr (FUSE) {
+    if (!uniform) return;  // workgroup-uniform
+    __syncthreads();       // T, C and the hand-off reads are done
+    const PairLayout GL = make_pair_layout(n, kAW, false);
+    if (tid < n) reinterpret_cast<uint16_t*>(smem + GL.Pt)[tid] = (uint16_t)ptv;
+    pair_gain_swarm<kAW, false, GM, false>(P.ctl, b, f, smem, tid, kAB, nullptr);
+  }
 }
 
 // test hook: acl_price (fast path) and the IEEE expression for m squared
@@ -1107,12 +1130,22 @@ __global__ void price_sweep_kernel(const double* x, float* fast, float* ieee, in
   }
 }
 
-hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream) {
-  const ALayout L = make_alayout(P.n);
+// the dynamic LDS of the auction kernel, fused or not
+static int auction_lds(int n, bool fuse) {
+  const int a = make_alayout(n).total;
+  if (!fuse) return a;
+  const int kAW = n <= 32 ? 2 : (n <= 64 ? 4 : 8);
+  const int g = make_pair_layout(n, kAW, false).total;
+  return a > g ? a : g;
+}
+
+template <bool FUSE, bool GM>
+static hipError_t launch_auction_t(const SolveParams& P, int nb, hipStream_t stream) {
   static PerDeviceOnce once;
   const hipError_t ea = once.run([] {
-    for (const void* k : {(const void*)auction_kernel<1, 128>, (const void*)auction_kernel<1, 256>,
-                          (const void*)auction_kernel<2, 512>}) {
+    for (const void* k : {(const void*)auction_kernel<1, 128, FUSE, GM>,
+                          (const void*)auction_kernel<1, 256, FUSE, GM>,
+                          (const void*)auction_kernel<2, 512, FUSE, GM>}) {
       const hipError_t e =
           hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
@@ -1120,14 +1153,23 @@ hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream) {
     return hipSuccess;
   });
   if (ea != hipSuccess) return ea;
+  const int lds = auction_lds(P.n, FUSE);
   // (64 threads for n <= 32 measured no faster at C2: 0.091 vs 0.088 ms)
   if (P.n <= 32)
-    hipLaunchKernelGGL((auction_kernel<1, 128>), dim3(nb), dim3(128), L.total, stream, P);
+    hipLaunchKernelGGL((auction_kernel<1, 128, FUSE, GM>), dim3(nb), dim3(128), lds, stream, P);
   else if (P.n <= 64)
-    hipLaunchKernelGGL((auction_kernel<1, 256>), dim3(nb), dim3(256), L.total, stream, P);
+    hipLaunchKernelGGL((auction_kernel<1, 256, FUSE, GM>), dim3(nb), dim3(256), lds, stream, P);
   else
-    hipLaunchKernelGGL((auction_kernel<2, 512>), dim3(nb), dim3(512), L.total, stream, P);
+    hipLaunchKernelGGL((auction_kernel<2, 512, FUSE, GM>), dim3(nb), dim3(512), lds, stream, P);
   return hipGetLastError();
+}
+
+// fuse: run the control phase in the auction's workgroups (P.ctl filled;
+// 5-plane gain records, n <= 128)
+hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream, bool fuse) {
+  if (!fuse) return launch_auction_t<false, false>(P, nb, stream);
+  if (P.ctl.gate_margin) return launch_auction_t<true, true>(P, nb, stream);
+  return launch_auction_t<true, false>(P, nb, stream);
 }
 
 }  // namespace acl_amd

@@ -70,33 +70,6 @@ __host__ __device__ inline WsLayout ws_layout(int n, int B) {
   return W;
 }
 
-struct SolveParams {
-  int n, B, F, b0;
-  const double* p;
-  const uint64_t* adj;
-  const double* gains;
-  const int64_t* gain_off;
-  const int32_t* fidx;
-  const double* q;
-  const double* vel;
-  const uint16_t* P_in;
-  uint16_t* P_out;
-  acl_swarm_status_t* status;
-  double* u;
-  double* u_safe;
-  uint8_t* ca_flag;
-  uint16_t* who;
-  double* align_Rt;
-  acl_cntrl_gains_t g;
-  acl_safety_params_t s;
-  int early_exit;
-  int do_control;
-  unsigned char* ws;  // workspace base (WsLayout)
-  WsLayout W;
-  unsigned long long* stamps;  // diagnostic: [B][16] s_memtime at phase ends (NULL = off)
-  double* gate_margin;         // acl_solve_args_t::gate_margin (+inf for BAD_INPUT swarms)
-};
-
 struct CtlParams {
   int n, B, b0;
   const double* p;
@@ -126,13 +99,44 @@ struct CtlParams {
   double* gate_margin;  // [B] optional: min | |e| - thr | / thr of the swarm's gates
 };
 
+struct SolveParams {
+  int n, B, F, b0;
+  const double* p;
+  const uint64_t* adj;
+  const double* gains;
+  const int64_t* gain_off;
+  const int32_t* fidx;
+  const double* q;
+  const double* vel;
+  const uint16_t* P_in;
+  uint16_t* P_out;
+  acl_swarm_status_t* status;
+  double* u;
+  double* u_safe;
+  uint8_t* ca_flag;
+  uint16_t* who;
+  double* align_Rt;
+  acl_cntrl_gains_t g;
+  acl_safety_params_t s;
+  int early_exit;
+  int do_control;
+  unsigned char* ws;  // workspace base (WsLayout)
+  WsLayout W;
+  unsigned long long* stamps;  // diagnostic: [B][16] s_memtime at phase ends (NULL = off)
+  double* gate_margin;         // acl_solve_args_t::gate_margin (+inf for BAD_INPUT swarms)
+  CtlParams ctl;               // the fused control phase's parameters (auction.hip, FUSE)
+};
+
+
 // misc int slots of the auction kernels' LDS
 enum { M_BAD = 0, M_NONFIN = 1, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 8,
        M_MARG = 10 /* u64: bits of the swarm's minimum decision gap (misc[10..11]) */ };
 
 // Control stage: which = 0 launches the gain kernel for swarms
 // [P.b0, P.b0 + nb) (DistCntrl::compute, saturation, the collision test),
-// 1 the collisionAvoidance kernel over the listed vehicles.
+// 1 the collisionAvoidance kernel over the listed vehicles, 2 the directed
+// gain kernel for the swarms with per-vehicle assignments only (after the
+// fused auction + control kernel, which did the others).
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream);
 hipError_t launch_tile_gains(int n, int F, const uint64_t* adj, const double* gains,
                              const int64_t* gain_off, double* out, hipStream_t stream);
@@ -151,7 +155,9 @@ acl_status_t run_control(const acl_formations_t* F, const acl_control_args_t* a,
                          int flags);
 
 // The n <= 128 auction kernel (auction.hip).
-hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream);
+// fuse: the control phase runs in the auction's workgroups (P.ctl; 5-plane
+// gain records) for the swarms whose vehicles all adopted one assignment.
+hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream, bool fuse = false);
 
 // The n > 128 auction kernel (solve_wide.hip).
 hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream);

@@ -172,39 +172,45 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   P.gate_margin = a->do_control ? a->gate_margin : nullptr;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
+  if (a->do_control) {
+    CtlParams& C = P.ctl;
+    C.n = n; C.B = a->B; C.b0 = 0;
+    C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
+    C.gain_planes = F->gain_planes == 5 ? 5 : 9;
+    C.gains_tiled = (C.gain_planes == 5 && n <= kMaxN) ? F->gains_tiled : nullptr;
+    C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P_out;
+    C.status = a->status;
+    C.u = a->u ? a->u : reinterpret_cast<double*>(P.ws + P.W.u);
+    C.u_safe = a->u_safe; C.ca_flag = a->ca_flag;
+    C.wsPt = reinterpret_cast<const uint16_t*>(P.ws + P.W.pt);
+    C.wsMode = P.ws + P.W.mode;
+    C.wsRows = reinterpret_cast<const uint16_t*>(P.ws + P.W.rows);
+    C.ca_list = reinterpret_cast<unsigned*>(P.ws + P.W.calist);
+    C.ca_count = reinterpret_cast<unsigned*>(P.ws + P.W.cacount);
+    C.g = a->cntrl; C.s = a->safety;
+    C.only_nonuniform = 0;
+    C.all_uniform = 0;
+    C.F = F->n_formations;
+    C.gate_margin = a->gate_margin;
+    if (hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
+      return acl__set_error("hipMemsetAsync failed");
+  }
+  // The control phase runs inside the auction's workgroups (one launch, the
+  // gain stream overlapping the auctions) for 5-plane records at n <= 128;
+  // the directed gain kernel then takes the swarms with per-vehicle rows.
+  const bool fuse = a->do_control && n <= kMaxN && P.ctl.gain_planes == 5;
   kt_record(0, 0, s);
   if (n <= kMaxN) {
-    e = launch_auction(P, a->B, s);
+    e = launch_auction(P, a->B, s, fuse);
   } else {
     e = launch_wide(P, a->B, s);
   }
   kt_record(0, 1, s);
   if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
   if (!a->do_control) return ACL_OK;
-  CtlParams C;
-  C.n = n; C.B = a->B; C.b0 = 0;
-  C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
-  C.gain_planes = F->gain_planes == 5 ? 5 : 9;
-  C.gains_tiled = (C.gain_planes == 5 && n <= kMaxN) ? F->gains_tiled : nullptr;
-  C.fidx = a->fidx; C.q = a->q; C.vel = a->vel; C.P_out = a->P_out;
-  C.status = a->status;
-  C.u = a->u ? a->u : reinterpret_cast<double*>(P.ws + P.W.u);
-  C.u_safe = a->u_safe; C.ca_flag = a->ca_flag;
-  C.wsPt = reinterpret_cast<const uint16_t*>(P.ws + P.W.pt);
-  C.wsMode = P.ws + P.W.mode;
-  C.wsRows = reinterpret_cast<const uint16_t*>(P.ws + P.W.rows);
-  C.ca_list = reinterpret_cast<unsigned*>(P.ws + P.W.calist);
-  C.ca_count = reinterpret_cast<unsigned*>(P.ws + P.W.cacount);
-  C.g = a->cntrl; C.s = a->safety;
-  C.only_nonuniform = 0;
-  C.all_uniform = 0;
-  C.F = F->n_formations;
-  C.gate_margin = a->gate_margin;
-  if (hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
-    return acl__set_error("hipMemsetAsync failed");
   for (int which = 0; which < 2; ++which) {
     kt_record(1 + which, 0, s);
-    e = launch_control(C, a->B, which, s);
+    e = launch_control(P.ctl, a->B, which == 0 ? (fuse ? 2 : 0) : 1, s);
     kt_record(1 + which, 1, s);
     if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
   }

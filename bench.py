@@ -366,15 +366,10 @@ def main():
                     help="run all 2N CBAA rounds instead of stopping at the fixed point")
     ap.add_argument("--cpu-budget", type=float, default=16.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-setup-ab", action="store_true",
-                    help="skip the row-major-records (no acl_tile_gains) comparison steps")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--gain-planes", type=int, default=5, choices=(5, 9),
                     help="5: ADMM-structured gain blocks (the reference's gains); "
                          "9: general 3x3 blocks")
-    ap.add_argument("--no-tile-gains", action="store_true",
-                    help="pair kernel reads the row-major records instead of the "
-                         "tile-ordered copy made at formation setup (acl_tile_gains)")
     ap.add_argument("--graph", action="store_true",
                     help="time the step (solve + device-side stats) as one captured HIP graph "
                          "replayed per step (launch-bound configurations such as C2; one GPU)")
@@ -424,16 +419,6 @@ def main():
     T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"],
                               w["planes"])
     stream = torch.cuda.current_stream(dev)
-    t_tile = None
-    if not args.no_tile_gains and w["planes"] == 5 and n <= 128:
-        # formation setup (once per formation table, outside the timed solves)
-        T.tile_gains()  # first call: code-object load; time the second
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        T.tile_gains()
-        e1.record(stream)
-        torch.cuda.synchronize()
-        t_tile = e0.elapsed_time(e1) * 1e-3
     out = {
         "P_out": torch.empty((B, n), dtype=torch.int16, device=dev),
         "status": torch.empty((B, 16), dtype=torch.uint8, device=dev),
@@ -510,32 +495,6 @@ def main():
     dt_max = float(dt_t.item())
     stats = D.stats_dict(res[2], res[3])
 
-    # setup accounting: the same solve on the row-major records (no
-    # acl_tile_gains), untimed for the headline
-    setup = None
-    if t_tile is not None:
-        setup = {"tile_gains_ms": t_tile * 1e3, "tile_gains_us_per_formation": t_tile * 1e6 / w["F"],
-                 "value_if_tiled_every_step": world * B / (dt_max + t_tile),
-                 "break_even_solves_per_formation": None}
-        if not args.no_setup_ab:
-            tiled = T.gains_tiled
-            T.gains_tiled = None
-            for _ in range(2):
-                solve()
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(3):
-                solve()
-            e1.record(stream)
-            torch.cuda.synchronize()
-            T.gains_tiled = tiled
-            ms_rm = e0.elapsed_time(e1) / 3
-            setup["row_major_records"] = {"call_ms": ms_rm, "value_1gpu": B / (ms_rm * 1e-3)}
-            gain_s = ms_rm * 1e-3 - call_ms * 1e-3
-            setup["break_even_solves_per_formation"] = (
-                (t_tile / w["F"]) / (gain_s / B) if gain_s > 0 else None)
-
     # collision-avoidance probe: the same swarms crowded (positions scaled by
     # 0.3 about each swarm's centre, most vehicles inside the 1.5 m avoidance
     # radius), so the sector algebra of Safety::collisionAvoidance
@@ -575,16 +534,26 @@ def main():
                     "ca_active_swarms": sc["ca_active"], "ca_vehicles": sc["ca_vehicles"]}
         del outc, qc
 
-    # algorithmic bytes per launch (every kernel is one launch over all B)
+    # algorithmic bytes per launch (every kernel is one launch over all B).
+    # n <= 128 with 5-plane records: the control phase runs inside the
+    # auction's workgroups (one fused launch carries every byte); the directed
+    # gain kernel then runs only for swarms with per-vehicle rows (none here).
     a_all, g_all, s_all, e_avg = algorithmic_bytes(w, 0, B)
-    per_launch = {"auction": a_all, "gain": g_all, "ca": s_all}
-    gain_sym = ("acl_amd::gain_pair_kernel<%s, false>" % ("true" if t_tile is not None else "false")
-                if w["planes"] == 5
-                else f"acl_amd::gain_kernel<{w['planes']}, false>")
-    auction_sym = (("acl_amd::auction_kernel<1, 128>" if n <= 32 else
-                    "acl_amd::auction_kernel<1, 256>" if n <= 64 else
-                    "acl_amd::auction_kernel<2, 512>") if n <= 128
-                   else "acl_amd::solve_wide_kernel")
+    fused = n <= 128 and w["planes"] == 5
+    if fused:
+        per_launch = {"auction": a_all + g_all, "gain": 0, "ca": s_all}
+        auction_sym = ("acl_amd::auction_kernel<1, 128, true, false>" if n <= 32 else
+                       "acl_amd::auction_kernel<1, 256, true, false>" if n <= 64 else
+                       "acl_amd::auction_kernel<2, 512, true, false>")
+        gain_sym = f"acl_amd::gain_kernel<{w['planes']}, false>"
+    else:
+        per_launch = {"auction": a_all, "gain": g_all, "ca": s_all}
+        auction_sym = (("acl_amd::auction_kernel<1, 128, false, false>" if n <= 32 else
+                        "acl_amd::auction_kernel<1, 256, false, false>" if n <= 64 else
+                        "acl_amd::auction_kernel<2, 512, false, false>") if n <= 128
+                       else "acl_amd::solve_wide_kernel")
+        gain_sym = ("acl_amd::gain_pair_kernel<false, false>" if w["planes"] == 5
+                    else f"acl_amd::gain_kernel<{w['planes']}, false>")
     kern = {}
     for k, (name, sym) in enumerate((("auction", auction_sym), ("gain", gain_sym),
                                      ("ca", "acl_amd::ca_kernel"))):
@@ -596,6 +565,10 @@ def main():
                       "bytes_per_launch": per_launch[name], "achieved_GBs": ach,
                       "frac": ach / HBM_PEAK_GBS,
                       "traffic": pm["hbm_bytes"] if pm else None, "traffic_source": src}
+    if fused:
+        kern["auction"]["what"] = ("fused: alignment, CBAA, adoption, then DistCntrl + "
+                                   "saturation + the collision test in the same workgroup")
+        kern["gain"]["what"] = "directed gain kernel for swarms with per-vehicle rows only"
     # the auction kernel is LDS/VALU/SALU-issue bound: its issue rates from the
     # committed SQ counters of the same configuration (scripts/gpu_pmc_auction.sh)
     iss, isrc = committed_profile("pmc_auction", n, B, auction_sym)
@@ -612,10 +585,10 @@ def main():
                                            "ports": ports, "source": isrc}
     pipe_bytes = a_all + g_all + s_all
     pipe_ach = pipe_bytes / (call_ms * 1e-3) / 1e9
-    tr = [kern[k]["traffic"] for k in ("auction", "gain")]
+    tr = [kern[k]["traffic"] for k in (("auction",) if fused else ("auction", "gain"))]
     pipe_traffic = sum(tr) if all(x is not None for x in tr) else None
-    pipe_traffic_src = kern["gain"]["traffic_source"] if pipe_traffic is not None else None
-    gk = kern["gain"]
+    pipe_traffic_src = kern["auction"]["traffic_source"] if pipe_traffic is not None else None
+    gk = kern["auction" if fused else "gain"]
     line = {
         "metric": METRIC,
         "value": world * B / dt_max,
@@ -646,8 +619,10 @@ def main():
             "gains": ("synthetic ADMM-structured blocks [a b 0; c d 0; 0 0 e] "
                       "(solver.cpp:49-77), 5-entry records = 40 B/edge" if w["planes"] == 5 else
                       "synthetic random 3x3 blocks, 9 planes = 72 B/edge"),
-            "gain_layout": ("tile-ordered copy (acl_tile_gains at formation setup, see `setup`)"
-                            if t_tile is not None else "row-major records"),
+            "gain_layout": "row-major 40-byte records (no formation-setup re-layout)",
+            "kernels": ("one fused auction + control launch (+ the collision-avoidance "
+                        "launch over the listed vehicles)" if fused else
+                        "auction launch, gain launch, collision-avoidance launch"),
         },
         "roofline": {
             "bound": "hbm", "scope": "pipeline",
@@ -658,7 +633,7 @@ def main():
             "frac": pipe_ach / HBM_PEAK_GBS,
             "traffic": pipe_traffic, "traffic_source": pipe_traffic_src,
             "call_ms": call_ms, "bytes_per_call": pipe_bytes,
-            "gain_kernel": {"kernel": gk["kernel"], "achieved": gk["achieved_GBs"],
+            "stream_kernel": {"kernel": gk["kernel"], "achieved": gk["achieved_GBs"],
                             "frac": gk["frac"], "avg_launch_ms": gk["avg_launch_ms"],
                             "bytes_per_launch": gk["bytes_per_launch"],
                             "traffic": gk["traffic"], "traffic_source": gk["traffic_source"]},
@@ -667,7 +642,6 @@ def main():
                     "auction is LDS/VALU/SALU-issue bound (kernels.auction.issue)",
             "kernels": kern,
         },
-        "setup": setup,
         "ca_probe": ca_probe,
         "stats": stats,
         "gen_s": t_gen,
