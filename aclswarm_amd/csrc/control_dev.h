@@ -254,7 +254,7 @@ __device__ __forceinline__ double swap_sum(double x) {
 }
 
 struct PairLayout {
-  int q, qf, p, pn, adjF, rowpre, Pt, acc, out, atab, tmask, tstart, total;
+  int q, qf, p, pn, adjF, rowpre, Pt, acc, out, atab, tmask, tstart, gmw, total;
 };
 
 __host__ __device__ inline PairLayout make_pair_layout(int n, int kW = kCtlWaves, bool tiled = true) {
@@ -274,6 +274,7 @@ __host__ __device__ inline PairLayout make_pair_layout(int n, int kW = kCtlWaves
   const int NT = (tiled && n <= kMaxN) ? pair_tiles(n) : 0;  // tiled records: n <= 128 only
   L.tmask = o;  o = cal16(o + 2 * NT * 8);
   L.tstart = o; o = cal16(o + 2 * NT * 4);
+  L.gmw = o;    o = cal16(o + 8);                  // gate margin word
   L.total = o;
   return L;
 }
@@ -331,7 +332,9 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
 #else
   if (tid < ACL_ATAB_N) atab[tid] = kAtanTab[tid / 6][tid % 6];
 #endif
-  __shared__ unsigned long long gmw;  // gate margin: set before the barriers below
+  // gate margin word (in the dynamic layout: the fused kernel may use all
+  // 160 KiB): set before the barriers below
+  unsigned long long& gmw = *reinterpret_cast<unsigned long long*>(smem + L.gmw);
   if (GM && tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
   {
