@@ -57,7 +57,8 @@ struct Scal {
   double trM11, c0, nrm, err2, diff, tr22;
   int active, inactive, ns_done, ns_final, ns_upd, ns_fail, itr, pad;
   int skip_s0, skip_s1;  // which S product runs: the sign is in N0 (even updates) or N1
-  int pad2[2];
+  int ns_fail_now;       // this iteration's sign iteration did not converge: Jacobi fallback
+  int jacobi;            // iterations whose projection the Jacobi fallback made
 };
 
 struct Part {
@@ -567,7 +568,7 @@ __global__ void __launch_bounds__(kT) norm_kernel(const Part* parts, double eps)
     // [0.37, 1] of the radius and the radius at 0.67-0.75 of the inf-norm, so
     // kNsScale = 1.5 starts the eigenvalues nearer 1 (about 20% fewer steps)
     sc.nrm = m > 0.0 ? m / kNsScale : 1.0;
-    sc.ns_done = 0; sc.ns_final = 0; sc.ns_upd = 0; sc.inactive = 0;
+    sc.ns_done = 0; sc.ns_final = 0; sc.ns_upd = 0; sc.inactive = 0; sc.ns_fail_now = 0;
   }
 }
 
@@ -613,10 +614,10 @@ __global__ void __launch_bounds__(1024) nsstep_kernel(const Part* parts, int npa
     const int n2 = 2 * parts[p].s;
     if (sc.err2 < 1e-20 * n2 || sc.ns_upd >= kNsMax || !(sc.err2 == sc.err2)) {
       sc.ns_done = 1;
-      if (!(sc.err2 < 1e-20 * n2)) sc.ns_fail = 1;
+      if (!(sc.err2 < 1e-20 * n2)) sc.ns_fail_now = 1;
     } else if (last) {
       sc.ns_done = 1;
-      sc.ns_fail = 1;
+      sc.ns_fail_now = 1;
     }
     sc.err2 = 0.0;
     if (!sc.ns_done) atomicAdd(&cnt, 1);
@@ -632,11 +633,154 @@ __global__ void __launch_bounds__(1024) nsparity_kernel(const Part* parts, int n
   for (int p = threadIdx.x; p < nparts; p += blockDim.x) {
     Scal& sc = *parts[p].sc;
     const int odd = sc.ns_upd & 1;
-    sc.skip_s0 = (!sc.active || odd) ? 1 : 0;
-    sc.skip_s1 = (!sc.active || !odd) ? 1 : 0;
+    const int skip = !sc.active || sc.ns_fail_now;  // no sign: psd_jacobi_kernel writes Sr
+    sc.skip_s0 = (skip || odd) ? 1 : 0;
+    sc.skip_s1 = (skip || !odd) ? 1 : 0;
   }
 }
 
+// test hook (acl_internal_psd_project): every active part takes the fallback
+__global__ void __launch_bounds__(1024) force_jacobi_kernel(const Part* parts, int nparts) {
+  for (int p = threadIdx.x; p < nparts; p += blockDim.x) parts[p].sc->ns_fail_now = 1;
+}
+
+// ---------------------------------------------------------------------------
+// PSD projection fallback: S = sum over lambda > eps of lambda v v^T from a
+// parallel two-sided Jacobi eigensolver (one workgroup per part), for the
+// parts whose Newton-Schulz sign iteration did not converge in kNsMax steps:
+// an eigenvalue of W at (or within ~1e-11 |W| of) eps, where sign(W - eps I)
+// is ill-conditioned. The reference decides that projection with its
+// eigensolver (admm::Solver: SelfAdjointEigenSolver, solver.cpp:296-316; the
+// codegen: eig -> schur, eig.cpp:24, ADMMGainDesign2D.m:430-445); so does
+// this, eigenvalue by eigenvalue.
+//
+// Pairing: the circle method. In step t (0 .. N-2) index 0 meets 1 + t and,
+// for k = 1 .. N/2 - 1, 1 + (t + k) % (N - 1) meets 1 + (t - k) % (N - 1);
+// the N/2 rotations of a step are disjoint, so A <- J^T A J is one pass over
+// the 2 x 2 blocks (block (k, l) <- R_k^T A_kl R_l for k <= l, mirrored: A
+// stays symmetric bit for bit) and V <- V J one pass over V's column pairs.
+// Rotation (Golub & Van Loan, sym.schur2): tau = (a_qq - a_pp) / (2 a_pq),
+// t = sign(tau) / (|tau| + sqrt(1 + tau^2)), c = 1 / sqrt(1 + t^2), s = t c.
+// Sweeps until the off-diagonal mass is below (1e-15 |A|_F)^2 (at most
+// kJacobiSweeps). Workspace: A in N0, V in N1; the result goes to Sr, full
+// and symmetric, where the S product would have put it.
+constexpr int kJT = 1024;
+constexpr int kJacobiSweeps = 40;
+
+__device__ __forceinline__ double block_sum_all(double v, double* red) {
+  const double t = block_sum(v, red);
+  __syncthreads();
+  if (threadIdx.x == 0) red[0] = t;
+  __syncthreads();
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ void __launch_bounds__(kJT) psd_jacobi_kernel(const Part* parts, double eps) {
+  const Part& P = parts[blockIdx.x];
+  Scal& sc = *P.sc;
+  if (!sc.active || !sc.ns_fail_now) return;
+  const int N = 2 * P.s, m = N / 2, N1 = N - 1;
+  extern __shared__ __attribute__((aligned(16))) double jsm[];
+  double* cs = jsm;                                  // [m][2] c, s
+  double* lam = jsm + 2 * m;                         // [N] eigenvalues kept (> eps), else 0
+  int* pq = reinterpret_cast<int*>(jsm + 2 * m + N); // [m][2] the step's pairs
+  __shared__ double red[kJT / 64];
+  double* A = P.N0;
+  double* V = P.N1;
+  const int tid = threadIdx.x;
+  double fro = 0.0;
+  for (int e = tid; e < N * N; e += kJT) {
+    const double w = P.W[e];
+    A[e] = w;
+    V[e] = (e % N == e / N) ? 1.0 : 0.0;
+    fro += w * w;
+  }
+  const double tol = 1e-30 * block_sum_all(fro, red);  // (1e-15 |A|_F)^2
+  __syncthreads();
+  for (int sweep = 0; sweep < kJacobiSweeps; ++sweep) {
+    double off = 0.0;
+    for (int e = tid; e < N * N; e += kJT) {
+      const int i = e % N, j = e / N;
+      if (i != j) off += A[e] * A[e];
+    }
+    if (!(block_sum_all(off, red) > tol)) break;  // (NaN: stop, the result is NaN)
+    for (int t = 0; t < N1; ++t) {
+      for (int k = tid; k < m; k += kJT) {
+        int p, q;
+        if (k == 0) { p = 0; q = 1 + t; }
+        else { p = 1 + (t + k) % N1; q = 1 + (t - k + N1) % N1; }
+        const double app = A[p + (size_t)p * N], aqq = A[q + (size_t)q * N];
+        const double apq = A[p + (size_t)q * N];
+        double c = 1.0, sn = 0.0;
+        if (apq != 0.0) {
+          const double tau = (aqq - app) / (2.0 * apq);
+          const double tt = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+          c = 1.0 / sqrt(1.0 + tt * tt);
+          sn = tt * c;
+        }
+        cs[2 * k] = c; cs[2 * k + 1] = sn;
+        pq[2 * k] = p; pq[2 * k + 1] = q;
+      }
+      __syncthreads();
+      // A <- J^T A J, block by block (k <= l)
+      const int nblk = m * (m + 1) / 2;
+      for (int bidx = tid; bidx < nblk; bidx += kJT) {
+        // bidx -> (k, l), k <= l, row by row of the upper triangle
+        int k = (int)((2.0 * m + 1.0 - sqrt((2.0 * m + 1.0) * (2.0 * m + 1.0) - 8.0 * bidx)) / 2.0);
+        while (k > 0 && k * (2 * m - k + 1) / 2 > bidx) --k;
+        while ((k + 1) * (2 * m - k) / 2 <= bidx) ++k;
+        const int l = k + bidx - k * (2 * m - k + 1) / 2;
+        const int pk = pq[2 * k], qk = pq[2 * k + 1], pl = pq[2 * l], ql = pq[2 * l + 1];
+        const double ck = cs[2 * k], sk = cs[2 * k + 1], cl = cs[2 * l], sl = cs[2 * l + 1];
+        const double x00 = A[pk + (size_t)pl * N], x01 = A[pk + (size_t)ql * N];
+        const double x10 = A[qk + (size_t)pl * N], x11 = A[qk + (size_t)ql * N];
+        // M = X R_l, Y = R_k^T M, R = [c s; -s c]
+        const double m00 = cl * x00 - sl * x01, m01 = sl * x00 + cl * x01;
+        const double m10 = cl * x10 - sl * x11, m11 = sl * x10 + cl * x11;
+        double y00 = ck * m00 - sk * m10, y01 = ck * m01 - sk * m11;
+        double y10 = sk * m00 + ck * m10, y11 = sk * m01 + ck * m11;
+        if (k == l) {  // the annihilated entry
+          y01 = 0.0;
+          y10 = 0.0;
+        }
+        A[pk + (size_t)pl * N] = y00; A[pk + (size_t)ql * N] = y01;
+        A[qk + (size_t)pl * N] = y10; A[qk + (size_t)ql * N] = y11;
+        if (k != l) {
+          A[pl + (size_t)pk * N] = y00; A[ql + (size_t)pk * N] = y01;
+          A[pl + (size_t)qk * N] = y10; A[ql + (size_t)qk * N] = y11;
+        }
+      }
+      // V <- V J: rows i, column pairs k
+      for (int e = tid; e < N * m; e += kJT) {
+        const int i = e % N, k = e / N;
+        const int p = pq[2 * k], q = pq[2 * k + 1];
+        const double c = cs[2 * k], sn = cs[2 * k + 1];
+        const double vp = V[i + (size_t)p * N], vq = V[i + (size_t)q * N];
+        V[i + (size_t)p * N] = c * vp - sn * vq;
+        V[i + (size_t)q * N] = sn * vp + c * vq;
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < N; i += kJT) {
+    const double l = A[i + (size_t)i * N];
+    lam[i] = l > eps ? l : 0.0;  // the eigenvalues the projection keeps
+  }
+  __syncthreads();
+  // Sr = V diag(lam) V^T, upper triangle computed, mirrored
+  for (int e = tid; e < N * N; e += kJT) {
+    const int i = e % N, j = e / N;
+    if (i > j) continue;
+    double a = 0.0;
+    for (int k = 0; k < N; ++k)
+      if (lam[k] != 0.0) a += V[i + (size_t)k * N] * lam[k] * V[j + (size_t)k * N];
+    P.Sr[i + (size_t)j * N] = a;
+    P.Sr[j + (size_t)i * N] = a;
+  }
+  if (tid == 0) sc.jacobi += 1;
+}
 
 // S = sym(Sr), Sr = (W + W sign)/2 from the GEMM; X = (S - W)/mu;
 // sum |X_old - X|, tr X22.
@@ -719,8 +863,8 @@ __global__ void __launch_bounds__(kT) assemble_kernel(const Part* parts, int n, 
     G[e] = (fabs(v) > 1e-10) ? v : 0.0;
   }
   if (iters && blockIdx.x == 0 && threadIdx.x == 0) {
-    iters[2 * (f0 + fl)] = Pxy.sc->ns_fail ? -Pxy.sc->itr : Pxy.sc->itr;
-    iters[2 * (f0 + fl) + 1] = Pz.sc->ns_fail ? -Pz.sc->itr : Pz.sc->itr;
+    iters[2 * (f0 + fl)] = Pxy.sc->itr;
+    iters[2 * (f0 + fl) + 1] = Pz.sc->itr;
   }
 }
 
@@ -751,6 +895,72 @@ unsigned long long* g_flops = nullptr;  // diagnostic GEMM flop counter (device)
 
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 inline int grid1(long long work) { return std::max(1, std::min(cdiv(work, kT), 1024)); }
+
+// GEMM job lists: one device array of NP descriptors per kind
+enum {
+  J_G, J_PRE1, J_PRE2, J_PIM1, J_PIM2, J_GINV, J_T, J_YK, J_NSY0, J_NSU0, J_NSY1, J_NSU1,
+  J_S, J_S1, J_A1, J_AP, J_COUNT
+};
+
+struct JobLists {
+  GemmJob* dj = nullptr;  // device: J_COUNT x NP
+  int NP = 0;
+  int njob[J_COUNT] = {};
+  int mx[J_COUNT][2] = {};
+  // symmetric products (exact arithmetic): G = Q Q^T, the Newton-Schulz
+  // Z^2 and Z Z^2 (polynomials in one symmetric Z commute), W sign(W)
+  static bool sym(int kind) {
+    return kind == J_G || kind == J_NSY0 || kind == J_NSU0 || kind == J_NSY1 ||
+           kind == J_NSU1 || kind == J_S || kind == J_S1;
+  }
+  hipError_t run(int kind, bool ta, bool tb, hipStream_t st) const {
+    return gemm_f64(ta, tb, dj + (size_t)kind * NP, njob[kind], mx[kind][0], mx[kind][1], st,
+                    g_flops, sym(kind) && mx[kind][0] == mx[kind][1]);
+  }
+};
+
+// The PSD part of every active part's W (eigenvalues > eps) into Sr: the
+// Newton-Schulz sign iteration on the matrix cores (S = (W + W sign(W - eps
+// I)) / 2), then psd_jacobi_kernel for the parts it did not resolve
+// (force_jacobi: for every part, a test hook). Synchronises the stream to
+// stop the sign iteration once every part has converged.
+hipError_t psd_project(const JobLists& J, Part* dp, int NP, int n2max, double eps, bool fuse_err,
+                       bool force_jacobi, Ctx& X, hipStream_t st) {
+  const dim3 gW(grid1((long long)n2max * n2max), NP);
+  hipLaunchKernelGGL(norm_kernel, dim3(NP), dim3(kT), 0, st, dp, eps);
+  hipLaunchKernelGGL(nsinit_kernel, gW, dim3(kT), 0, st, dp, eps);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  for (int it = 0; it < kNsMax; ++it) {
+    const bool odd = it & 1;
+    if ((e = J.run(odd ? J_NSY1 : J_NSY0, false, false, st)) != hipSuccess) return e;
+    if (!fuse_err)
+      hipLaunchKernelGGL(nserr_kernel, dim3(std::min(grid1((long long)n2max * n2max), 64), NP),
+                         dim3(kT), 0, st, dp);
+    if ((e = J.run(odd ? J_NSU1 : J_NSU0, false, false, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(nsstep_kernel, dim3(1), dim3(1024), 0, st, dp, NP,
+                       it == kNsMax - 1 ? 1 : 0, X.d_cnt);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (it >= 5) {
+      if ((e = hipMemcpyAsync(X.h_cnt, X.d_cnt, sizeof(int), hipMemcpyDeviceToHost, st)) !=
+          hipSuccess)
+        return e;
+      if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+      if (*X.h_cnt == 0) break;
+    }
+  }
+  if (force_jacobi) hipLaunchKernelGGL(force_jacobi_kernel, dim3(1), dim3(1024), 0, st, dp, NP);
+  hipLaunchKernelGGL(nsparity_kernel, dim3(1), dim3(1024), 0, st, dp, NP);
+  if ((e = J.run(J_S, false, false, st)) != hipSuccess) return e;
+  if ((e = J.run(J_S1, false, false, st)) != hipSuccess) return e;
+  const size_t jlds = (size_t)20 * n2max;
+  if (jlds > 64 * 1024 &&
+      (e = hipFuncSetAttribute((const void*)psd_jacobi_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)jlds)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(psd_jacobi_kernel, dim3(NP), dim3(kJT), jlds, st, dp, eps);
+  return hipGetLastError();
+}
 
 }  // namespace admm
 }  // namespace acl_amd
@@ -883,17 +1093,13 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       P.sc = scal + p;
     }
     // ---- GEMM job lists
-    enum {
-      J_G, J_PRE1, J_PRE2, J_PIM1, J_PIM2, J_GINV, J_T, J_YK, J_NSY0, J_NSU0, J_NSY1, J_NSU1,
-      J_S, J_S1, J_A1, J_AP, J_COUNT
-    };
     std::vector<GemmJob> jobs((size_t)J_COUNT * NP);
-    std::vector<int> njob(J_COUNT, 0);
-    int mx[J_COUNT][2] = {};
+    JobLists JL;
+    JL.NP = NP;
     auto add = [&](int kind, const GemmJob& j) {
-      jobs[(size_t)kind * NP + njob[kind]++] = j;
-      mx[kind][0] = std::max(mx[kind][0], j.m);
-      mx[kind][1] = std::max(mx[kind][1], j.n);
+      jobs[(size_t)kind * NP + JL.njob[kind]++] = j;
+      JL.mx[kind][0] = std::max(JL.mx[kind][0], j.m);
+      JL.mx[kind][1] = std::max(JL.mx[kind][1], j.n);
     };
     // the default GEMM kernel (the four-wave 80 tile) fuses nserr_kernel's
     // |Y - I|_F^2 into the epilogue of the Newton-Schulz product Y = Z^2
@@ -932,16 +1138,8 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
             "hipMemcpyAsync");
     ACL_HIP(hipMemcpyAsync(dp, hp.data(), NP * sizeof(Part), hipMemcpyHostToDevice, st),
             "hipMemcpyAsync");
-    // symmetric products (exact arithmetic): G = Q Q^T, the Newton-Schulz
-    // Z^2 and Z Z^2 (polynomials in one symmetric Z commute), W sign(W)
-    auto symk = [](int kind) {
-      return kind == J_G || kind == J_NSY0 || kind == J_NSU0 || kind == J_NSY1 ||
-             kind == J_NSU1 || kind == J_S || kind == J_S1;
-    };
-    auto gemm = [&](int kind, bool ta, bool tb) -> hipError_t {
-      return gemm_f64(ta, tb, dj + (size_t)kind * NP, njob[kind], mx[kind][0], mx[kind][1], st,
-                      g_flops, symk(kind) && mx[kind][0] == mx[kind][1]);
-    };
+    JL.dj = dj;
+    auto gemm = [&](int kind, bool ta, bool tb) -> hipError_t { return JL.run(kind, ta, tb, st); };
     int max_s = 0, max_np = 0, maxK1 = 1;
     for (const Info& in : info) {
       max_s = std::max(max_s, in.s);
@@ -972,30 +1170,11 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       hipLaunchKernelGGL(rc_kernel, dim3(NP), dim3(kT), 0, st, dp, 1, mu);
       ACL_HIP(gemm(J_T, true, false), "gemm T");
       hipLaunchKernelGGL(w_kernel, gW, dim3(kT), 0, st, dp, mu);
-      hipLaunchKernelGGL(norm_kernel, dim3(NP), dim3(kT), 0, st, dp, eps);
-      hipLaunchKernelGGL(nsinit_kernel, gW, dim3(kT), 0, st, dp, eps);
       ACL_HIP(hipGetLastError(), "iteration kernels");
-      for (int it = 0; it < kNsMax; ++it) {
-        const bool odd = it & 1;
-        ACL_HIP(gemm(odd ? J_NSY1 : J_NSY0, false, false), "gemm NS");
-        if (!fuse_err)
-          hipLaunchKernelGGL(nserr_kernel, dim3(std::min(grid1((long long)n2max * n2max), 64), NP),
-                             dim3(kT), 0, st, dp);
-        ACL_HIP(gemm(odd ? J_NSU1 : J_NSU0, false, false), "gemm NS");
-        hipLaunchKernelGGL(nsstep_kernel, dim3(1), dim3(1024), 0, st, dp, NP,
-                           it == kNsMax - 1 ? 1 : 0, X.d_cnt);
-        ACL_HIP(hipGetLastError(), "NS kernels");
-        if (it >= 5) {
-          ACL_HIP(hipMemcpyAsync(X.h_cnt, X.d_cnt, sizeof(int), hipMemcpyDeviceToHost, st), "copy");
-          ACL_HIP(hipStreamSynchronize(st), "sync");
-          if (*X.h_cnt == 0) break;
-        }
-      }
-      hipLaunchKernelGGL(nsparity_kernel, dim3(1), dim3(1024), 0, st, dp, NP);
-      ACL_HIP(gemm(J_S, false, false), "gemm S");
-      ACL_HIP(gemm(J_S1, false, false), "gemm S");
+      ACL_HIP(psd_project(JL, dp, NP, n2max, eps, fuse_err, false, X, st), "PSD projection");
       hipLaunchKernelGGL(post_kernel, dim3(std::min(grid1((long long)n2max * n2max), 64), NP),
-                         dim3(kT), 0, st, dp, mu, symk(J_S) ? gemm_tile_size() : (1 << 30));
+                         dim3(kT), 0, st, dp, mu,
+                         JobLists::sym(J_S) ? gemm_tile_size() : (1 << 30));
       hipLaunchKernelGGL(check_kernel, dim3(1), dim3(1024), 0, st, dp, NP, prm.thresh,
                          prm.threshTr, X.d_cnt + 1);
       ACL_HIP(hipGetLastError(), "iteration kernels");
@@ -1025,4 +1204,101 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
 // every ADMM GEMM tile into *counter (a device pointer; NULL turns it off).
 extern "C" void acl_internal_admm_flop_counter(unsigned long long* counter) {
   acl_amd::admm::g_flops = counter;
+}
+
+// Test hook (not part of the public ABI; tests/test_gpu_admm.py): the PSD
+// projection of nm symmetric N x N matrices W (device, column-major, N even)
+// into S = (Sr + Sr^T) / 2 exactly as an ADMM iteration makes it (Newton-
+// Schulz on the matrix cores, the Jacobi fallback where the sign iteration
+// does not converge; force_jacobi: the fallback for every matrix).
+// jacobi_used (host, may be NULL): per matrix, 1 if the fallback made it.
+// Synchronous; returns 0 on success.
+extern "C" int acl_internal_psd_project(int nm, int N, const double* W, double eps, double* S,
+                                        int force_jacobi, int* jacobi_used) {
+  using namespace acl_amd;
+  using namespace acl_amd::admm;
+  if (nm <= 0 || N < 2 || (N & 1)) return 1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  Ctx& X = g_ctx[dev & 15];
+  if (!X.h_cnt) {
+    if (hipHostMalloc((void**)&X.h_cnt, sizeof(int) * 4) != hipSuccess ||
+        hipMalloc((void**)&X.d_cnt, sizeof(int) * 4) != hipSuccess)
+      return 1;
+  }
+  const size_t NN = (size_t)N * N;
+  double* buf = nullptr;
+  Scal* sc = nullptr;
+  Part* dp = nullptr;
+  GemmJob* dj = nullptr;
+  if (hipMalloc((void**)&buf, 5 * NN * nm * sizeof(double)) != hipSuccess) return 1;
+  if (hipMalloc((void**)&sc, nm * sizeof(Scal)) != hipSuccess) return 1;
+  if (hipMalloc((void**)&dp, nm * sizeof(Part)) != hipSuccess) return 1;
+  if (hipMalloc((void**)&dj, (size_t)J_COUNT * nm * sizeof(GemmJob)) != hipSuccess) return 1;
+  std::vector<Part> hp(nm);
+  std::vector<Scal> hs(nm);
+  std::vector<GemmJob> jobs((size_t)J_COUNT * nm);
+  JobLists JL;
+  JL.NP = nm;
+  JL.dj = dj;
+  auto add = [&](int kind, const GemmJob& j) {
+    jobs[(size_t)kind * nm + JL.njob[kind]++] = j;
+    JL.mx[kind][0] = std::max(JL.mx[kind][0], j.m);
+    JL.mx[kind][1] = std::max(JL.mx[kind][1], j.n);
+  };
+  const bool fuse_err = gemm_tile() == 80;
+  for (int p = 0; p < nm; ++p) {
+    Part& P = hp[p];
+    P = Part{};
+    P.s = N / 2;
+    P.W = const_cast<double*>(W) + p * NN;
+    P.N0 = buf + (5 * (size_t)p + 0) * NN;
+    P.N1 = buf + (5 * (size_t)p + 1) * NN;
+    P.Y = buf + (5 * (size_t)p + 2) * NN;
+    P.Sr = buf + (5 * (size_t)p + 3) * NN;
+    P.sc = sc + p;
+    hs[p] = Scal{};
+    hs[p].active = 1;
+    const int* nsd = &P.sc->ns_done;
+    double* e2 = fuse_err ? &P.sc->err2 : nullptr;
+    add(J_NSY0, {P.N0, P.N0, nullptr, P.Y, N, N, N, N, N, N, N, 1.0, 0.0, nsd, e2});
+    add(J_NSU0, {P.N0, P.Y, P.N0, P.N1, N, N, N, N, N, N, N, -0.5, 1.5, nsd});
+    add(J_NSY1, {P.N1, P.N1, nullptr, P.Y, N, N, N, N, N, N, N, 1.0, 0.0, nsd, e2});
+    add(J_NSU1, {P.N1, P.Y, P.N1, P.N0, N, N, N, N, N, N, N, -0.5, 1.5, nsd});
+    add(J_S, {P.W, P.N0, P.W, P.Sr, N, N, N, N, N, N, N, 0.5, 0.5, &P.sc->skip_s0});
+    add(J_S1, {P.W, P.N1, P.W, P.Sr, N, N, N, N, N, N, N, 0.5, 0.5, &P.sc->skip_s1});
+  }
+  int rc = 1;
+  do {
+    if (hipMemcpy(dj, jobs.data(), jobs.size() * sizeof(GemmJob), hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        hipMemcpy(dp, hp.data(), nm * sizeof(Part), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(sc, hs.data(), nm * sizeof(Scal), hipMemcpyHostToDevice) != hipSuccess)
+      break;
+    if (psd_project(JL, dp, nm, N, eps, fuse_err, force_jacobi != 0, X, 0) != hipSuccess) break;
+    if (hipDeviceSynchronize() != hipSuccess) break;
+    // S = (Sr + Sr^T) / 2 on the host side of the copy (test hook only)
+    std::vector<double> sr(NN);
+    bool ok = true;
+    for (int p = 0; p < nm && ok; ++p) {
+      ok = hipMemcpy(sr.data(), hp[p].Sr, NN * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess;
+      std::vector<double> o(NN);
+      for (int j = 0; j < N; ++j)
+        for (int i = 0; i < N; ++i)
+          o[i + (size_t)j * N] = 0.5 * (sr[i + (size_t)j * N] + sr[j + (size_t)i * N]);
+      ok = ok && hipMemcpy(S + p * NN, o.data(), NN * sizeof(double), hipMemcpyHostToDevice) ==
+                     hipSuccess;
+    }
+    if (!ok) break;
+    if (jacobi_used) {
+      if (hipMemcpy(hs.data(), sc, nm * sizeof(Scal), hipMemcpyDeviceToHost) != hipSuccess) break;
+      for (int p = 0; p < nm; ++p) jacobi_used[p] = hs[p].jacobi;
+    }
+    rc = 0;
+  } while (0);
+  (void)hipFree(buf);
+  (void)hipFree(sc);
+  (void)hipFree(dp);
+  (void)hipFree(dj);
+  return rc;
 }

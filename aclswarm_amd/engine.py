@@ -191,8 +191,9 @@ def admm_design(pts, adj, params=None, stream=None):
 
     pts [F][n][3] f64 and adj [F][n][n] f64 (0/1, symmetric) on the device.
     Returns (gains [F][3n][3n] f64 with gains[f][r][c] = GainMat(r, c),
-    iters [F][2] int32: ADMM iterations of the xy and z designs, negative if
-    that part's sign iteration did not converge).
+    iters [F][2] int32: ADMM iterations of the xy and z designs; a PSD
+    projection the sign iteration does not resolve is made by the Jacobi
+    eigensolver fallback).
     """
     lib = L.lib()
     F, n = int(pts.shape[0]), int(pts.shape[1])

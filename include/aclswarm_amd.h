@@ -524,7 +524,11 @@ acl_status_t acl_generate_formation_groups(int32_t F, int32_t n, const uint32_t*
  * F formations of n points: pts [F][3][n] column-major 3 x n per formation
  * (Eigen::Matrix<double,3,Dynamic>), adj [F][n][n] f64 (symmetric 0/1),
  * gains out [F][3n][3n] column-major. Device pointers. iters [F][2]
- * (2-D and 1-D ADMM iteration counts, may be NULL). */
+ * (2-D and 1-D ADMM iteration counts, may be NULL). The PSD projection of
+ * each ADMM iteration (eigenvalues > epsEig kept, solver.cpp:296-316) is a
+ * Newton-Schulz matrix-sign iteration on the matrix cores; a part whose sign
+ * iteration does not converge in 64 steps (an eigenvalue within ~1e-11 |W|
+ * of epsEig) is projected by a Jacobi eigendecomposition instead. */
 acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double* pts,
                                   const double* adj, double* gains,
                                   int32_t* iters,

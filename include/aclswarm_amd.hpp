@@ -699,8 +699,7 @@ class Solver {
     detail::check(acl_stream_synchronize(nullptr));
   }
 
-  /* ADMM iteration counts of the last solve (2-D, 1-D); negative when the
-   * PSD projection's sign iteration did not converge (aclswarm_amd.h). */
+  /* ADMM iteration counts of the last solve (2-D, 1-D). */
   int iterations2d() const { return iters_[0]; }
   int iterations1d() const { return iters_[1]; }
 

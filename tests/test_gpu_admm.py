@@ -93,3 +93,62 @@ def test_admm_abi_errors():
     prm = L.default_admm_params()
     assert lib.acl_admm_solve_batch(1, 2, None, None, None, None, ct.byref(prm), None) != 0
     assert lib.acl_admm_solve_batch(0, 10, None, None, None, None, ct.byref(prm), None) == 0
+
+
+def _psd_ref(W, eps):
+    """The reference's projection: keep the eigenvalues > eps (solver.cpp:296-316,
+    ADMMGainDesign2D.m:430-445; admm_oracle.Part.run's eigh form)."""
+    d, V = np.linalg.eigh(W)
+    pos = d > eps
+    return (V[:, pos] * d[pos]) @ V[:, pos].T
+
+
+def _spectrum_case(rng, N, near, eps=1e-5):
+    """Symmetric N x N W with |W|_2 = 1 and eigenvalues at eps +- near (and
+    eps exactly when near == 0), the rest spread over [-1, 1]."""
+    lam = rng.uniform(-1.0, 1.0, N)
+    lam[0], lam[1] = 1.0, -1.0
+    lam[2], lam[3] = eps + near, eps - near
+    Q, _ = np.linalg.qr(rng.normal(size=(N, N)))
+    W = (Q * lam) @ Q.T
+    return 0.5 * (W + W.T)
+
+
+def _psd_gpu(Ws, eps, force):
+    import ctypes as ct
+    import torch
+    from aclswarm_amd import _lib as L
+    dev = torch.device("cuda:0")
+    nm, N = len(Ws), Ws[0].shape[0]
+    W = torch.from_numpy(np.stack([np.asfortranarray(w).T.copy() for w in Ws])).to(dev)
+    S = torch.empty_like(W)
+    used = (ct.c_int * nm)()
+    rc = L.lib().acl_internal_psd_project(nm, N, ct.c_void_p(W.data_ptr()), eps,
+                                          ct.c_void_p(S.data_ptr()), int(force), used)
+    assert rc == 0
+    # column-major device matrices: transpose back (symmetric anyway)
+    return [m.T for m in S.cpu().numpy()], list(used)
+
+
+@pytest.mark.parametrize("N", [40, 392])
+def test_psd_projection_near_eps(N):
+    """The ADMM PSD step on spectra with eigenvalues near epsEig, against the
+    eigendecomposition projection the reference uses. 1e-3 |W| away: the
+    Newton-Schulz sign converges (slowly) and is used; 1e-12 |W| away: it
+    cannot converge in 64 steps and the Jacobi eigensolver fallback makes the
+    projection; both within 1e-9 |W| (a misclassified eigenvalue would cost
+    ~1e-5). The fallback forced on a well-separated spectrum agrees too."""
+    rng = np.random.RandomState(900 + N)
+    eps = 1e-5
+    Ws = [_spectrum_case(rng, N, 1e-3), _spectrum_case(rng, N, 1e-12),
+          _spectrum_case(rng, N, 0.3)]
+    S, used = _psd_gpu(Ws, eps, force=False)
+    assert used == [0, 1, 0], used
+    for k, W in enumerate(Ws):
+        err = np.abs(S[k] - _psd_ref(W, eps)).max()
+        assert err <= 1e-9, (k, err)
+    S2, used2 = _psd_gpu(Ws, eps, force=True)
+    assert used2 == [1, 1, 1], used2
+    for k, W in enumerate(Ws):
+        err = np.abs(S2[k] - _psd_ref(W, eps)).max()
+        assert err <= 1e-11, (k, err)
