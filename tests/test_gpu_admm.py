@@ -137,7 +137,10 @@ def test_psd_projection_near_eps(N):
     Newton-Schulz sign converges (slowly) and is used; 1e-12 |W| away: it
     cannot converge in 64 steps and the Jacobi eigensolver fallback makes the
     projection; both within 1e-9 |W| (a misclassified eigenvalue would cost
-    ~1e-5). The fallback forced on a well-separated spectrum agrees too."""
+    ~1e-5; the pair eps +- 1e-12 is a near-degenerate pair whose eigenvectors
+    are determined only to ~1e-16 / 2e-12, in any eigensolver, so the kept
+    one's direction carries ~1e-11 of the projection). The fallback forced
+    on every spectrum agrees too."""
     rng = np.random.RandomState(900 + N)
     eps = 1e-5
     Ws = [_spectrum_case(rng, N, 1e-3), _spectrum_case(rng, N, 1e-12),
@@ -151,4 +154,4 @@ def test_psd_projection_near_eps(N):
     assert used2 == [1, 1, 1], used2
     for k, W in enumerate(Ws):
         err = np.abs(S2[k] - _psd_ref(W, eps)).max()
-        assert err <= 1e-11, (k, err)
+        assert err <= (1e-9 if k == 1 else 1e-12), (k, err)

@@ -34,7 +34,6 @@ def c3():
     gen.manual_seed(2024)
     w = workload.simform_workload(B, N, gen, dev, L=40.0, complete=False, planes=5, seed0=0)
     T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"], w["planes"])
-    T.tile_gains()
     return w, T
 
 
