@@ -56,6 +56,9 @@ namespace acl_amd {
 #define ACL_AUCTION_LEVELS 4   // price levels per dirty column before the exact scan
 #endif
 constexpr int kAL = ACL_AUCTION_LEVELS;
+#ifndef ACL_FUSED_PREFETCH
+#define ACL_FUSED_PREFETCH 2  // the fused control phase's record prefetch (control_dev.h)
+#endif
 
 __host__ __device__ inline int a16(int x) { return (x + 15) & ~15; }
 
@@ -1113,10 +1116,13 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   // to gain_kernel (launch_control which = 2).
   if constexpr (FUSE) {
     if (!uniform) return;  // workgroup-uniform
+#ifdef ACL_EXP_SKIP_GAIN
+    return;  // diagnostic builds: the fused kernel without its control phase
+#endif
     __syncthreads();       // T, C and the hand-off reads are done
     const PairLayout GL = make_pair_layout(n, kAW, false);
     if (tid < n) reinterpret_cast<uint16_t*>(smem + GL.Pt)[tid] = (uint16_t)ptv;
-    pair_gain_swarm<kAW, false, GM, false>(P.ctl, b, f, smem, tid, kAB, nullptr);
+    pair_gain_swarm<kAW, false, GM, ACL_FUSED_PREFETCH>(P.ctl, b, f, smem, tid, kAB, nullptr);
   }
 }
 

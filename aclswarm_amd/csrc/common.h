@@ -190,6 +190,24 @@ __device__ __forceinline__ double fma_k(double a, double b) {
 }
 #define ACL_FMA_K(a, b, c) fma_k<__builtin_bit_cast(unsigned long long, (double)(c))>(a, b)
 
+// a * C1 + C2 (two roundings) for compile-time constants, both built in the
+// reserved SGPR pair: no VGPR holds a hoisted constant across a loop (the
+// fused auction + control kernel runs its gain loop at the 80-VGPR limit).
+template <unsigned long long C1, unsigned long long C2>
+__device__ __forceinline__ double mul_add_k(double a) {
+  double r;
+  asm("s_mov_b32 s98, %2\n\ts_mov_b32 s99, %3\n\tv_mul_f64 %0, %1, s[98:99]\n\t"
+      "s_mov_b32 s98, %4\n\ts_mov_b32 s99, %5\n\tv_add_f64 %0, %0, s[98:99]"
+      : "=&v"(r)
+      : "v"(a), "i"((unsigned)(C1 & 0xffffffffu)), "i"((unsigned)(C1 >> 32)),
+        "i"((unsigned)(C2 & 0xffffffffu)), "i"((unsigned)(C2 >> 32))
+      : "s98", "s99");
+  return r;
+}
+#define ACL_MUL_ADD_K(a, c1, c2)                                       \
+  mul_add_k<__builtin_bit_cast(unsigned long long, (double)(c1)),    \
+            __builtin_bit_cast(unsigned long long, (double)(c2))>(a)
+
 __device__ __forceinline__ double acl_atan_tab(double x, const double* tab) {
   const double ax = fabs(x);
   const int id = (ax >= 0.4375) + (ax >= 0.6875) + (ax >= 1.1875) + (ax >= 2.4375);
@@ -272,7 +290,7 @@ __device__ __forceinline__ double acl_atan_k32(double x, const double* tab) {
   r = __builtin_fma(__builtin_fma(-den, r, 1.0), r, r);
   const double t = num * r;
   const double z = t * t;
-  double p = __builtin_fma(z, 1.0 / 9.0, -1.0 / 7.0);
+  double p = ACL_MUL_ADD_K(z, 1.0 / 9.0, -1.0 / 7.0);
   p = ACL_FMA_K(z, p, 1.0 / 5.0);
   p = ACL_FMA_K(z, p, -1.0 / 3.0);
   const double res = rw[4] + __builtin_fma(t * z, p, t);
@@ -334,6 +352,11 @@ __device__ __forceinline__ void margin_track(MarginPair& m, float hi, float lo) 
     m.hi = hi;
     m.lo = lo;
   }
+}
+
+// this lane's bit of a wave lane mask (a per-lane predicate, no VALU)
+__device__ __forceinline__ bool lanebit_u64(unsigned long long m) {
+  return __builtin_amdgcn_inverse_ballot_w64(m);
 }
 
 // a per-lane flag held as a VGPR integer (0 or 1), combined with bitwise

@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kern
   const int b = P.b0 + blockIdx.x;
   if (P.status[b].flags & ACL_SWARM_BAD_INPUT) return;
   if (P.wsMode[b] != 0) return;  // per-vehicle assignments: gain_kernel
-  pair_gain_swarm<kCtlWaves, kTiled, GM, true>(P, b, P.fidx[b], smem, threadIdx.x, kCtlBlock,
+  pair_gain_swarm<kCtlWaves, kTiled, GM, 1>(P, b, P.fidx[b], smem, threadIdx.x, kCtlBlock,
                                                P.wsPt + (size_t)b * P.n);
 }
 
@@ -519,7 +519,13 @@ __device__ __forceinline__ bool ca_resolve_wave(int lane, int nslot, const doubl
   return true;
 }
 
-__global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
+#ifndef ACL_CA_WAVES_PER_SIMD
+#define ACL_CA_WAVES_PER_SIMD 1
+#endif
+#ifndef ACL_CA_GRID
+#define ACL_CA_GRID 1024
+#endif
+__global__ void __launch_bounds__(64 * kCaWaves, ACL_CA_WAVES_PER_SIMD) ca_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const int NW = (n + 63) >> 6;
@@ -779,7 +785,7 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
     if (lds > 64 * 1024)
       (void)hipFuncSetAttribute((const void*)ca_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(ca_kernel, dim3(nb < 1024 ? nb : 1024), dim3(64 * kCaWaves), lds, stream,
+    hipLaunchKernelGGL(ca_kernel, dim3(nb < ACL_CA_GRID ? nb : ACL_CA_GRID), dim3(64 * kCaWaves), lds, stream,
                        P);
   }
   return hipGetLastError();

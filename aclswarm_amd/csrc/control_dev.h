@@ -254,7 +254,7 @@ __device__ __forceinline__ double swap_sum(double x) {
 }
 
 struct PairLayout {
-  int q, qf, p, pn, adjF, rowpre, Pt, acc, out, atab, tmask, tstart, gmw, total;
+  int q, qf, p, pn, adjF, rowpre, etab, Pt, acc, out, atab, tmask, tstart, gmw, total;
 };
 
 __host__ __device__ inline PairLayout make_pair_layout(int n, int kW = kCtlWaves, bool tiled = true) {
@@ -267,6 +267,7 @@ __host__ __device__ inline PairLayout make_pair_layout(int n, int kW = kCtlWaves
   L.pn = o;     o = cal16(o + n * 2 * 8);
   L.adjF = o;   o = cal16(o + n * NW * 8);
   L.rowpre = o; o = cal16(o + (n * NW + 1) * 4);
+  L.etab = o;   o = cal16(o + n * ((n + 7) >> 3) * 4);  // [i][J] record base << 8 | column bits
   L.Pt = o;     o = cal16(o + n * 2);
   L.acc = o;    o = cal16(o + kW * n * 3 * 8);       // per-wave u partial sums (row order)
   L.out = o;    o = cal16(o + n * 3 * 8);            // u per vehicle
@@ -297,16 +298,17 @@ __host__ __device__ inline PairLayout make_pair_layout(int n, int kW = kCtlWaves
 // and column sums (over r) are butterfly shuffles; each wave accumulates into
 // its own u array in LDS in a fixed tile order, and the kW arrays are added in
 // wave order: deterministic for a given kW (tolerance-based parity, 1e-5
-// relative). kPrefetch: the next tile's two 40-byte records are loaded into
-// registers before the current tile's math (20 VGPRs; the stand-alone
-// kernel), else each tile's loads are waited for (the fused kernel, whose
-// co-resident auctions cover the latency and which must stay within 80 VGPRs).
+// relative). kPrefetch: 1 -- the next tile's two 40-byte records are loaded
+// into registers before the current tile's math (20 VGPRs; the stand-alone
+// kernel); 2 -- loaded once the current tile's scale terms are done (the fused
+// kernel, which must stay within 80 VGPRs: the records then are not live
+// across the atan evaluations); 0 -- each tile's loads are waited for.
 //
 // LDS: make_pair_layout(n, kW, kTiled) at `smem`. The caller has written
 // Pt (formation point -> vehicle) into L.Pt, or passes the global row Ptg.
 // Ends with the epilogue (saturation, the collision test, u / u_safe /
 // ca_flag / gate_margin writes) over nthreads threads.
-template <int kW, bool kTiled, bool GM, bool kPrefetch>
+template <int kW, bool kTiled, bool GM, int kPrefetch>
 __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f,
                                                 unsigned char* smem, int tid, int nthreads,
                                                 const uint16_t* Ptg) {
@@ -382,6 +384,22 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
   int* tstart = reinterpret_cast<int*>(smem + L.tstart);
   if (kTiled && wave == (kW > 1 ? 1 : 0)) build_tiles(adjF, NW, n, lane, tmask, tstart);
   __syncthreads();
+  // record table of the 8-column blocks: etab[i][J] = (index of row i's first
+  // edge at a column >= 8J) << 8 | adjmat(i, 8J .. 8J + 7) bits; a lane's
+  // record is then one LDS read and a byte popcount (row-major records)
+  const int nbk = (n + 7) >> 3;
+  unsigned* etab = reinterpret_cast<unsigned*>(smem + L.etab);
+  if (!kTiled) {
+    for (int k = tid; k < n * nbk; k += nthreads) {
+      const int i = k / nbk, J = k - i * nbk;
+      const int w = (8 * J) >> 6, sh = (8 * J) & 63;
+      const unsigned long long word = adjF[i * NW + w];
+      const unsigned below = (unsigned)__popcll(sh ? (word & ((1ull << sh) - 1ull)) : 0ull);
+      etab[k] = ((unsigned)(rowpre[i * NW + w] + (int)below) << 8) |
+                (unsigned)((word >> sh) & 0xFFull);
+    }
+    __syncthreads();
+  }
 
   double gmxy = __builtin_inf(), gmz = __builtin_inf();
   if (inw) {
@@ -391,16 +409,23 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
         __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 5 * E * 8, 0x00020000);
     const acl_cntrl_gains_t g = P.g;
     const int r = lane >> 3, c = lane & 7;
-    const int nb = (n + 7) >> 3;
+    const int nb = nbk;
     const int NT = nb * (nb + 1) / 2;
     double* myacc = acc + wave * n * 3;
+    // this wave's tiles: a contiguous range of the row-block-major order, so
+    // consecutive tiles mostly share their row block I and the row sums can
+    // stay per lane in registers until the block changes
+    const int t0 = (wave * NT) / kW, t1 = ((wave + 1) * NT) / kW;
 
-    // edge index of (i, j), -1 if adjmat(i, j) == 0
-    auto edge_idx = [&](int i, int j) -> int {
-      const int jw = j >> 6, jb = j & 63;
-      const unsigned long long word = adjF[i * NW + jw];
-      if (!((word >> jb) & 1ull)) return -1;
-      return rowpre[i * NW + jw] + __popcll(word & ((1ull << jb) - 1ull));
+    // record of (i, j) in column block J (cc = j - 8J), -1 if no edge
+    auto rec_of = [&](int i, int J, int cc) -> int {
+      const unsigned x = etab[i * nb + J];
+      if (!((x >> cc) & 1u)) return -1;
+      // (1 << cc) - 1 made where it is used (v_bfm_b32; volatile: a hoisted
+      // per-lane mask would hold a VGPR across the loop)
+      unsigned below;
+      asm volatile("v_bfm_b32 %0, %1, 0" : "=v"(below) : "v"(cc));
+      return (int)(x >> 8) + __popc(x & below);
     };
     auto load_rec = [&](int e, double (&Lg)[5]) {
       const int voff = e >= 0 ? e * 40 : 0x40000000;  // past num_records -> 0
@@ -421,12 +446,10 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
       I = ii;
       J = ii + rem;
     };
-    auto lane_pair = [&](int t, int& i, int& j, int& eij, int& eji) {
+    auto lane_pair = [&](int t, int I, int J, int& i, int& j, int& eij, int& eji) {
       eij = eji = -1;
       i = j = 0;
-      if (t >= NT) return;
-      int I, J;
-      tile_of(t, I, J);
+      if (t >= t1) return;
       i = 8 * I + r;
       j = 8 * J + c;
       if (i >= n || j >= n || (I == J && r > c)) {
@@ -445,43 +468,75 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
                                                     __builtin_amdgcn_mbcnt_lo((unsigned)m2, 0u));
         return;
       }
-      eij = edge_idx(i, j);
-      if (i != j) eji = edge_idx(j, i);
+      eij = rec_of(i, J, c);
+      if (i != j) eji = rec_of(j, I, r);
     };
 
-    int i_c = 0, j_c = 0, eij_c = -1, eji_c = -1;
+    int I = 0, J = 0;
+    if (t0 < t1) tile_of(t0, I, J);
+    // a tile's lanes with a record in each direction, as lane masks (SGPRs:
+    // the pair indices are 8I + r, 8J + c, nothing else stays in VGPRs)
+    unsigned long long m_ij = 0ull, m_ji = 0ull;
     double Aij[5], Aji[5];
-    if (kPrefetch) {
-      lane_pair(wave, i_c, j_c, eij_c, eji_c);
-      load_rec(eij_c, Aij);
-      load_rec(eji_c, Aji);
+    if (kPrefetch != 0) {
+      int i0, j0, e0, e1;
+      lane_pair(t0, I, J, i0, j0, e0, e1);
+      m_ij = __ballot(e0 >= 0);
+      m_ji = __ballot(e1 >= 0);
+      load_rec(e0, Aij);
+      load_rec(e1, Aji);
     }
+    // row sums of the current row block, per lane (row 8I + r, this lane's c)
+    double ra0 = 0.0, ra1 = 0.0, ra2 = 0.0;
 #pragma unroll 1
-    for (int t = wave; t < NT; t += kW) {
-      int i_n = 0, j_n = 0, eij_n = -1, eji_n = -1;
-      double Bij[5], Bji[5];
-      if (kPrefetch) {
-        lane_pair(t + kW, i_n, j_n, eij_n, eji_n);
-        load_rec(eij_n, Bij);
-        load_rec(eji_n, Bji);
-      } else {
-        lane_pair(t, i_c, j_c, eij_c, eji_c);
-        load_rec(eij_c, Aij);
-        load_rec(eji_c, Aji);
+    for (int t = t0; t < t1; ++t) {
+      int In = I, Jn = J;  // the next tile
+      if (++Jn == nb) {
+        ++In;
+        Jn = In;
       }
+      unsigned long long mn_ij = 0ull, mn_ji = 0ull;
+      double Bij[5], Bji[5];
+      auto prefetch_next = [&]() {
+        int i1, j1, e0, e1;
+        lane_pair(t + 1, In, Jn, i1, j1, e0, e1);
+        mn_ij = __ballot(e0 >= 0);
+        mn_ji = __ballot(e1 >= 0);
+        load_rec(e0, Bij);
+        load_rec(e1, Bji);
+      };
+      if (kPrefetch == 1) {
+        prefetch_next();
+      } else if (kPrefetch == 0) {
+        int i0, j0, e0, e1;
+        lane_pair(t, I, J, i0, j0, e0, e1);
+        m_ij = __ballot(e0 >= 0);
+        m_ji = __ballot(e1 >= 0);
+        load_rec(e0, Aij);
+        load_rec(e1, Aji);
+      }
+      const bool has_ij = lanebit_u64(m_ij), has_ji = lanebit_u64(m_ji);
       double rs0 = 0.0, rs1 = 0.0, rs2 = 0.0, cs0 = 0.0, cs1 = 0.0, cs2 = 0.0;
-      if (eij_c >= 0 || eji_c >= 0) {
+#ifdef ACL_EXP_GAIN_STREAM_ONLY
+      // diagnostic builds: the record stream without the edge math
+      rs0 = Aij[0] + Aji[1]; rs1 = Aij[2] + Aji[3]; rs2 = Aij[4] + Aji[4];
+      const bool anyedge = false;
+#else
+      const bool anyedge = has_ij || has_ji;
+#endif
+      double q0 = 0.0, q1 = 0.0, q2 = 0.0, Fxy = 0.0, Fz = 0.0;
+      if (anyedge) {
 #pragma clang fp contract(fast)
-        const int i = i_c, j = j_c;
-        const double q0 = qf[3 * j] - qf[3 * i], q1 = qf[3 * j + 1] - qf[3 * i + 1],
-                     q2 = qf[3 * j + 2] - qf[3 * i + 2];
+        const int i = 8 * I + r, j = 8 * J + c;
+        q0 = qf[3 * j] - qf[3 * i];
+        q1 = qf[3 * j + 1] - qf[3 * i + 1];
+        q2 = qf[3 * j + 2] - qf[3 * i + 2];
         const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
         const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
         const double dxy = ACL_GAIN_SQRT((pn[2 * i] + pn[2 * j]) - 2.0 * (pix * pjx + piy * pjy));
         const double dz = ACL_GAIN_SQRT((pn[2 * i + 1] + pn[2 * j + 1]) - 2.0 * (piz * pjz));
         const double e_xy = ACL_GAIN_SQRT(q0 * q0 + q1 * q1) - dxy;
         const double e_z = fabs(q2) - dz;
-        double Fxy = 0.0, Fz = 0.0;
         bool gxy, gz;
         gate_decide<GM>(g, e_xy, e_z, q0, q1, q2, pn[2 * i], pn[2 * j], pn[2 * i + 1],
                         pn[2 * j + 1], pix, piy, piz, pjx, pjy, pjz, gxy, gz, gmxy, gmz);
@@ -494,15 +549,24 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
             if (kk) Fz = fa; else Fxy = fa;
           }
         }
+      }
+      if (kPrefetch == 2) {
+        // the next tile's records, issued once the scale terms are done (the
+        // registers they need are free from here on): their latency is
+        // covered by this tile's block products, sums and LDS updates
+        prefetch_next();
+      }
+      if (anyedge) {
+#pragma clang fp contract(fast)
         // (0,0) (0,1) (1,0) (1,1) (2,2) stored; the structural zeros still
         // multiply q (solver.cpp:49-77, NaN propagation as the 3x3 product)
-        if (eij_c >= 0) {
+        if (has_ij) {
           const double up0 = ((Aij[0] * q0 + Aij[1] * q1) + 0.0 * q2) + Fxy * q0;
           const double up1 = ((Aij[2] * q0 + Aij[3] * q1) + 0.0 * q2) + Fxy * q1;
           const double up2 = ((0.0 * q0 + 0.0 * q1) + Aij[4] * q2) + Fz * q2;
           rs0 = g.kp * up0; rs1 = g.kp * up1; rs2 = g.kp * up2;
         }
-        if (eji_c >= 0) {
+        if (has_ji) {
           const double m0 = -q0, m1 = -q1, m2 = -q2;  // q_ji
           const double up0 = ((Aji[0] * m0 + Aji[1] * m1) + 0.0 * m2) + Fxy * m0;
           const double up1 = ((Aji[2] * m0 + Aji[3] * m1) + 0.0 * m2) + Fxy * m1;
@@ -510,34 +574,41 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
           cs0 = g.kp * up0; cs1 = g.kp * up1; cs2 = g.kp * up2;
         }
       }
-      // row sums over c (lanes 8r .. 8r + 7), column sums over r (stride 8)
-      // (DPP for the steps inside a 16-lane row: quad_perm xor 1, xor 2, then
-      // row_half_mirror -- after the quad sums lane 8r + c reads the other
-      // quad's sum -- and row_ror:8 = xor 8; the same additions in the same
-      // order as the xor butterfly)
-      rs0 += dpp_f64_all<0xB1>(rs0); rs1 += dpp_f64_all<0xB1>(rs1); rs2 += dpp_f64_all<0xB1>(rs2);
-      rs0 += dpp_f64_all<0x4E>(rs0); rs1 += dpp_f64_all<0x4E>(rs1); rs2 += dpp_f64_all<0x4E>(rs2);
-      rs0 += dpp_f64_all<0x141>(rs0); rs1 += dpp_f64_all<0x141>(rs1); rs2 += dpp_f64_all<0x141>(rs2);
+      ra0 += rs0; ra1 += rs1; ra2 += rs2;
+      // column sums over r (stride 8): DPP row_ror:8 = xor 8, then gfx950's
+      // v_permlane{16,32}_swap for xor 16 and xor 32 (the same additions in
+      // the same order as the xor butterfly)
       cs0 += dpp_f64_all<0x128>(cs0); cs1 += dpp_f64_all<0x128>(cs1); cs2 += dpp_f64_all<0x128>(cs2);
       cs0 = swap_sum<16>(cs0); cs1 = swap_sum<16>(cs1); cs2 = swap_sum<16>(cs2);
       cs0 = swap_sum<32>(cs0); cs1 = swap_sum<32>(cs1); cs2 = swap_sum<32>(cs2);
       {
-        int I, J;
-        tile_of(t, I, J);
-        const int ri = 8 * I + r, cj = 8 * J + c;
-        if (c == 0 && ri < n) {
-          myacc[3 * ri] += rs0; myacc[3 * ri + 1] += rs1; myacc[3 * ri + 2] += rs2;
-        }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
+        const int cj = 8 * J + c;
         if (r == 0 && cj < n) {
           myacc[3 * cj] += cs0; myacc[3 * cj + 1] += cs1; myacc[3 * cj + 2] += cs2;
         }
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
       }
-      if (kPrefetch) {
-        i_c = i_n; j_c = j_n; eij_c = eij_n; eji_c = eji_n;
+      if (t + 1 == t1 || In != I) {
+        // the row block ends: row sums over c (lanes 8r .. 8r + 7; DPP
+        // quad_perm xor 1, xor 2, then row_half_mirror -- after the quad sums
+        // lane 8r + c reads the other quad's sum)
+        ra0 += dpp_f64_all<0xB1>(ra0); ra1 += dpp_f64_all<0xB1>(ra1); ra2 += dpp_f64_all<0xB1>(ra2);
+        ra0 += dpp_f64_all<0x4E>(ra0); ra1 += dpp_f64_all<0x4E>(ra1); ra2 += dpp_f64_all<0x4E>(ra2);
+        ra0 += dpp_f64_all<0x141>(ra0); ra1 += dpp_f64_all<0x141>(ra1); ra2 += dpp_f64_all<0x141>(ra2);
+        const int ri = 8 * I + r;
+        if (c == 0 && ri < n) {
+          myacc[3 * ri] += ra0; myacc[3 * ri + 1] += ra1; myacc[3 * ri + 2] += ra2;
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        ra0 = ra1 = ra2 = 0.0;
+      }
+      I = In;
+      J = Jn;
+      if (kPrefetch != 0) {
+        m_ij = mn_ij;
+        m_ji = mn_ji;
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
           Aij[k] = Bij[k];
