@@ -267,7 +267,8 @@ __host__ __device__ inline PairLayout make_pair_layout(int n, int kW = kCtlWaves
   L.pn = o;     o = cal16(o + n * 2 * 8);
   L.adjF = o;   o = cal16(o + n * NW * 8);
   L.rowpre = o; o = cal16(o + (n * NW + 1) * 4);
-  L.etab = o;   o = cal16(o + n * ((n + 7) >> 3) * 4);  // [i][J] record base << 8 | column bits
+  L.etab = o;   // [i][J] record base << 8 | column bits (n <= 128; else edge_idx from adjF)
+  o = cal16(o + (n <= kMaxN ? n * ((n + 7) >> 3) * 4 : 0));
   L.Pt = o;     o = cal16(o + n * 2);
   L.acc = o;    o = cal16(o + kW * n * 3 * 8);       // per-wave u partial sums (row order)
   L.out = o;    o = cal16(o + n * 3 * 8);            // u per vehicle
@@ -389,7 +390,8 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
   // record is then one LDS read and a byte popcount (row-major records)
   const int nbk = (n + 7) >> 3;
   unsigned* etab = reinterpret_cast<unsigned*>(smem + L.etab);
-  if (!kTiled) {
+  const bool use_etab = n <= kMaxN;
+  if (!kTiled && use_etab) {
     for (int k = tid; k < n * nbk; k += nthreads) {
       const int i = k / nbk, J = k - i * nbk;
       const int w = (8 * J) >> 6, sh = (8 * J) & 63;
@@ -419,6 +421,12 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
 
     // record of (i, j) in column block J (cc = j - 8J), -1 if no edge
     auto rec_of = [&](int i, int J, int cc) -> int {
+      if (!use_etab) {  // n > 128: the row's bit words and prefixes
+        const int j = 8 * J + cc, jw = j >> 6, jb = j & 63;
+        const unsigned long long word = adjF[i * NW + jw];
+        if (!((word >> jb) & 1ull)) return -1;
+        return rowpre[i * NW + jw] + __popcll(word & ((1ull << jb) - 1ull));
+      }
       const unsigned x = etab[i * nb + J];
       if (!((x >> cc) & 1u)) return -1;
       // (1 << cc) - 1 made where it is used (v_bfm_b32; volatile: a hoisted
