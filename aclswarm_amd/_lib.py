@@ -22,7 +22,7 @@ FLAG_CHANGED = 0x04
 FLAG_NONFINITE = 0x08
 FLAG_BAD_INPUT = 0x10
 FLAG_CA_ACTIVE = 0x20
-ABI_VERSION = 4  # include/aclswarm_amd.h ACL_ABI_VERSION
+ABI_VERSION = 5  # include/aclswarm_amd.h ACL_ABI_VERSION
 FLAG_FRAGILE = 0x40
 FRAGILE_MARGIN = 1e-6
 
@@ -102,7 +102,7 @@ class EpisodeParams(ct.Structure):
     trial.sh:96, supervisor.py:47,61-62,121)."""
     _fields_ = [("control_dt", ct.c_double), ("auction_every", ct.c_int32),
                 ("sample_every", ct.c_int32), ("bufflen", ct.c_int32),
-                ("reserved", ct.c_int32), ("max_accel_xy", ct.c_double),
+                ("auction_latency", ct.c_int32), ("max_accel_xy", ct.c_double),
                 ("max_accel_z", ct.c_double), ("bounds_min", ct.c_double * 3),
                 ("bounds_max", ct.c_double * 3), ("orig_zero_vel_thr", ct.c_double),
                 ("avg_active_ca_thr", ct.c_double)]
@@ -112,7 +112,9 @@ EPISODE_STATUS_DTYPE = np.dtype([("converged_step", "<i4"), ("gridlock_step", "<
                                  ("converged", "<i4"), ("gridlocked", "<i4"),
                                  ("n_auctions", "<u2"), ("n_invalid", "<u2"),
                                  ("n_skipped", "<u2"), ("n_disagree", "<u2"),
-                                 ("n_samples", "<u4"), ("n_ca_steps", "<u4")])
+                                 ("n_samples", "<u4"), ("n_ca_steps", "<u4"),
+                                 ("pending_step", "<i4"), ("n_restarted", "<u2"),
+                                 ("reserved", "<u2")])
 
 
 class EpisodeArgs(ct.Structure):

@@ -1123,6 +1123,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     const PairLayout GL = make_pair_layout(n, kAW, false);
     if (tid < n) reinterpret_cast<uint16_t*>(smem + GL.Pt)[tid] = (uint16_t)ptv;
     pair_gain_swarm<kAW, false, GM, ACL_FUSED_PREFETCH>(P.ctl, b, f, smem, tid, kAB, nullptr);
+    if (!ACL_AUCTION_PROF) stamp_phase(P, b, tid, 7);  // diagnostic: end of the control phase
   }
 }
 

@@ -34,7 +34,7 @@ constexpr int kEpBlock = 128;
 // Episode workspace: the solve/control workspace, then the auction's output
 // and the control stage's output of the current step.
 struct EpLayout {
-  size_t solve, Pnew, st, cst, u, us, ca, total;
+  size_t solve, Pnew, st, cst, u, us, ca, lat, total;
 };
 
 inline EpLayout ep_layout(int n, int B) {
@@ -48,38 +48,96 @@ inline EpLayout ep_layout(int n, int B) {
   L.u = o;     o = ws_al(o + bb * nb * 3 * 8);
   L.us = o;    o = ws_al(o + bb * nb * 3 * 8);
   L.ca = o;    o = ws_al(o + bb * nb);
+  L.lat = o;   o = ws_al(o + bb * 4);  // per-swarm auction latency (control steps)
   L.total = o;
   return L;
 }
 
-// autoauctionCb after the auction of this tick: a swarm flagged by the last
-// auction (didConvergeOnInvalidAssignment) flushes and skips this one;
-// otherwise an agreed valid result is adopted, an agreed invalid one sets
-// the flag, and a disagreeing swarm keeps its assignment.
-__global__ void __launch_bounds__(64) adopt_kernel(int n, uint16_t* P, const uint16_t* Pnew,
+// An auction's latency in control steps, per swarm (acl_episode_params_t::
+// auction_latency): fixed, or the reference's timing -- one bid processed per
+// auctioneer_dt = 1 ms tick (coordination.launch:23, auctioneer.cpp:139-160)
+// and every neighbour's bid needed in each of the 2n rounds
+// (auctioneer.cpp:198-241): ceil(2 n d_max 1 ms / control_dt), d_max the
+// largest degree of the swarm's formation graph (the slowest vehicle gates
+// its neighbours' rounds, and transitively the swarm's).
+constexpr double kAuctioneerDt = 0.001;
+
+__global__ void __launch_bounds__(64) latency_kernel(int n, const int32_t* fidx, int F,
+                                                     const uint64_t* adj, int mode,
+                                                     double control_dt, int32_t* lat) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  if (mode >= 0) {
+    if (lane == 0) lat[b] = mode;
+    return;
+  }
+  const int f = fidx[b];
+  const int NW = (n + 63) >> 6;
+  int dmax = 0;
+  if (f >= 0 && f < F) {
+    const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+    for (int i = lane; i < n; i += 64) {
+      int d = 0;
+      for (int w = 0; w < NW; ++w) {
+        unsigned long long x = adj[((size_t)f * n + i) * NW + w];
+        if (w == NW - 1) x &= lastmask;
+        d += __popcll(x & ~(w == (i >> 6) ? (1ull << (i & 63)) : 0ull));
+      }
+      dmax = d > dmax ? d : dmax;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const int y = __shfl_xor(dmax, o, 64);
+    dmax = y > dmax ? y : dmax;
+  }
+  if (lane == 0) lat[b] = (int32_t)ceil(2.0 * n * dmax * kAuctioneerDt / control_dt);
+}
+
+// CoordinationROS::autoauctionCb and the auction's completion.
+// mode 0 (an auto-auction step, after the auction kernel ran on every swarm):
+//   a swarm flagged by its last completed auction (didConvergeOnInvalid-
+//   Assignment) flushes and skips this one (coordination_ros.cpp:339-345);
+//   otherwise the auction (re)starts -- a pending one is restarted, :355-358
+//   -- and completes after lat[b] steps (lat == NULL or 0: now).
+// mode 1 (every other step when auctions take time): a pending auction whose
+//   step has come completes.
+// Completion (auctioneer.cpp:250-295): an agreed valid result is adopted, an
+// agreed invalid one sets the flag, a disagreeing swarm keeps its assignment.
+__global__ void __launch_bounds__(64) adopt_kernel(int n, int step, int mode, const int32_t* lat,
+                                                   uint16_t* P, const uint16_t* Pnew,
                                                    const acl_swarm_status_t* st, uint8_t* flush,
                                                    acl_episode_status_t* est) {
   const int b = blockIdx.x, tid = threadIdx.x;
-  const bool fl = flush[b] != 0;
-  const uint32_t flags = st[b].flags;
-  const bool valid = (flags & ACL_SWARM_VALID) != 0, agree = (flags & ACL_SWARM_AGREE) != 0;
+  __shared__ int take;
   if (tid == 0) {
     acl_episode_status_t e = est[b];
-    if (fl) {
-      flush[b] = 0;
-      ++e.n_skipped;
-    } else {
-      ++e.n_auctions;
-      if (agree && !valid) {
-        flush[b] = 1;
-        ++e.n_invalid;
-      } else if (!agree) {
-        ++e.n_disagree;
+    bool complete = false;
+    if (mode == 0) {
+      if (flush[b] != 0) {
+        flush[b] = 0;
+        ++e.n_skipped;
+      } else {
+        ++e.n_auctions;
+        if (e.pending_step >= 0) ++e.n_restarted;
+        const int L = lat ? lat[b] : 0;
+        e.pending_step = L > 0 ? step + L : -1;
+        complete = L <= 0;
       }
+    } else if (e.pending_step >= 0 && e.pending_step <= step) {
+      e.pending_step = -1;
+      complete = true;
+    }
+    take = 0;
+    if (complete) {
+      const uint32_t flags = st[b].flags;
+      const bool valid = (flags & ACL_SWARM_VALID) != 0, agree = (flags & ACL_SWARM_AGREE) != 0;
+      if (agree && valid) take = 1;
+      else if (agree) { flush[b] = 1; ++e.n_invalid; }
+      else ++e.n_disagree;
     }
     est[b] = e;
   }
-  if (!fl && agree && valid)
+  __syncthreads();
+  if (take)
     for (int v = tid; v < n; v += 64) P[(size_t)b * n + v] = Pnew[(size_t)b * n + v];
 }
 
@@ -223,7 +281,7 @@ extern "C" void acl_default_episode_params(acl_episode_params_t* e) {
   e->auction_every = 120;
   e->sample_every = 2;
   e->bufflen = 50;
-  e->reserved = 0;
+  e->auction_latency = 0;
   e->max_accel_xy = 0.5;
   e->max_accel_z = 0.8;
   e->bounds_min[0] = -100.0; e->bounds_min[1] = -100.0; e->bounds_min[2] = 0.0;
@@ -281,16 +339,32 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
   // rebuilt on the first step of a call and after every auction (which also
   // overwrites it); the collision-avoidance count is zeroed by traj_kernel
   T.ca_count = reinterpret_cast<unsigned*>(ws + W.solve + ws_layout(n, B).cacount);
+  // auctions that take time: each swarm's latency in control steps
+  const bool timed = ep.auction_latency != 0;
+  int32_t* lat = reinterpret_cast<int32_t*>(ws + W.lat);
+  if (timed) {
+    hipLaunchKernelGGL(latency_kernel, dim3(B), dim3(64), 0, s, n, a->fidx, F->n_formations,
+                       F->adj, ep.auction_latency < 0 ? -1 : ep.auction_latency, ep.control_dt,
+                       lat);
+    if (hipGetLastError() != hipSuccess) return acl__set_error("latency_kernel launch failed");
+  }
   for (int k = 0; k < a->steps; ++k) {
     const int step = a->step0 + k;
     int flags = k == 0 ? (CTL_PREP | CTL_RESET) : 0;
     if (step % ep.auction_every == 0) {
       const acl_status_t r = acl_solve_batch(F, &sa, stream);
       if (r != ACL_OK) return r;
-      hipLaunchKernelGGL(adopt_kernel, dim3(B), dim3(64), 0, s, n, a->P, Pnew, st, a->flush,
-                         a->est);
+      hipLaunchKernelGGL(adopt_kernel, dim3(B), dim3(64), 0, s, n, step, 0,
+                         timed ? lat : nullptr, a->P, Pnew, st, a->flush, a->est);
       if (hipGetLastError() != hipSuccess) return acl__set_error("adopt_kernel launch failed");
       flags |= CTL_PREP | CTL_RESET;
+    } else if (timed) {
+      // a pending auction completing at this step changes P: rebuild the
+      // control hand-off
+      hipLaunchKernelGGL(adopt_kernel, dim3(B), dim3(64), 0, s, n, step, 1, lat, a->P, Pnew, st,
+                         a->flush, a->est);
+      if (hipGetLastError() != hipSuccess) return acl__set_error("adopt_kernel launch failed");
+      flags |= CTL_PREP;
     }
     const acl_status_t r = run_control(F, &cs, s, flags);
     if (r != ACL_OK) return r;

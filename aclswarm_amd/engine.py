@@ -337,6 +337,7 @@ class Episode:
         est = np.zeros(self.B, L.EPISODE_STATUS_DTYPE)
         est["converged_step"] = -1
         est["gridlock_step"] = -1
+        est["pending_step"] = -1
         self.est = torch.from_numpy(est.view(np.uint8).reshape(self.B, -1).copy()).to(dev)
         Lb = int(self.ep.bufflen)
         self.ring_u = torch.zeros((self.B, Lb, self.n), dtype=torch.float64, device=dev)

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define ACL_ABI_VERSION 4
+#define ACL_ABI_VERSION 5
 
 typedef enum {
   ACL_OK = 0,
@@ -445,7 +445,20 @@ typedef struct {
                               = 2 (supervisor.py:121) */
   int32_t bufflen;         /* BUFFER_SECONDS * tick_rate = 50 (supervisor.py:
                               47,126) */
-  int32_t reserved;
+  int32_t auction_latency; /* control steps from an auto-auction's start to the
+                              adoption of its result. 0: within its own step
+                              (instantaneous). > 0: that many steps. -1: the
+                              reference's timing per swarm: the auctioneer
+                              processes one bid per auctioneer_dt = 1 ms tick
+                              (coordination.launch:23, auctioneer.cpp:139-160)
+                              and a vehicle needs every neighbour's bid in each
+                              of the 2n rounds (auctioneer.cpp:198-241), so
+                              ceil(2 n d_max 1 ms / control_dt) steps, d_max
+                              the formation graph's largest degree. Control
+                              keeps the old assignment meanwhile; an auto-
+                              auction that finds one pending restarts it
+                              (coordination_ros.cpp:355-358: "Auctioneer is
+                              busy! Restarting."). */
   double max_accel_xy;     /* 0.5 (safety.cpp:45) */
   double max_accel_z;      /* 0.8 (safety.cpp:46) */
   double bounds_min[3];    /* room bounds: trial.sh:96 {-100, -100, 0} */
@@ -469,7 +482,12 @@ typedef struct {
                               the reference is not carried) */
   uint32_t n_samples;      /* supervisor ticks taken */
   uint32_t n_ca_steps;     /* vehicle-steps with collision avoidance active */
-} acl_episode_status_t; /* 32 bytes */
+  int32_t pending_step;    /* global step at which the pending auction's result
+                              is adopted, -1 if none (auction_latency != 0; its
+                              result stays in the workspace between calls) */
+  uint16_t n_restarted;    /* auctions restarted before they completed */
+  uint16_t reserved;
+} acl_episode_status_t; /* 40 bytes */
 
 typedef struct {
   int32_t B;

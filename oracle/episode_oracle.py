@@ -26,6 +26,8 @@ supervisor predicates are restated here from the reference text and are
 "parity unpinned" (no reference test or fixture covers them; the ROS nodes
 do not build here).
 """
+import math
+
 import numpy as np
 
 import pyoracle as O
@@ -35,7 +37,7 @@ def default_params():
     """acl_default_episode_params: coordination.launch:6,24-25,
     safety.cpp:45-46, trial.sh:96, supervisor.py:47,61-62,121."""
     return dict(control_dt=0.01, auction_every=120, sample_every=2, bufflen=50,
-                max_accel_xy=0.5, max_accel_z=0.8,
+                auction_latency=0, max_accel_xy=0.5, max_accel_z=0.8,
                 bounds_min=(-100.0, -100.0, 0.0), bounds_max=(100.0, 100.0, 30.0),
                 orig_zero_vel_thr=1.0, avg_active_ca_thr=0.95)
 
@@ -43,6 +45,7 @@ def default_params():
 def params_from_struct(e):
     return dict(control_dt=e.control_dt, auction_every=e.auction_every,
                 sample_every=e.sample_every, bufflen=e.bufflen,
+                auction_latency=e.auction_latency,
                 max_accel_xy=e.max_accel_xy, max_accel_z=e.max_accel_z,
                 bounds_min=tuple(e.bounds_min), bounds_max=tuple(e.bounds_max),
                 orig_zero_vel_thr=e.orig_zero_vel_thr, avg_active_ca_thr=e.avg_active_ca_thr)
@@ -144,22 +147,81 @@ def adopt(P, flush, res):
     return P, 0, "disagree"
 
 
+AUCTIONEER_DT = 0.001  # coordination.launch:23: one bid processed per tick
+
+
+def auction_latency_steps(n, adj, ep):
+    """Control steps from an auto-auction's start to its completion
+    (acl_episode_params_t::auction_latency): fixed, or the reference's timing
+    ceil(2 n d_max auctioneer_dt / control_dt) -- one bid per 1 ms tick
+    (auctioneer.cpp:139-160), every neighbour's bid in each of the 2n rounds
+    (auctioneer.cpp:198-241), d_max the formation graph's largest degree."""
+    L = int(ep.get("auction_latency", 0))
+    if L >= 0:
+        return L
+    a = np.asarray(adj) != 0
+    np.fill_diagonal(a, False)
+    dmax = int(a.sum(axis=1).max()) if n else 0
+    return int(math.ceil(2.0 * n * dmax * AUCTIONEER_DT / ep["control_dt"]))
+
+
+class Auctions:
+    """CoordinationROS::autoauctionCb and the auction's completion for one
+    swarm, with auctions that take `latency` control steps (0: complete in
+    their own step). An auto-auction that finds one pending restarts it
+    (coordination_ros.cpp:355-358); the flush rule (:339-345) skips one."""
+
+    def __init__(self, latency, flush=0):
+        self.latency = latency
+        self.flush = flush
+        self.pending = -1
+        self.res = None
+        self.counts = dict(skipped=0, auctions=0, adopted=0, invalid=0, disagree=0, restarted=0)
+
+    def auto(self, step, P, solve):
+        """An auto-auction step; solve() runs CBAA from the current state."""
+        if self.flush:
+            self.flush = 0
+            self.counts["skipped"] += 1
+            return P
+        self.counts["auctions"] += 1
+        if self.pending >= 0:
+            self.counts["restarted"] += 1
+        self.res = solve()
+        if self.latency <= 0:
+            self.pending = -1
+            return self._complete(P)
+        self.pending = step + self.latency
+        return P
+
+    def tick(self, step, P):
+        """Any other step: a pending auction whose step has come completes."""
+        if 0 <= self.pending <= step:
+            self.pending = -1
+            return self._complete(P)
+        return P
+
+    def _complete(self, P):
+        P2, self.flush, ev = adopt(P, 0, self.res)
+        self.counts[ev] += 1
+        return P2
+
+
 def run_episode(q, vel, P, p, adj, gains, steps, ep, step0=0, g=None, s=None):
     """The whole closed loop for one swarm on the CPU (small cases only)."""
     q = np.array(q, np.float64)
     vel = np.array(vel, np.float64)
     P = np.array(P, np.uint16)
-    flush = 0
     sup = Supervisor(q.shape[0], ep)
-    counts = dict(skipped=0, adopted=0, invalid=0, disagree=0)
+    auc = Auctions(auction_latency_steps(q.shape[0], adj, ep))
     conv_step = grid_step = -1
     qs = []
     for k in range(steps):
         step = step0 + k
         if step % ep["auction_every"] == 0:
-            res = O.solve(q, vel, p, adj, gains, P, g, s)
-            P, flush, ev = adopt(P, flush, res)
-            counts[ev] += 1
+            P = auc.auto(step, P, lambda: O.solve(q, vel, p, adj, gains, P, g, s))
+        else:
+            P = auc.tick(step, P)
         u, us, ca = control_step(q, vel, p, adj, gains, P, g, s)
         q, vel = make_safe_traj(q, vel, us, ep)
         if step % ep["sample_every"] == 0:
@@ -170,5 +232,5 @@ def run_episode(q, vel, P, p, adj, gains, steps, ep, step0=0, g=None, s=None):
                 if r[1] and grid_step < 0:
                     grid_step = step
         qs.append(q.copy())
-    return dict(q=q, vel=vel, P=P, flush=flush, counts=counts, converged_step=conv_step,
+    return dict(q=q, vel=vel, P=P, flush=auc.flush, counts=auc.counts, converged_step=conv_step,
                 gridlock_step=grid_step, q_hist=np.array(qs))

@@ -17,7 +17,7 @@ from aclswarm_amd import engine, workload  # noqa: E402
 NAMES = ["load+nbhd", "align", "prices", "cbaa", "adopt", "handoff"]
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--B", type=int, default=8192)
+ap.add_argument("--B", type=int, default=65536)
 ap.add_argument("--n", type=int, default=100)
 ap.add_argument("--formations", type=int, default=0)
 args = ap.parse_args()
@@ -42,6 +42,14 @@ tot = d.sum(1)
 print(f"per-swarm cycles: mean {tot.mean():.0f}  median {np.median(tot):.0f}")
 for k, nm in enumerate(NAMES):
     print(f"  {nm:16s} mean {d[:, k].mean():10.0f}  share {d[:, k].sum() / tot.sum() * 100:5.1f}%")
+# fused control phase (stamp 7, non-PROF builds): its cycles, and how the
+# swarms' phases overlap on the chip (busy workgroups over the kernel span)
+g = s[:, 7] - s[:, 6]
+if (s[:, 7] > 0).all():
+    print(f"  control (fused)  mean {g.mean():10.0f}  share of swarm life "
+          f"{g.sum() / (g.sum() + tot.sum()) * 100:5.1f}%")
+    span = s[:, 7].max() - s[:, 0].min()
+    print(f"  span {span:.0f} cycles; mean resident swarms {(s[:, 7] - s[:, 0]).sum() / span:.1f}")
 # CBAA column-step sections (a -DACL_AUCTION_PROF=1 build): cycles summed
 # over a swarm's waves, and the counts of evaluated columns, walks and scans
 sec = st.cpu().numpy()[:, 7:16].astype(np.uint64)

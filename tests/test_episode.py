@@ -143,8 +143,9 @@ int main(void) {
   printf("params %zu status %zu args %zu\n", sizeof(acl_episode_params_t),
          sizeof(acl_episode_status_t), sizeof(acl_episode_args_t));
   P(acl_episode_params_t, max_accel_xy) P(acl_episode_params_t, bounds_max)
-  P(acl_episode_params_t, avg_active_ca_thr)
+  P(acl_episode_params_t, avg_active_ca_thr) P(acl_episode_params_t, auction_latency)
   P(acl_episode_status_t, n_auctions) P(acl_episode_status_t, n_ca_steps)
+  P(acl_episode_status_t, pending_step) P(acl_episode_status_t, n_restarted)
   P(acl_episode_args_t, step0) P(acl_episode_args_t, vel_hist) P(acl_episode_args_t, workspace)
   P(acl_episode_args_t, cntrl) P(acl_episode_args_t, safety) P(acl_episode_args_t, ep)
   return 0;
@@ -215,3 +216,30 @@ def test_formation_generator_argument_errors_without_gpu():
     assert lib.acl_generate_formation_groups(4, 600, z, 1, 1.0, 1.0, 1.0, 2.0, 0, z, z, z, z, z) != 0
     assert lib.acl_generate_formation_groups(0, 20, z, 1, 1.0, 1.0, 1.0, 2.0, 0, z, z, z, z, z) == 0
     assert lib.acl_generate_formation_groups(2, 20, z, 1, 1.0, 1.0, 1.0, 2.0, 0, z, z, z, z, z) != 0
+
+
+def test_auction_latency_model():
+    """acl_episode_params_t::auction_latency on the CPU: the reference timing
+    ceil(2 n d_max 1 ms / control_dt), and the autoauctionCb state machine --
+    an auction completes after its latency, one still pending at the next
+    auto-auction is restarted (coordination_ros.cpp:355-358)."""
+    pts, adj, gains, q0 = H.swarm6()
+    ep = dict(E.default_params(), auction_latency=-1)
+    n = 6
+    for A in adj:
+        d = int(((np.asarray(A) != 0) & ~np.eye(n, dtype=bool)).sum(axis=1).max())
+        assert E.auction_latency_steps(n, A, ep) == math.ceil(2.0 * n * d * 0.001 / 0.01)
+    a = np.ones((100, 100), np.uint8) - np.eye(100, dtype=np.uint8)
+    a[0, 1:51] = a[1:51, 0] = 0
+    assert E.auction_latency_steps(100, a, ep) == 1980  # 2 * 100 * 99 ms / 10 ms
+    assert E.auction_latency_steps(n, adj[0], dict(ep, auction_latency=7)) == 7
+    # latency longer than the auto-auction period: every auction restarts
+    ep2 = dict(E.default_params(), auction_every=10, auction_latency=25)
+    P0 = np.array([1, 0, 2, 3, 5, 4])
+    r = E.run_episode(q0, np.zeros((n, 3)), P0, pts[0], adj[0], gains[0], 60, ep2)
+    assert r["counts"]["auctions"] == 6 and r["counts"]["restarted"] == 5
+    assert r["counts"]["adopted"] == 0 and (r["P"] == P0).all()
+    # shorter: every auction completes `latency` steps after it started
+    ep3 = dict(ep2, auction_latency=4)
+    r = E.run_episode(q0, np.zeros((n, 3)), P0, pts[0], adj[0], gains[0], 60, ep3)
+    assert r["counts"]["restarted"] == 0 and r["counts"]["adopted"] == 6

@@ -156,3 +156,47 @@ def test_episode_chunks_equal_one_call(cuda):
     torch.cuda.synchronize()
     for k in ("q", "vel", "P", "flush", "est", "ring_u", "ring_ca"):
         assert torch.equal(getattr(e1, k), getattr(e2, k)), k
+
+
+@pytest.mark.parametrize("lat", [-1, 3, 25])
+def test_episode_auction_latency(cuda, lat):
+    """Auctions that take time (acl_episode_params_t::auction_latency): the
+    reference timing (-1: ceil(2 n d_max 1 ms / control_dt), 4-6 steps for
+    the swarm6 formations), a fixed 3 steps, and 25 steps > the auto-auction period of 10
+    (every auction restarted, coordination_ros.cpp:355-358). Teacher-forced:
+    the CPU state machine (episode_oracle.Auctions) runs CBAA from the GPU's
+    own state at each auto-auction and must give the assignment the GPU's
+    controller used at every step, and the same counters."""
+    import torch
+    case = dict(_cases()[0], ep=dict(auction_every=10, auction_latency=lat), steps=64)
+    e, eps = _episode(case, cuda)
+    hist = e.run(40, history=True)
+    hist2 = e.run(24, history=True)  # a pending auction crosses the call boundary
+    torch.cuda.synchronize()
+    h = {k: np.concatenate([v.cpu().numpy(), hist2[k].cpu().numpy()]) for k, v in hist.items()}
+    h["P"] = h["P"].view(np.uint16)
+    est = e.status()
+    ep = E.params_from_struct(eps)
+    B, n = case["q"].shape[:2]
+    for b in range(B):
+        f = case["fidx"][b]
+        p, adj, G = case["pts"][f], case["adj"][f], case["gains"][f]
+        auc = E.Auctions(E.auction_latency_steps(n, adj, ep))
+        P = case["P"][b].astype(np.uint16)
+        qprev, vprev = case["q"][b], case["vel"][b]
+        for k in range(case["steps"]):
+            if k % ep["auction_every"] == 0:
+                P = auc.auto(k, P, lambda: O.solve(qprev, vprev, p, adj, G, P))
+            else:
+                P = auc.tick(k, P)
+            assert (h["P"][k, b] == P).all(), (lat, b, k)
+            qprev, vprev = h["q"][k, b], h["vel"][k, b]
+        st, c = est[b], auc.counts
+        assert (st["n_auctions"], st["n_restarted"], st["n_skipped"]) == \
+            (c["auctions"], c["restarted"], c["skipped"]), (st, c)
+        assert (st["n_invalid"], st["n_disagree"]) == (c["invalid"], c["disagree"])
+        assert st["pending_step"] == auc.pending
+        if lat == 25:
+            assert c["adopted"] == 0 and c["restarted"] == c["auctions"] - 1
+        else:
+            assert c["adopted"] > 0
