@@ -59,7 +59,7 @@ struct GainLayout {
   int q, p, pn, adjF, rowpre, Pt, myi, out, red, atab, total;
 };
 
-__host__ __device__ inline GainLayout make_gain_layout(int n) {
+__host__ __device__ inline GainLayout make_gain_layout(int n, int waves = kCtlWaves) {
   const int NW = (n + 63) >> 6;
   GainLayout L;
   int o = 0;
@@ -71,19 +71,20 @@ __host__ __device__ inline GainLayout make_gain_layout(int n) {
   L.Pt = o;     o = cal16(o + n * 2);
   L.myi = o;    o = cal16(o + n * 2);
   L.out = o;    o = cal16(o + n * 3 * 8);       // u (DistCntrl)
-  L.red = o;    o = cal16(o + kCtlWaves * 64 * 3 * 8);  // per-lane partial sums
+  L.red = o;    o = cal16(o + waves * 64 * 3 * 8);  // per-lane partial sums
   L.atab = o;   o = cal16(o + ACL_ATAB_N * 8);  // atan range-reduction table
   L.total = o;
   return L;
 }
 
 // GM: the caller asked for the gate margin (acl_solve_args_t::gate_margin)
-template <int NP, bool GM>
-__global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_kernel(const CtlParams P) {
+template <int NP, bool GM, int kB>
+__global__ void __launch_bounds__(kB, kB == 256 ? (NP == 5 ? ACL_GAIN_WAVES : 4) : 1) gain_kernel(const CtlParams P) {
+  constexpr int kW = kB / 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const int NW = (n + 63) >> 6;
-  const GainLayout L = make_gain_layout(n);
+  const GainLayout L = make_gain_layout(n, kW);
   const int b = P.b0 + blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -118,22 +119,22 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
   {
     const double* gq = P.q + (size_t)b * n * 3;
     const double* gp = P.p + (size_t)f * n * 3;
-    for (int k = tid; k < 3 * n; k += kCtlBlock) {
+    for (int k = tid; k < 3 * n; k += kB) {
       q[k] = gq[k];
       p[k] = gp[k];
     }
-    for (int j = tid; j < n; j += kCtlBlock) {
+    for (int j = tid; j < n; j += kB) {
       const double x = gp[3 * j], y = gp[3 * j + 1], z = gp[3 * j + 2];
       pn[2 * j] = x * x + y * y;
       pn[2 * j + 1] = z * z;
     }
     const uint64_t* ga = P.adj + (size_t)f * n * NW;
-    for (int k = tid; k < n * NW; k += kCtlBlock) {
+    for (int k = tid; k < n * NW; k += kB) {
       unsigned long long x = ga[k];
       if (k % NW == NW - 1) x &= lastmask;
       adjF[k] = x;
     }
-    for (int v = tid; v < n; v += kCtlBlock) {
+    for (int v = tid; v < n; v += kB) {
       myi[v] = P.P_out[(size_t)b * n + v];
       if (uniform) Pt[v] = P.wsPt[(size_t)b * n + v];
     }
@@ -175,7 +176,7 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
   // assignment (vehicle v = Pt[i] of row i): consecutive rows are consecutive
   // edge ranges, so the gain stream is read nearly sequentially.
   // Otherwise groups walk vehicles, each with its own adopted point.
-  for (int grp = wave; grp < ngroups; grp += kCtlWaves) {
+  for (int grp = wave; grp < ngroups; grp += kW) {
     const int r = grp * GV + seg;
     const bool act = seg < GV && r < n;
     const int rr = act ? r : 0;
@@ -310,7 +311,7 @@ __global__ void __launch_bounds__(kCtlBlock, NP == 5 ? ACL_GAIN_WAVES : 4) gain_
   if (GM) gate_margin_reduce(&gmw, gate_margin_of(g, gmxy, gmz));
   __syncthreads();
   if (GM && tid == 0) P.gate_margin[b] = __longlong_as_double((long long)gmw);
-  gain_epilogue(P, b, n, q, uo, tid);
+  gain_epilogue(P, b, n, q, uo, tid, kB);
 }
 
 
@@ -739,12 +740,17 @@ hipError_t launch_control_prep(const CtlParams& P, const uint16_t* Pgiven, int n
 #ifndef ACL_GAIN_PAIR
 #define ACL_GAIN_PAIR 1
 #endif
+// n > 128: every swarm in the directed walk on 1024-thread workgroups
+// (ACL_WIDE_DIRECTED=0, diagnostic builds: the 256-thread pair kernel)
+#ifndef ACL_WIDE_DIRECTED
+#define ACL_WIDE_DIRECTED 1
+#endif
 
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream) {
   if (which == 0 || which == 2) {
     CtlParams Q = P;
     Q.only_nonuniform = which == 2 ? 1 : 0;
-    if (which == 0 && P.gain_planes == 5 && ACL_GAIN_PAIR) {
+    if (which == 0 && P.gain_planes == 5 && ACL_GAIN_PAIR && (P.n <= kMaxN || !ACL_WIDE_DIRECTED)) {
       // uniform swarms: one evaluation per undirected edge; then gain_kernel
       // for the swarms whose vehicles hold different assignments
       const bool tiled = P.gains_tiled != nullptr && P.n <= kMaxN;
@@ -765,14 +771,25 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
       if (P.all_uniform) return hipGetLastError();
       Q.only_nonuniform = 1;
     }
-    const GainLayout L = make_gain_layout(P.n);
+    // n > 128: 16 waves per swarm (the directed walk keeps per-lane sums;
+    // the pair kernel's per-wave accumulators would not fit the LDS)
+    const bool big = P.n > kMaxN;
+    const GainLayout L = make_gain_layout(P.n, big ? 16 : kCtlWaves);
     const bool gm = P.gate_margin != nullptr;
 #define ACL_GAIN(NP_, G_)                                                                    \
   do {                                                                                       \
-    if (L.total > 64 * 1024)                                                                 \
-      (void)hipFuncSetAttribute((const void*)gain_kernel<NP_, G_>,                           \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, L.total);        \
-    hipLaunchKernelGGL((gain_kernel<NP_, G_>), dim3(nb), dim3(kCtlBlock), L.total, stream, Q); \
+    if (big) {                                                                               \
+      if (L.total > 64 * 1024)                                                               \
+        (void)hipFuncSetAttribute((const void*)gain_kernel<NP_, G_, 1024>,                   \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, L.total);      \
+      hipLaunchKernelGGL((gain_kernel<NP_, G_, 1024>), dim3(nb), dim3(1024), L.total, stream, Q); \
+    } else {                                                                                 \
+      if (L.total > 64 * 1024)                                                               \
+        (void)hipFuncSetAttribute((const void*)gain_kernel<NP_, G_, kCtlBlock>,              \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, L.total);      \
+      hipLaunchKernelGGL((gain_kernel<NP_, G_, kCtlBlock>), dim3(nb), dim3(kCtlBlock), L.total, \
+                         stream, Q);                                                         \
+    }                                                                                        \
   } while (0)
     if (P.gain_planes == 5 && gm) ACL_GAIN(5, true);
     else if (P.gain_planes == 5) ACL_GAIN(5, false);
