@@ -53,7 +53,7 @@ __host__ __device__ inline WLayout make_wlayout(int n) {
     o = wal(o + (a > t ? a : t));
   }
   L.adjF = o;  o = wal(o + n * NW * 8);
-  L.vadj = o;  o = wal(o + n * NW * 8);
+  L.vadj = o;  o = wal(o + n * NW * 8);  // [word][vehicle]: conflict-free per-lane reads
   L.Pin = o;   o = wal(o + n * 2);
   L.Ptin = o;  o = wal(o + n * 2);
   L.valid = o; o = wal(o + n);
@@ -118,6 +118,11 @@ __device__ int wide_select(int n, int NW, int v, int lane, const float* C, const
   return js;
 }
 
+// diagnostic: s_memtime at phase ends into P.stamps[b][k] (scripts/phase_profile.py)
+__device__ __forceinline__ void wstamp(const SolveParams& P, int b, int k) {
+  if (P.stamps && threadIdx.x == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
+}
+
 __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
@@ -157,6 +162,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   MarginPair mp;
   margin_init(mp);
   double galign = 1.0;
+  wstamp(P, b, 0);
 
   // ---------------- phase 0: load -----------------------------------------
   {
@@ -232,10 +238,11 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         e = (u == v) || ((adjF[i * NW + (pu >> 6)] >> (pu & 63)) & 1ull);
       }
       const unsigned long long m = __ballot(e);
-      if (lane == 0) vadj[v * NW + c] = m;
+      if (lane == 0) vadj[c * n + v] = m;  // word-major: lanes over vehicles read consecutive words
     }
   }
   __syncthreads();
+  wstamp(P, b, 1);
 
   // ---------------- phase 1: alignment (see solve.hip) --------------------
   for (int t = tid; t < 4 * n; t += kWBlock) {
@@ -330,6 +337,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
   }
   __syncthreads();
+  wstamp(P, b, 2);
   if (P.align_Rt)
     for (int k = tid; k < 6 * n; k += kWBlock) P.align_Rt[(size_t)b * n * 6 + k] = out[k];
 
@@ -369,6 +377,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   for (int k = tid; k < n * n; k += kWBlock) T[k] = (uint16_t)n;  // reset: all `none`
   __syncthreads();
   const bool nonfinite = misc[M_NONFIN] != 0;
+  wstamp(P, b, 3);
 
   // ---------------- phase 3: CBAA ------------------------------------------
   for (int v = wave; v < n; v += kWWaves) {
@@ -443,7 +452,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
               bool hit = false;
 #pragma unroll
               for (int w2 = 0; w2 < kWMaxW; ++w2)
-                if (h[w2]) hit |= (vadj[u * NW + w2] & h[w2]) != 0ull;
+                if (h[w2]) hit |= (vadj[w2 * n + u] & h[w2]) != 0ull;
               if (hit) {
                 if (st[c] == 0) {
                   nw[c] = (unsigned)wk;
@@ -482,7 +491,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
               unsigned bw = (unsigned)n;
               bool first = true, have2 = false;
               for (int w2 = 0; w2 < NW; ++w2) {
-                unsigned long long mm = vadj[u * NW + w2];
+                unsigned long long mm = vadj[w2 * n + u];
                 while (mm) {
                   const int uu = 64 * w2 + __ffsll((long long)mm) - 1;
                   mm &= mm - 1;
@@ -565,6 +574,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     if (!next && P.early_exit) break;
   }
 
+  wstamp(P, b, 4);
   // swarm margin: min over every thread's CBAA pair and alignment gaps
   {
     const double gc = margin_gap(mp);
@@ -618,6 +628,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     }
   }
   __syncthreads();
+  wstamp(P, b, 5);
   {
     const bool allvalid = misc[M_NINV] == 0;
     const bool uniform = (allvalid && misc[M_AGREE]) || misc[M_NINV] == n;
@@ -650,6 +661,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     st.margin = (float)g;
     P.status[b] = st;
   }
+  wstamp(P, b, 6);
 }
 
 hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream) {

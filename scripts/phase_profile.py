@@ -20,11 +20,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--B", type=int, default=65536)
 ap.add_argument("--n", type=int, default=100)
 ap.add_argument("--formations", type=int, default=0)
+ap.add_argument("--L", type=float, default=None)
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 gen = torch.Generator(device=dev)
 gen.manual_seed(1)
-w = workload.simform_workload(args.B, args.n, gen, dev, F=(args.formations or None))
+w = workload.simform_workload(args.B, args.n, gen, dev, F=(args.formations or None), L=args.L)
+if args.n > 128:
+    NAMES[:] = ["load+nbhd", "align", "prices", "cbaa", "adopt", "handoff"]
 T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"],
                               w["planes"])
 lib = L.lib()
