@@ -583,7 +583,47 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   }
 
   // ---------------- phase 4: adoption --------------------------------------
-  for (int v = wave; v < n; v += kWWaves) {
+  // Do all vehicles hold vehicle 0's table? T is column-major, so compare
+  // each column with its row-0 entry (coalesced). Then one table decides
+  // every vehicle's validity (isValidAssignment of row 0, as auction.hip).
+  {
+    bool diff = false;
+    for (int j = wave; j < n; j += kWWaves) {
+      const uint16_t* Tc = T + (size_t)j * n;
+      const uint16_t t0 = Tc[0];
+      for (int u = lane; u < n; u += 64) diff |= Tc[u] != t0;
+    }
+    if (__any(diff) && lane == 0) misc[M_AGREE] = 0;
+  }
+  __syncthreads();
+  const bool allagree = misc[M_AGREE] != 0;
+  if (allagree) {
+    // row 0 = column entries T[j][0]: a permutation <=> every entry < n and
+    // each vehicle holds exactly one task
+    unsigned long long* sw = seen;  // [NW] words
+    if (tid < NW) sw[tid] = 0ull;
+    __syncthreads();
+    for (int j = tid; j < n; j += kWBlock) {
+      const int w = T[(size_t)j * n];
+      if (w >= n) misc[M_NINV] = n;
+      else atomicOr(&sw[w >> 6], 1ull << (w & 63));
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int cnt = 0;
+      for (int w = 0; w < NW; ++w) cnt += __popcll(sw[w]);
+      if (cnt != n) misc[M_NINV] = n;
+    }
+    __syncthreads();
+    const bool valid0 = misc[M_NINV] == 0;
+    for (int j = tid; j < n; j += kWBlock) {
+      const int v = valid0 ? T[(size_t)j * n] : Ptin[j];
+      validv[v] = valid0;
+      if (j != Pin[v]) misc[M_CHANGED] = 1;
+      P.P_out[(size_t)b * n + v] = (uint16_t)j;
+    }
+  }
+  for (int v = wave; !allagree && v < n; v += kWWaves) {
     unsigned long long* sw = seen + wave * NW;
     if (lane < NW) sw[lane] = 0ull;
     __builtin_amdgcn_wave_barrier();
