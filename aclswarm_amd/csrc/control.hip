@@ -18,11 +18,15 @@
 //                  and the first test of Safety::collisionAvoidance
 //                  (safety.cpp:412-541): a vehicle with no other vehicle
 //                  inside d_avoid_thresh keeps its saturated command; the
-//                  others are appended to a list.
-//   ca_kernel      the rest of collisionAvoidance for the listed vehicles:
-//                  lanes build the sector edges of the close vehicles, lane 0
-//                  sorts them (std::sort on (angle, sign)), unions them and
-//                  picks the closest safe edge exactly as the reference.
+//                  others are marked in the swarm's mask words and the swarm
+//                  is appended (once) to a list.
+//   ca_kernel      the rest of collisionAvoidance for the listed swarms, one
+//                  workgroup per swarm: a wave per close vehicle builds the
+//                  sector edges (lanes over the other vehicles), sorts them
+//                  (std::sort on (angle, sign): a bitonic network over lanes,
+//                  or a rank sort for more than 16 close vehicles), unions
+//                  them by a prefix count and picks the closest safe edge
+//                  exactly as the reference.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -112,6 +116,8 @@ __global__ void __launch_bounds__(kB, kB == 256 ? (NP == 5 ? ACL_GAIN_WAVES : 4)
   // wave's atomicMin after the edge loop follows it
   __shared__ unsigned long long gmw;
   if (GM && tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
+  __shared__ unsigned caw;  // the swarm is on the collision list (gain_epilogue)
+  if (tid == 0) caw = 0u;
   const int f = P.fidx[b];
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
   const bool uniform = P.wsMode[b] == 0;
@@ -311,7 +317,7 @@ __global__ void __launch_bounds__(kB, kB == 256 ? (NP == 5 ? ACL_GAIN_WAVES : 4)
   if (GM) gate_margin_reduce(&gmw, gate_margin_of(g, gmxy, gmz));
   __syncthreads();
   if (GM && tid == 0) P.gate_margin[b] = __longlong_as_double((long long)gmw);
-  gain_epilogue(P, b, n, q, uo, tid, kB);
+  gain_epilogue(P, b, n, q, uo, &caw, tid, kB);
 }
 
 
@@ -417,22 +423,49 @@ hipError_t launch_tile_gains(int n, int F, const uint64_t* adj, const double* ga
   return hipGetLastError();
 }
 
-// collisionAvoidance (safety.cpp:412-541) for the vehicles gain_kernel
-// listed; one wave per listed vehicle, the swarm's q in the wave's LDS.
+// collisionAvoidance (safety.cpp:412-541) for the swarms gain_epilogue
+// listed: one workgroup per listed swarm, the swarm's q loaded once into LDS,
+// its kCaWaves waves taking the swarm's close vehicles (mask bits) in turn;
+// each vehicle's sector edges in wave-private LDS.
 constexpr int kCaWaves = 4;
 
-__host__ __device__ inline int ca_wave_bytes(int n) {
-  return cal16(n * 3 * 8) + cal16(4 * n * 8) + cal16(4 * n);
+// LDS of ca_kernel: q [n][3] f64 shared, then per wave the sector edges of
+// one vehicle (caA/caS: up to 4 per other vehicle, sign 0 = unused slot) and
+// the sorted copy of the general path (tA/tS), then the swarm's count of
+// modified commands.
+struct CaLayout {
+  int a, t, s, ts, wbytes, wave, nca, total;
+};
+__host__ __device__ inline CaLayout ca_layout(int n) {
+  CaLayout L;
+  L.a = 0;
+  L.t = cal16(4 * n * 8);
+  L.s = 2 * L.t;
+  L.ts = L.s + cal16(4 * n);
+  L.wbytes = L.ts + cal16(4 * n);
+  L.wave = cal16(n * 3 * 8);
+  L.nca = L.wave + kCaWaves * L.wbytes;
+  L.total = L.nca + 16;
+  return L;
+}
+
+// sort key of a sector edge: the angle's total order (-0.0 as +0.0, so equal
+// angles tie as in the double comparison), unused slots last
+__device__ __forceinline__ unsigned long long ca_key(double x, int sgn) {
+  if (sgn == 0) return ~0ull;
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x + 0.0);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
 
 // Wave-parallel tail of collisionAvoidance for one vehicle whose sector
-// edges fit one wave (lane k < nslot holds slot k of caA / caS; sign 0 =
-// unused). Same results as the serial lane-0 path below: the edges sorted as
-// std::sort on (angle, sign) pairs (bitonic network on lanes; the order of a
-// sequence of keys is unique), the parenthesis-count union as a prefix sum of
-// the signs, a zone's start the edge after the previous zone's end, the
-// closest zone edge by lower_bound over the sorted, flattened zone edges.
+// edges fit K <= 64 lanes (lane k < nslot holds slot k of caA / caS). Same
+// results as the serial restatement (ca_resolve_serial): the edges sorted as
+// std::sort on (angle, sign) pairs (bitonic network over K lanes; the order
+// of a sequence of keys is unique), the parenthesis-count union as a prefix
+// sum of the signs, a zone's start the edge after the previous zone's end,
+// the closest zone edge by lower_bound over the sorted, flattened zone edges.
 // Returns true when psi lies strictly inside a zone (cmd is then updated).
+template <int K>
 __device__ __forceinline__ bool ca_resolve_wave(int lane, int nslot, const double* caA,
                                                 const signed char* caS, bool didWrap,
                                                 double& cmd0, double& cmd1, double& cmd2) {
@@ -442,20 +475,14 @@ __device__ __forceinline__ bool ca_resolve_wave(int lane, int nslot, const doubl
     a = caA[lane];
     sg = caS[lane];
   }
-  // sort key: the angle's total order (-0.0 as +0.0, so equal angles tie as
-  // in the double comparison), unused slots last
-  auto keyof = [](double x, int sgn) -> unsigned long long {
-    if (sgn == 0) return ~0ull;
-    const unsigned long long u = (unsigned long long)__double_as_longlong(x + 0.0);
-    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
-  };
+  // lanes >= K hold unused slots only; their K-blocks sort among themselves
 #pragma unroll
-  for (int k = 2; k <= 64; k <<= 1) {
+  for (int k = 2; k <= K; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
       const double pa = __shfl_xor(a, j, 64);
       const int ps = __shfl_xor(sg, j, 64);
-      const unsigned long long mk = keyof(a, sg), pk = keyof(pa, ps);
+      const unsigned long long mk = ca_key(a, sg), pk = ca_key(pa, ps);
       const bool pless = pk < mk || (pk == mk && ps < sg);
       const bool mless = mk < pk || (mk == pk && sg < ps);
       const bool take_min = ((lane & k) == 0) == ((lane & j) == 0);
@@ -465,15 +492,15 @@ __device__ __forceinline__ bool ca_resolve_wave(int lane, int nslot, const doubl
       }
     }
   }
-  // union: inclusive prefix count of the signs
+  // union: inclusive prefix count of the signs (exact on lanes < K)
   int incl = sg;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
+  for (int o = 1; o < K; o <<= 1) {
     const int y = __shfl_up(incl, o, 64);
     if (lane >= o) incl += y;
   }
   const int excl = incl - sg;
-  const bool isEnd = sg != 0 && incl == 0;
+  const bool isEnd = lane < K && sg != 0 && incl == 0;
   const unsigned long long endMask = __ballot(isEnd);
   if (!endMask) return false;
   // zone of an end lane e: from the lane after the previous end (or lane 0)
@@ -486,7 +513,7 @@ __device__ __forceinline__ bool ca_resolve_wave(int lane, int nslot, const doubl
   // zone edges in order: every closed zone's start and end; +-pi dropped
   // when some sector wrapped
   const int lastEnd = 63 - __clzll(endMask);
-  const bool isStart = sg != 0 && excl == 0 && lane < lastEnd;
+  const bool isStart = lane < K && sg != 0 && excl == 0 && lane < lastEnd;
   const bool keep = (isStart || isEnd) && !(didWrap && fabs(a) == kPi);
   const unsigned long long km = __ballot(keep);
   const int m = __popcll(km);
@@ -520,170 +547,332 @@ __device__ __forceinline__ bool ca_resolve_wave(int lane, int nslot, const doubl
   return true;
 }
 
-#ifndef ACL_CA_WAVES_PER_SIMD
-#define ACL_CA_WAVES_PER_SIMD 1
-#endif
+// The same for any number of sector edges (more than 16 close vehicles):
+// a rank sort of the used slots into tA / tS (rank = the number of edges
+// before it in (angle, sign, slot) order -- stable, as the insertion sort of
+// the serial restatement), then one pass over the sorted edges in chunks of
+// 64 lanes carrying the sign count, the previous zone end and the counts of
+// the flattened zone edges; the kept-edge masks per chunk (in caA, free once
+// sorted) locate the lower_bound neighbours.
+__device__ __forceinline__ bool ca_resolve_general(int lane, int nslot, double* caA,
+                                                const signed char* caS, double* tA,
+                                                signed char* tS, bool didWrap, double& cmd0,
+                                                double& cmd1, double& cmd2) {
+  int m = 0;
+  for (int e0 = 0; e0 < nslot; e0 += 64)
+    m += __popcll(__ballot(e0 + lane < nslot && caS[e0 + lane] != 0));
+  for (int e = lane; e < nslot; e += 64) {
+    const int s = caS[e];
+    if (s == 0) continue;
+    const double a = caA[e];
+    const unsigned long long k = ca_key(a, s);
+    int r = 0;
+    for (int e2 = 0; e2 < nslot; ++e2) {
+      const int s2 = caS[e2];
+      const unsigned long long k2 = ca_key(caA[e2], s2);  // unused: ~0, never before
+      r += (k2 < k) || (k2 == k && s2 != 0 && (s2 < s || (s2 == s && e2 < e)));
+    }
+    tA[r] = a;
+    tS[r] = (signed char)s;
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  const double psi = atan2(cmd1, cmd0);
+  unsigned long long* keepm = reinterpret_cast<unsigned long long*>(caA);
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int carry = 0, prevEnd = -1, m2 = 0, it = 0;
+  bool inside = false;
+  const int C = (m + 63) >> 6;
+  for (int c = 0; c < C; ++c) {
+    const int k = 64 * c + lane;
+    const bool valid = k < m;
+    const double a = valid ? tA[k] : 0.0;
+    const int sg = valid ? (int)tS[k] : 0;
+    int incl = sg;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    incl += carry;
+    // every sector adds +1 and -1, so the count ends at 0 and no start
+    // follows the last end (the serial path's unclosed zone cannot occur)
+    const bool isEnd = sg != 0 && incl == 0;
+    const bool isStart = sg != 0 && incl - sg == 0;
+    const unsigned long long em = __ballot(isEnd);
+    const unsigned long long below = em & lt;
+    const int pe = below ? 64 * c + 63 - __clzll(below) : prevEnd;
+    if (isEnd) inside |= psi > tA[pe + 1] && psi < a;
+    const bool keep = (isStart || isEnd) && !(didWrap && fabs(a) == kPi);
+    const unsigned long long km = __ballot(keep);
+    if (lane == 0) keepm[c] = km;
+    m2 += __popcll(km);
+    it += __popcll(__ballot(keep && a < psi));
+    carry = __shfl(incl, 63, 64);
+    if (em) prevEnd = 64 * c + 63 - __clzll(em);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  if (!__any(inside)) return false;
+  if (m2 == 0) {
+    cmd0 = cmd1 = 0.0;
+    cmd2 = 0.0;
+    return true;
+  }
+  auto nth = [&](int r) -> int {  // sorted index of the r-th kept edge
+    int c = 0;
+    unsigned long long x = keepm[0];
+    while (r >= __popcll(x)) {
+      r -= __popcll(x);
+      x = keepm[++c];
+    }
+    for (int t = 0; t < r; ++t) x &= x - 1ull;
+    return 64 * c + __ffsll((long long)x) - 1;
+  };
+  int idx;
+  if (it == 0) idx = 0;
+  else if (it == m2) idx = it - 1;
+  else idx = fabs(tA[nth(it - 1)] - psi) < fabs(tA[nth(it)] - psi) ? it - 1 : it;
+  const double edge = tA[nth(idx)];
+  if (fabs(wrap_to_pi(edge - psi)) <= kPi / 2) {
+    const double umag = sqrt(cmd0 * cmd0 + cmd1 * cmd1);
+    cmd0 = umag * cos(edge);
+    cmd1 = umag * sin(edge);
+  } else {
+    cmd0 = cmd1 = 0.0;
+    cmd2 = 0.0;
+  }
+  return true;
+}
+
+// Serial restatement (lane 0) for sector edges with a NaN angle, whose
+// std::sort order the comparison networks above do not reproduce: insertion
+// sort on (angle, sign), parenthesis-count union, closest zone edge.
+__device__ __forceinline__ bool ca_resolve_serial(int nslot, double* caA, signed char* caS,
+                                               bool didWrap, double& cmd0, double& cmd1,
+                                               double& cmd2) {
+  int ne = 0;
+  for (int k = 0; k < nslot; ++k) {
+    const signed char sg = caS[k];
+    if (sg == 0) continue;
+    const double a = caA[k];
+    int pos = ne;
+    while (pos > 0 && (a < caA[pos - 1] || (!(caA[pos - 1] < a) && sg < caS[pos - 1]))) {
+      caA[pos] = caA[pos - 1];
+      caS[pos] = caS[pos - 1];
+      --pos;
+    }
+    caA[pos] = a;
+    caS[pos] = sg;
+    ++ne;
+  }
+  // parenthesis-count union into zones, stored in place (nz <= ne/2)
+  int nz = 0, count = 0;
+  double start = 0.0;
+  for (int k = 0; k < ne; ++k) {
+    const double a = caA[k];
+    if (count == 0) start = a;
+    count += caS[k];
+    if (count == 0) {
+      caA[2 * nz] = start;
+      caA[2 * nz + 1] = a;
+      ++nz;
+    }
+  }
+  const double psi = atan2(cmd1, cmd0);
+  bool safe = true;
+  for (int k = 0; k < nz; ++k)
+    if (psi > caA[2 * k] && psi < caA[2 * k + 1]) { safe = false; break; }
+  if (safe) return false;
+  // flatten zone edges (drop +-pi ones when wrapped), sort
+  int m = 0;
+  for (int k = 0; k < 2 * nz; ++k) {
+    const double a = caA[k];
+    if (!didWrap || fabs(a) != kPi) caA[m++] = a;
+  }
+  if (m == 0) {
+    cmd0 = cmd1 = 0.0;
+    cmd2 = 0.0;
+    return true;
+  }
+  for (int k = 1; k < m; ++k) {
+    const double a = caA[k];
+    int pos = k;
+    while (pos > 0 && a < caA[pos - 1]) { caA[pos] = caA[pos - 1]; --pos; }
+    caA[pos] = a;
+  }
+  int it = 0;  // std::lower_bound
+  while (it < m && caA[it] < psi) ++it;
+  int idx;
+  if (it == 0) idx = 0;
+  else if (it == m || fabs(caA[it - 1] - psi) < fabs(caA[it] - psi)) idx = it - 1;
+  else idx = it;
+  const double edge = caA[idx];
+  if (fabs(wrap_to_pi(edge - psi)) <= kPi / 2) {
+    const double umag = sqrt(cmd0 * cmd0 + cmd1 * cmd1);
+    cmd0 = umag * cos(edge);
+    cmd1 = umag * sin(edge);
+  } else {
+    cmd0 = cmd1 = 0.0;
+    cmd2 = 0.0;
+  }
+  return true;
+}
+
 #ifndef ACL_CA_GRID
-#define ACL_CA_GRID 1024
+#define ACL_CA_GRID 2048
 #endif
-__global__ void __launch_bounds__(64 * kCaWaves, ACL_CA_WAVES_PER_SIMD) ca_kernel(const CtlParams P) {
+// diagnostic build (-DACL_CA_PROF=1, scripts/phase_profile.py --crowd): wave
+// cycles of the sector build, the resolution and the rest into
+// P.stamps[b][8..10], close vehicles into [11]
+#ifndef ACL_CA_PROF
+#define ACL_CA_PROF 0
+#endif
+#if ACL_CA_PROF
+#define CPROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define CPROF_ADD(acc, x) acc += (x)
+#else
+#define CPROF_T(v)
+#define CPROF_ADD(acc, x)
+#endif
+__global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const int NW = (n + 63) >> 6;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  unsigned char* base_ = smem + wave * ca_wave_bytes(n);
-  double* q = reinterpret_cast<double*>(base_);
-  double* caA = reinterpret_cast<double*>(base_ + cal16(n * 3 * 8));
-  signed char* caS = reinterpret_cast<signed char*>(base_ + cal16(n * 3 * 8) + cal16(4 * n * 8));
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const CaLayout L = ca_layout(n);
+  double* q = reinterpret_cast<double*>(smem);
+  unsigned char* wb = smem + L.wave + wave * L.wbytes;
+  double* caA = reinterpret_cast<double*>(wb + L.a);
+  double* tA = reinterpret_cast<double*>(wb + L.t);
+  signed char* caS = reinterpret_cast<signed char*>(wb + L.s);
+  signed char* tS = reinterpret_cast<signed char*>(wb + L.ts);
+  unsigned* nca = reinterpret_cast<unsigned*>(smem + L.nca);
   const acl_safety_params_t sp = P.s;
   const unsigned count = *P.ca_count;
-  for (unsigned it = blockIdx.x * kCaWaves + wave; it < count; it += gridDim.x * kCaWaves) {
-    const unsigned ent = P.ca_list[it];
-    const int b = (int)(ent / (unsigned)n), v = (int)(ent % (unsigned)n);
+  for (unsigned it = blockIdx.x; it < count; it += gridDim.x) {
+    const int b = (int)P.ca_list[it];
     const double* gq = P.q + (size_t)b * n * 3;
-    for (int k = lane; k < 3 * n; k += 64) q[k] = gq[k];
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-    const double* gu = P.u + ((size_t)b * n + v) * 3;
-    double cmd0 = gu[0], cmd1 = gu[1], cmd2 = gu[2];
-    saturate(sp, cmd0, cmd1, cmd2);
-    const double qv0 = q[3 * v], qv1 = q[3 * v + 1];
-    // Safety::collisionAvoidance (safety.cpp:412-541)
-    bool modified = false;
-    {
-      int base = 0;
-      bool wrapped = false;
-      for (int c = 0; c < NW; ++c) {
-        const int j = lane + 64 * c;
-        bool cand = false;
-        double dx = 0.0, dy = 0.0, dd = 0.0;
-        if (j < n && j != v) {
-          dx = q[3 * j] - qv0;
-          dy = q[3 * j + 1] - qv1;
-          dd = sqrt(dx * dx + dy * dy);
-          cand = !(dd > sp.d_avoid_thresh);
-        }
-        const unsigned long long m = __ballot(cand);
-        if (cand) {
-          const int slot = 4 * (base + __popcll(m & ((1ull << lane) - 1ull)));
-          const double theta = atan2(dy, dx);
-          const double x = sp.r_keep_out / dd;
-          const double alpha = fabs(asin(x < 1.0 ? x : 1.0));
-          const double beg = wrap_to_pi(theta - alpha);
-          const double end = wrap_to_pi(theta + alpha);
-          caA[slot] = beg;     caS[slot] = +1;
-          caA[slot + 1] = end; caS[slot + 1] = -1;
-          if (beg > end) {
-            wrapped = true;
-            caA[slot + 2] = -kPi; caS[slot + 2] = +1;
-            caA[slot + 3] = kPi;  caS[slot + 3] = -1;
-          } else {
-            caS[slot + 2] = 0;
-            caS[slot + 3] = 0;
+    for (int k = tid; k < 3 * n; k += 64 * kCaWaves) q[k] = gq[k];
+    if (tid == 0) *nca = 0u;
+    __syncthreads();
+#if ACL_CA_PROF
+    unsigned long long cp_build = 0, cp_res = 0, cp_all = 0, cp_cnt = 0;
+    CPROF_T(cw0);
+#endif
+    unsigned mine = 0;  // commands this wave modified (lane 0)
+    int r = 0;          // rank of the close vehicle in the swarm: wave r % kCaWaves
+    const uint64_t* cmask = P.ca_mask + (size_t)b * NW;
+    for (int w = 0; w < NW; ++w) {
+      unsigned long long mw = cmask[w];
+      while (mw) {
+        const int v = 64 * w + __ffsll((long long)mw) - 1;
+        mw &= mw - 1ull;
+        if ((r++ % kCaWaves) != wave) continue;
+        CPROF_T(cb0);
+        CPROF_ADD(cp_cnt, 1ull);
+        const double* gu = P.u + ((size_t)b * n + v) * 3;
+        double cmd0 = gu[0], cmd1 = gu[1], cmd2 = gu[2];
+        saturate(sp, cmd0, cmd1, cmd2);
+        const double qv0 = q[3 * v], qv1 = q[3 * v + 1];
+        // Safety::collisionAvoidance (safety.cpp:412-541): the sector of
+        // every vehicle within d_avoid_thresh, 4 slots per vehicle (the
+        // wrapped part [-pi, pi] when the sector crosses +-pi)
+        bool modified = false;
+        int base = 0;
+        bool wrapped = false;
+        for (int c = 0; c < NW; ++c) {
+          const int j = lane + 64 * c;
+          bool cand = false;
+          double dx = 0.0, dy = 0.0, dd = 0.0;
+          if (j < n && j != v) {
+            dx = q[3 * j] - qv0;
+            dy = q[3 * j + 1] - qv1;
+            dd = sqrt(dx * dx + dy * dy);
+            cand = !(dd > sp.d_avoid_thresh);
           }
-        }
-        base += __popcll(m);
-      }
-      if (base > 0) {
-        const bool didWrap = __any(wrapped);
-        const int nslot = 4 * base;
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        // up to 16 close vehicles: the whole wave resolves the sectors; more
-        // (or a NaN angle) take the serial path
-        bool nanA = false;
-        if (nslot <= 64 && lane < nslot) nanA = caS[lane] != 0 && caA[lane] != caA[lane];
-        const bool par = nslot <= 64 && !__any(nanA);
-        if (par) modified = ca_resolve_wave(lane, nslot, caA, caS, didWrap, cmd0, cmd1, cmd2);
-        if (!par && lane == 0) {
-          // compact + insertion sort by (angle, sign) = std::sort on pairs
-          int ne = 0;
-          for (int k = 0; k < nslot; ++k) {
-            const signed char sg = caS[k];
-            if (sg == 0) continue;
-            const double a = caA[k];
-            int pos = ne;
-            while (pos > 0 && (a < caA[pos - 1] || (!(caA[pos - 1] < a) && sg < caS[pos - 1]))) {
-              caA[pos] = caA[pos - 1];
-              caS[pos] = caS[pos - 1];
-              --pos;
-            }
-            caA[pos] = a;
-            caS[pos] = sg;
-            ++ne;
-          }
-          // parenthesis-count union into zones, stored in place (nz <= ne/2)
-          int nz = 0, count = 0;
-          double start = 0.0;
-          for (int k = 0; k < ne; ++k) {
-            const double a = caA[k];
-            if (count == 0) start = a;
-            count += caS[k];
-            if (count == 0) {
-              caA[2 * nz] = start;
-              caA[2 * nz + 1] = a;
-              ++nz;
-            }
-          }
-          const double psi = atan2(cmd1, cmd0);
-          bool safe = true;
-          for (int k = 0; k < nz; ++k)
-            if (psi > caA[2 * k] && psi < caA[2 * k + 1]) { safe = false; break; }
-          if (!safe) {
-            modified = true;
-            // flatten zone edges (drop +-pi ones when wrapped), sort
-            int m = 0;
-            for (int k = 0; k < 2 * nz; ++k) {
-              const double a = caA[k];
-              if (!didWrap || fabs(a) != kPi) caA[m++] = a;
-            }
-            if (m == 0) {
-              cmd0 = cmd1 = 0.0;
-              cmd2 = 0.0;
+          const unsigned long long m = __ballot(cand);
+          if (cand) {
+            const int slot = 4 * (base + __popcll(m & ((1ull << lane) - 1ull)));
+            const double theta = atan2(dy, dx);
+            const double x = sp.r_keep_out / dd;
+            const double alpha = fabs(asin(x < 1.0 ? x : 1.0));
+            const double beg = wrap_to_pi(theta - alpha);
+            const double end = wrap_to_pi(theta + alpha);
+            caA[slot] = beg;     caS[slot] = +1;
+            caA[slot + 1] = end; caS[slot + 1] = -1;
+            if (beg > end) {
+              wrapped = true;
+              caA[slot + 2] = -kPi; caS[slot + 2] = +1;
+              caA[slot + 3] = kPi;  caS[slot + 3] = -1;
             } else {
-              for (int k = 1; k < m; ++k) {
-                const double a = caA[k];
-                int pos = k;
-                while (pos > 0 && a < caA[pos - 1]) { caA[pos] = caA[pos - 1]; --pos; }
-                caA[pos] = a;
-              }
-              int it = 0;  // std::lower_bound
-              while (it < m && caA[it] < psi) ++it;
-              int idx;
-              if (it == 0) idx = 0;
-              else if (it == m || fabs(caA[it - 1] - psi) < fabs(caA[it] - psi)) idx = it - 1;
-              else idx = it;
-              const double edge = caA[idx];
-              if (fabs(wrap_to_pi(edge - psi)) <= kPi / 2) {
-                const double umag = sqrt(cmd0 * cmd0 + cmd1 * cmd1);
-                cmd0 = umag * cos(edge);
-                cmd1 = umag * sin(edge);
-              } else {
-                cmd0 = cmd1 = 0.0;
-                cmd2 = 0.0;
-              }
+              caS[slot + 2] = 0;
+              caS[slot + 3] = 0;
             }
           }
+          base += __popcll(m);
         }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
+        CPROF_T(cb1);
+        CPROF_ADD(cp_build, cb1 - cb0);
+        if (base > 0) {
+          const bool didWrap = __any(wrapped);
+          const int nslot = 4 * base;
+          __builtin_amdgcn_wave_barrier();
+          asm volatile("" ::: "memory");
+          bool nanA = false;
+          for (int e = lane; e < nslot; e += 64) nanA |= caS[e] != 0 && caA[e] != caA[e];
+          if (__any(nanA)) {
+            if (lane == 0) modified = ca_resolve_serial(nslot, caA, caS, didWrap, cmd0, cmd1, cmd2);
+          } else if (nslot <= 8) {
+            modified = ca_resolve_wave<8>(lane, nslot, caA, caS, didWrap, cmd0, cmd1, cmd2);
+          } else if (nslot <= 16) {
+            modified = ca_resolve_wave<16>(lane, nslot, caA, caS, didWrap, cmd0, cmd1, cmd2);
+          } else if (nslot <= 32) {
+            modified = ca_resolve_wave<32>(lane, nslot, caA, caS, didWrap, cmd0, cmd1, cmd2);
+          } else if (nslot <= 64) {
+            modified = ca_resolve_wave<64>(lane, nslot, caA, caS, didWrap, cmd0, cmd1, cmd2);
+          } else {
+            modified = ca_resolve_general(lane, nslot, caA, caS, tA, tS, didWrap, cmd0, cmd1,
+                                          cmd2);
+          }
+          __builtin_amdgcn_wave_barrier();
+          asm volatile("" ::: "memory");
+        }
+        CPROF_T(cb2);
+        CPROF_ADD(cp_res, cb2 - cb1);
+        if (lane == 0) {
+          if (P.u_safe) {
+            double* o = P.u_safe + ((size_t)b * n + v) * 3;
+            o[0] = cmd0; o[1] = cmd1; o[2] = cmd2;
+          }
+          if (modified) {
+            if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 1;
+            ++mine;
+          }
+        }
       }
     }
-    if (lane == 0) {
-      if (P.u_safe) {
-        double* o = P.u_safe + ((size_t)b * n + v) * 3;
-        o[0] = cmd0; o[1] = cmd1; o[2] = cmd2;
-      }
-      if (modified) {
-        if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 1;
-        // n_ca is the high half of the status word at byte offset 8
-        atomicAdd(reinterpret_cast<unsigned*>(&P.status[b]) + 2, 1u << 16);
-        atomicOr(&P.status[b].flags, (uint32_t)ACL_SWARM_CA_ACTIVE);
-      }
+    if (lane == 0 && mine) atomicAdd(nca, mine);
+#if ACL_CA_PROF
+    CPROF_T(cw1);
+    if (P.stamps && lane == 0) {
+      unsigned long long* ps = P.stamps + (size_t)b * 16;
+      atomicAdd(ps + 8, cp_build);
+      atomicAdd(ps + 9, cp_res);
+      atomicAdd(ps + 10, (cw1 - cw0) - cp_build - cp_res);
+      atomicAdd(ps + 11, cp_cnt);
     }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
+#endif
+    __syncthreads();
+    // the workgroup owns the swarm's status word here (the control kernels
+    // before it are stream-ordered): n_ca is the high half of the word at
+    // byte offset 8
+    if (tid == 0 && *nca) {
+      reinterpret_cast<unsigned*>(&P.status[b])[2] += *nca << 16;
+      P.status[b].flags |= (uint32_t)ACL_SWARM_CA_ACTIVE;
+    }
   }
 }
 
@@ -797,13 +986,13 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
     else ACL_GAIN(9, false);
 #undef ACL_GAIN
   } else {
-    // a fixed grid striding over the device-side count of listed vehicles
-    const int lds = kCaWaves * ca_wave_bytes(P.n);
+    // a fixed grid striding over the device-side count of listed swarms
+    const int lds = ca_layout(P.n).total;
     if (lds > 64 * 1024)
       (void)hipFuncSetAttribute((const void*)ca_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(ca_kernel, dim3(nb < ACL_CA_GRID ? nb : ACL_CA_GRID), dim3(64 * kCaWaves), lds, stream,
-                       P);
+    hipLaunchKernelGGL(ca_kernel, dim3(nb < ACL_CA_GRID ? nb : ACL_CA_GRID), dim3(64 * kCaWaves),
+                       lds, stream, P);
   }
   return hipGetLastError();
 }

@@ -55,8 +55,14 @@ __device__ __forceinline__ void saturate(const acl_safety_params_t& sp, double& 
 // !(|dq_xy| > d_avoid_thresh)? |dq_xy|^2 above (thr (1 + 2^-40))^2 is far
 // for certain, so the sqrt is taken only near the threshold. q: the swarm's
 // positions in vehicle order (LDS), uo: DistCntrl's u per vehicle (LDS).
-__device__ __forceinline__ void gain_epilogue(const CtlParams& P, int b, int n, const double* q, const double* uo,
-                              int tid, int nthreads = kCtlBlock) {
+// The close vehicles go to the swarm's mask words (a wave's 64 lanes are the
+// vehicles of one word: nthreads is a multiple of 64), and the swarm once to
+// the collision list: caw is an LDS word the caller zeroed before a barrier
+// that precedes this call (the first wave with a close vehicle appends).
+__device__ __forceinline__ void gain_epilogue(const CtlParams& P, int b, int n, const double* q,
+                                              const double* uo, unsigned* caw, int tid,
+                                              int nthreads = kCtlBlock) {
+  const int NW = (n + 63) >> 6;
   const acl_safety_params_t sp = P.s;
   const double thr_hi = sp.d_avoid_thresh * (1.0 + 0x1p-40);
   const double thr2hi = thr_hi * thr_hi;
@@ -84,9 +90,11 @@ __device__ __forceinline__ void gain_epilogue(const CtlParams& P, int b, int n, 
       o[0] = cmd0; o[1] = cmd1; o[2] = cmd2;
     }
     if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 0;
-    if (close) {  // the rest of collisionAvoidance runs in ca_kernel
-      const unsigned slot = atomicAdd(P.ca_count, 1u);
-      P.ca_list[slot] = (unsigned)(b * n + v);
+    // the rest of collisionAvoidance runs in ca_kernel
+    const unsigned long long cm = __ballot(close);
+    if ((tid & 63) == 0) {
+      P.ca_mask[(size_t)b * NW + (v >> 6)] = cm;
+      if (cm && atomicOr(caw, 1u) == 0u) P.ca_list[atomicAdd(P.ca_count, 1u)] = (unsigned)b;
     }
   }
 }
@@ -254,7 +262,7 @@ __device__ __forceinline__ double swap_sum(double x) {
 }
 
 struct PairLayout {
-  int q, qf, p, pn, adjF, rowpre, etab, Pt, acc, out, atab, tmask, tstart, gmw, total;
+  int q, qf, p, pn, adjF, rowpre, etab, Pt, acc, out, atab, tmask, tstart, gmw, caw, total;
 };
 
 __host__ __device__ inline PairLayout make_pair_layout(int n, int kW = kCtlWaves, bool tiled = true) {
@@ -276,7 +284,8 @@ __host__ __device__ inline PairLayout make_pair_layout(int n, int kW = kCtlWaves
   const int NT = (tiled && n <= kMaxN) ? pair_tiles(n) : 0;  // tiled records: n <= 128 only
   L.tmask = o;  o = cal16(o + 2 * NT * 8);
   L.tstart = o; o = cal16(o + 2 * NT * 4);
-  L.gmw = o;    o = cal16(o + 8);                  // gate margin word
+  L.gmw = o;    o = o + 8;                         // gate margin word
+  L.caw = o;    o = cal16(o + 4);                  // the swarm is on the collision list
   L.total = o;
   return L;
 }
@@ -339,6 +348,8 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
   // 160 KiB): set before the barriers below
   unsigned long long& gmw = *reinterpret_cast<unsigned long long*>(smem + L.gmw);
   if (GM && tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
+  unsigned* caw = reinterpret_cast<unsigned*>(smem + L.caw);
+  if (tid == 0) *caw = 0u;
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
   {
     const double* gq = P.q + (size_t)b * n * 3;
@@ -652,7 +663,7 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
     }
   }
   __syncthreads();
-  gain_epilogue(P, b, n, q, uo, tid, nthreads);
+  gain_epilogue(P, b, n, q, uo, caw, tid, nthreads);
 }
 
 }  // namespace acl_amd

@@ -43,12 +43,16 @@ constexpr int kMaxNWide = 512;  // tables-in-HBM auction kernel (solve_wide.hip)
 //   mode    [B]    u8     0: all vehicles use pt, 1: per-vehicle rows
 //   rows    [B][n][n] u16 per-vehicle inverse assignments (mode 1)
 //   u       [B][n][3] f64 DistCntrl output when the caller passes u = NULL
-//   calist  [B*n] u32     vehicles whose collisionAvoidance must finish
-//   cacount u32
+//   calist  [B]    u32    swarms with a vehicle whose collisionAvoidance must
+//                         finish (appended once per swarm)
+//   cacount u32           entries of calist
+//   camask  [B][NW] u64   the swarm's vehicles within d_avoid_thresh of
+//                         another (bit v of word v/64; every word rewritten
+//                         by each control step's epilogue)
 //   wide    [B] x (C n*n f32, CT n*n f32, T n*n u16): the CBAA tables of
 //           the n > 128 kernel, which do not fit LDS
 struct WsLayout {
-  size_t pt, mode, rows, u, calist, cacount, wide, wide_stride, total;
+  size_t pt, mode, rows, u, calist, cacount, camask, wide, wide_stride, total;
 };
 
 __host__ __device__ inline size_t ws_al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -61,8 +65,9 @@ __host__ __device__ inline WsLayout ws_layout(int n, int B) {
   W.mode = o;    o = ws_al(o + bb);
   W.rows = o;    o = ws_al(o + bb * nb * nb * 2);
   W.u = o;       o = ws_al(o + bb * nb * 3 * 8);
-  W.calist = o;  o = ws_al(o + bb * nb * 4);
+  W.calist = o;  o = ws_al(o + bb * 4);
   W.cacount = o; o = ws_al(o + 16);
+  W.camask = o;  o = ws_al(o + bb * (size_t)((n + 63) >> 6) * 8);
   W.wide = o;
   W.wide_stride = n > kMaxN ? ws_al(nb * nb * (4 + 4 + 2)) : 0;
   o += bb * W.wide_stride;
@@ -89,14 +94,16 @@ struct CtlParams {
   const uint16_t* wsPt;
   const uint8_t* wsMode;
   const uint16_t* wsRows;
-  unsigned* ca_list;
+  unsigned* ca_list;   // swarms with close vehicles (WsLayout::calist)
   unsigned* ca_count;
+  uint64_t* ca_mask;   // [B][NW] close vehicles per swarm (WsLayout::camask)
   acl_cntrl_gains_t g;
   acl_safety_params_t s;
   int only_nonuniform;  // set by launch_control: gain_kernel skips uniform swarms
   int all_uniform;      // every swarm has one assignment (given P): no gain_kernel pass
   int F;                // formations in the table (fidx range check of the hand-off)
   double* gate_margin;  // [B] optional: min | |e| - thr | / thr of the swarm's gates
+  unsigned long long* stamps;  // diagnostic (SolveParams::stamps; NULL = off)
 };
 
 struct SolveParams {
@@ -134,7 +141,7 @@ enum { M_BAD = 0, M_NONFIN = 1, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 
 
 // Control stage: which = 0 launches the gain kernel for swarms
 // [P.b0, P.b0 + nb) (DistCntrl::compute, saturation, the collision test),
-// 1 the collisionAvoidance kernel over the listed vehicles, 2 the directed
+// 1 the collisionAvoidance kernel over the listed swarms, 2 the directed
 // gain kernel for the swarms with per-vehicle assignments only (after the
 // fused auction + control kernel, which did the others).
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream);

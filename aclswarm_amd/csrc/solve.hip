@@ -187,6 +187,8 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
     C.wsRows = reinterpret_cast<const uint16_t*>(P.ws + P.W.rows);
     C.ca_list = reinterpret_cast<unsigned*>(P.ws + P.W.calist);
     C.ca_count = reinterpret_cast<unsigned*>(P.ws + P.W.cacount);
+    C.ca_mask = reinterpret_cast<uint64_t*>(P.ws + P.W.camask);
+    C.stamps = P.stamps;
     C.g = a->cntrl; C.s = a->safety;
     C.only_nonuniform = 0;
     C.all_uniform = 0;
@@ -247,6 +249,8 @@ acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_a
   C.wsRows = reinterpret_cast<const uint16_t*>(ws + W.rows);
   C.ca_list = reinterpret_cast<unsigned*>(ws + W.calist);
   C.ca_count = reinterpret_cast<unsigned*>(ws + W.cacount);
+  C.ca_mask = reinterpret_cast<uint64_t*>(ws + W.camask);
+  C.stamps = nullptr;
   C.g = a->cntrl; C.s = a->safety;
   C.only_nonuniform = 0;
   C.all_uniform = 1;  // the hand-off of a given P is one assignment per swarm

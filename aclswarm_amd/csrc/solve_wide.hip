@@ -123,6 +123,21 @@ __device__ __forceinline__ void wstamp(const SolveParams& P, int b, int k) {
   if (P.stamps && threadIdx.x == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
 }
 
+// diagnostic build (-DACL_WIDE_PROF=1, scripts/phase_profile.py): CBAA
+// section cycles summed over the swarm's waves into P.stamps[b][7..10] and
+// counts into [11] (columns | exact scans << 21 | re-selects << 42), [12]
+// rounds
+#ifndef ACL_WIDE_PROF
+#define ACL_WIDE_PROF 0
+#endif
+#if ACL_WIDE_PROF
+#define WPROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define WPROF_ADD(acc, x) acc += (x)
+#else
+#define WPROF_T(v)
+#define WPROF_ADD(acc, x)
+#endif
+
 __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
@@ -389,6 +404,9 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   }
   __syncthreads();
   int eff = 0;
+#if ACL_WIDE_PROF
+  unsigned long long pf_col = 0, pf_scan = 0, pf_sel = 0, pf_bar = 0, pf_cnt = 0, pf_rounds = 0;
+#endif
   unsigned obf = 0u;  // per-lane outbid bits (bit c: vehicle lane + 64 c), one round
   const int max_rounds = 2 * n;
   for (int r = 1; r <= max_rounds; ++r) {
@@ -400,6 +418,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         const int j = 64 * w + __ffsll((long long)m) - 1;
         m &= m - 1;
         if ((idx++ % kWWaves) != wave) continue;
+        WPROF_T(pc0);
+        WPROF_ADD(pf_cnt, 1ull);
         const uint16_t* Tc = T + (size_t)j * n;
         const float* CTc = CT + (size_t)j * n;
         unsigned wu[kWMaxW], key[kWMaxW], nw[kWMaxW], k1[kWMaxW], k2[kWMaxW];
@@ -479,7 +499,9 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           if (!need[c] && st[c] == 2 && k2[c] != 0u)
             margin_track(mp, __uint_as_float(k1[c] - 1u), __uint_as_float(k2[c] - 1u));
         }
+        WPROF_T(ps0);
         if (__ballot(anyneed) != 0ull) {
+          WPROF_ADD(pf_cnt, 1ull << 21);
           // exact ordered scan (ascending vehid, strict >): ties, NaN prices,
           // vehicles no tracked level decides; the runner-up is the best
           // price of another `who` (entries of one `who` share its price)
@@ -513,6 +535,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
             }
           }
         }
+        WPROF_T(ps1);
+        WPROF_ADD(pf_scan, ps1 - ps0);
         __builtin_amdgcn_wave_barrier();
         bool ch = false, mx = false;
         const unsigned nw0 = (unsigned)__builtin_amdgcn_readfirstlane((int)nw[0]);  // vehicle 0
@@ -534,6 +558,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           misc[W_RCH + par] = 1;
           if (anymx || nonfinite) atomicOr(&dmask[npar * NW + (j >> 6)], 1ull << (j & 63));
         }
+        WPROF_T(pc1);
+        WPROF_ADD(pf_col, pc1 - pc0 - (ps1 - ps0));
       }
     }
 #pragma unroll
@@ -542,7 +568,11 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       if (ob && lane == 0) atomicOr(&obm[par * NW + c], ob);
     }
     obf = 0u;
+    WPROF_T(pb0);
     __syncthreads();
+    WPROF_T(pb1);
+    WPROF_ADD(pf_bar, pb1 - pb0);
+    WPROF_ADD(pf_rounds, 1ull);
     if (tid < NW) {
       dmask[par * NW + tid] = 0ull;
       obm[npar * NW + tid] = 0ull;
@@ -556,15 +586,22 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           const int v = 64 * w + __ffsll((long long)m) - 1;
           m &= m - 1;
           if ((idx2++ % kWWaves) != wave) continue;
+          WPROF_T(pr0);
+          WPROF_ADD(pf_cnt, 1ull << 42);
           const int task = wide_select(n, NW, v, lane, C, CT, T, false, mp);
           if (task >= 0 && lane == 0) {
             T[(size_t)task * n + v] = (uint16_t)v;
             atomicOr(&dmask[npar * NW + (task >> 6)], 1ull << (task & 63));
           }
+          WPROF_T(pr1);
+          WPROF_ADD(pf_sel, pr1 - pr0);
         }
       }
     }
+    WPROF_T(pb2);
     __syncthreads();
+    WPROF_T(pb3);
+    WPROF_ADD(pf_bar, pb3 - pb2);
     bool next = false;
     for (int w = 0; w < NW; ++w) next |= dmask[npar * NW + w] != 0ull;
     if (next || misc[W_RCH + par]) eff = r;
@@ -573,6 +610,17 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     // remaining (empty) rounds, the reference's literal schedule
     if (!next && P.early_exit) break;
   }
+#if ACL_WIDE_PROF
+  if (P.stamps && lane == 0) {
+    unsigned long long* ps = reinterpret_cast<unsigned long long*>(P.stamps) + (size_t)b * 16;
+    atomicAdd(ps + 7, pf_col);
+    atomicAdd(ps + 8, pf_scan);
+    atomicAdd(ps + 9, pf_sel);
+    atomicAdd(ps + 10, pf_bar);
+    atomicAdd(ps + 11, pf_cnt);
+    if (wave == 0) ps[12] = pf_rounds;
+  }
+#endif
 
   wstamp(P, b, 4);
   // swarm margin: min over every thread's CBAA pair and alignment gaps

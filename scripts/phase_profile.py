@@ -21,6 +21,8 @@ ap.add_argument("--B", type=int, default=65536)
 ap.add_argument("--n", type=int, default=100)
 ap.add_argument("--formations", type=int, default=0)
 ap.add_argument("--L", type=float, default=None)
+ap.add_argument("--crowd", type=float, default=None,
+                help="scale positions about each swarm's centre (collision avoidance active)")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 gen = torch.Generator(device=dev)
@@ -30,6 +32,9 @@ if args.n > 128:
     NAMES[:] = ["load+nbhd", "align", "prices", "cbaa", "adopt", "handoff"]
 T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"],
                               w["planes"])
+if args.crowd:
+    c = w["q"][:, :, :2].mean(dim=1, keepdim=True)
+    w["q"][:, :, :2] = c + args.crowd * (w["q"][:, :, :2] - c)
 lib = L.lib()
 lib.acl_internal_set_stamps.argtypes = [ct.c_void_p]
 st = torch.zeros((args.B, 16), dtype=torch.int64, device=dev)
@@ -56,7 +61,7 @@ if (s[:, 7] > 0).all():
 # CBAA column-step sections (a -DACL_AUCTION_PROF=1 build): cycles summed
 # over a swarm's waves, and the counts of evaluated columns, walks and scans
 sec = st.cpu().numpy()[:, 7:16].astype(np.uint64)
-if sec[:, :8].any():
+if args.n <= 128 and not args.crowd and sec[:, :8].any():
     SN = ["level 0", "levels", "margin bound", "runner-up walk", "exact scan", "write-back",
           "selects+barrier", "column barrier"]
     tot8 = sec[:, :8].astype(np.float64).sum()
@@ -69,3 +74,22 @@ if sec[:, :8].any():
     scans = (cnt >> np.uint64(42)).astype(np.float64)
     print(f"  per swarm: columns evaluated {cols.mean():.1f}, runner-up walks {walks.mean():.1f}, "
           f"exact scans {scans.mean():.1f}")
+# wide CBAA sections (a -DACL_WIDE_PROF=1 build, n > 128): wave-cycles summed
+# over the swarm's 16 waves
+if args.n > 128 and sec[:, :4].any():
+    WN = ["column updates", "exact scans", "re-selects", "round barriers"]
+    for k, nm in enumerate(WN):
+        x = sec[:, k].astype(np.float64)
+        print(f"  wide {nm:16s} wave-cycles/swarm {x.mean():12.0f}")
+    cnt = sec[:, 4]
+    m21 = np.uint64((1 << 21) - 1)
+    print(f"  per swarm: columns {(cnt & m21).astype(float).mean():.1f}, exact scans "
+          f"{((cnt >> np.uint64(21)) & m21).astype(float).mean():.1f}, re-selects "
+          f"{(cnt >> np.uint64(42)).astype(float).mean():.1f}, rounds {sec[:, 5].astype(float).mean():.1f}")
+# collision avoidance (a -DACL_CA_PROF=1 build, --crowd): ca_kernel wave-cycles
+if args.crowd:
+    x = st.cpu().numpy()[:, 8:12].astype(np.float64)
+    cnt = x[:, 3].sum()
+    print(f"  ca close vehicles {cnt:.0f} ({cnt / args.B:.1f} per swarm)")
+    for k, nm in enumerate(["sector build", "resolve", "other (q, loop)"]):
+        print(f"  ca {nm:16s} wave-cycles per close vehicle {x[:, k].sum() / max(cnt, 1):10.0f}")

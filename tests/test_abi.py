@@ -120,14 +120,14 @@ def test_status_record_is_16_bytes():
 
 
 def test_abi_version_and_formations_init():
-    """ABI 3 (gains_tiled in acl_formations_t, margin in the status, gate
-    margins): acl_formations_init zero-fills the struct so no optional pointer
+    """ABI 5 (gains_tiled in acl_formations_t, margin in the status, gate
+    margins, the episode's auction latency and pending state): acl_formations_init zero-fills the struct so no optional pointer
     is left as garbage; the solve rejects an empty formation table."""
     from aclswarm_amd import _lib as L
     with open(os.path.join(ROOT, "include", "aclswarm_amd.h")) as f:
-        assert "#define ACL_ABI_VERSION 4" in f.read()
+        assert "#define ACL_ABI_VERSION 5" in f.read()
     lib = L.lib()
-    assert lib.acl_abi_version() == 4 == L.ABI_VERSION  # the load-time check's inputs
+    assert lib.acl_abi_version() == 5 == L.ABI_VERSION  # the load-time check's inputs
     F = L.Formations()
     ct.memset(ct.byref(F), 0xAB, ct.sizeof(F))
     lib.acl_formations_init(ct.byref(F), 100, 7)

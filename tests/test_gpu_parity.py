@@ -303,6 +303,32 @@ def test_wide_collision_avoidance(cuda):
     _compare(gpu, ref)
 
 
+@pytest.mark.parametrize("n", [24, 64, 128, 200])
+def test_collision_avoidance_packed(cuda, n):
+    """Packed swarms: most vehicles have more than 16 others within
+    d_avoid_thresh (more than 64 sector edges: ca_kernel's rank-sort path),
+    beside sparser swarms of the same batch (the bitonic paths)."""
+    from aclswarm_amd import _lib
+    rng = np.random.RandomState(900 + n)
+    p = H.random_positions(rng, n, 3.0 * n)
+    adj = (np.ones((n, n)) - np.eye(n)).astype(np.uint8)
+    G = H.synth_gains(rng, adj, scale=1.0)
+    B = 4
+    side = [2.0, 3.0, 0.25 * n ** 0.5 + 2.0, 0.6 * n ** 0.5 + 3.0]
+    q = np.stack([H.dense_positions(rng, n, side[b]) for b in range(B)])
+    vel = rng.normal(0, 0.5, (B, n, 3))
+    P_in = np.stack([H.random_perm(rng, n) for _ in range(B)])
+    thr = _lib.default_safety().d_avoid_thresh
+    d = np.hypot(q[:, :, None, 0] - q[:, None, :, 0], q[:, :, None, 1] - q[:, None, :, 1])
+    close = (d <= thr).sum(axis=2) - 1
+    assert (close > 16).sum() > n // 2 and ((close > 0) & (close <= 16)).sum() > 0
+    args = ([p], [adj], [G], np.zeros(B, np.int32), q, vel, P_in)
+    gpu = _gpu_solve(*args)
+    ref = _oracle(*args)
+    assert sum(int(r["status"]["n_ca"]) for r in ref) > n // 2
+    _compare(gpu, ref)
+
+
 def _c4_inputs(B, seed):
     """Config C4: simform500 formations (N=500, L=90, the reference generator's
     own output, tests/golden/simform500_nc.npz), u16 indices."""
