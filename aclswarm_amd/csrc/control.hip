@@ -876,6 +876,389 @@ __global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
   }
 }
 
+// ---- collisionAvoidance by pairs (n <= 128) ----------------------------------
+//
+// ca_kernel gives every close vehicle a wave whose lanes run over the other
+// vehicles: in a crowded swarm a vehicle has a handful of neighbours inside
+// d_avoid_thresh, so the atan2 / asin of the sector edges (the kernel's fp64
+// bulk) ran on a few lanes of two 64-lane chunks. ca_pair_kernel works by
+// (vehicle, neighbour) pairs instead: one workgroup per listed swarm
+//   A  lanes over the swarm's close vehicles: the saturated command and psi
+//   B  a wave per close vehicle: its candidates (distance test, lanes over
+//      the others) as mask words and counts; a prefix gives each vehicle a
+//      contiguous run of pairs
+//   C  lanes over the pairs (64 per instruction): theta, alpha and the
+//      sector's two edges (beg, +1), (end, -1) at slots 2p, 2p + 1; a wrapped
+//      sector adds (-pi, +1), (pi, -1) -- identical for every wrap, so only
+//      counted per vehicle and synthesized where a vehicle's edges are read
+//   D  the union and closest safe edge of up to 4 vehicles per wave: 16-,
+//      32- or 64-lane segments by edge count (bitonic sort of (angle, sign)
+//      keys, prefix count, ballots per segment); more than 64 edges or a NaN
+//      angle: one vehicle at a time on the general / serial paths
+//   E  lanes over the close vehicles: cos / sin of the chosen edge, u_safe,
+//      ca_flag
+// The same math as ca_kernel in the same operation order (identical results).
+// Pairs are processed in batches of at most kCaPairCap (a vehicle has at most
+// n - 1 <= 127), so the LDS image stays bounded.
+constexpr int kCaPairCap = 1024;
+constexpr int kCaPT = 256;
+
+struct CaPairLayout {
+  int q, cl, cmd, psi, cnt, off, wr, flg, edge, cmk, lists, pairs, ang, sA, sS, tA, tS, misc,
+      total;
+};
+__host__ __device__ inline CaPairLayout ca_pair_layout(int n) {
+  CaPairLayout L;
+  int o = 0;
+  L.q = o;     o = cal16(o + n * 24);
+  L.cl = o;    o = cal16(o + n * 2);        // close vehicles (ascending)
+  L.cmd = o;   o = cal16(o + n * 24);       // saturated commands
+  L.psi = o;   o = cal16(o + n * 8);
+  L.cnt = o;   o = cal16(o + n * 4);        // candidates per close vehicle
+  L.off = o;   o = cal16(o + (n + 1) * 4);  // exclusive prefix of cnt
+  L.wr = o;    o = cal16(o + n * 4);        // wrapped sectors
+  L.flg = o;   o = cal16(o + n * 4);        // NaN edge (bit 0); result: 1 edge, 2 stop (bits 8..)
+  L.edge = o;  o = cal16(o + n * 8);        // the chosen edge
+  L.cmk = o;   o = cal16(o + n * 2 * 8);    // candidate masks [k][2]
+  L.lists = o; o = cal16(o + 4 * n * 2);    // vehicles per resolve class (16/32/64/general)
+  L.pairs = o; o = cal16(o + kCaPairCap * 2);   // neighbour of each pair (u8 k | u8 j)
+  L.ang = o;   o = cal16(o + kCaPairCap * 2 * 8);
+  L.sA = o;    o = cal16(o + 4 * n * 8);    // general / serial paths: one vehicle's slots
+  L.sS = o;    o = cal16(o + 4 * n);
+  L.tA = o;    o = cal16(o + 4 * n * 8);
+  L.tS = o;    o = cal16(o + 4 * n);
+  L.misc = o;  o = cal16(o + 16 * 4);
+  L.total = o;
+  return L;
+}
+
+// Segmented resolution: S-lane segments (S = 16, 32, 64), one vehicle each;
+// lane e of a segment holds element e of its vehicle (m elements, e >= m an
+// unused slot sorting last). As ca_resolve_wave, per segment. Returns the
+// outcome for the lane's vehicle: 0 safe, 1 new direction `edge`, 2 stop.
+template <int S>
+__device__ __forceinline__ int ca_resolve_seg(int lane, int m, double a, int sg, bool didWrap,
+                                              double psi, double& edge) {
+  const int e = lane & (S - 1), base = lane & ~(S - 1);
+  const unsigned long long segm = S == 64 ? ~0ull : (((1ull << S) - 1ull) << base);
+  if (e >= m) {
+    a = 0.0;
+    sg = 0;
+  }
+#pragma unroll
+  for (int k = 2; k <= S; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const double pa = __shfl_xor(a, j, 64);
+      const int ps = __shfl_xor(sg, j, 64);
+      const unsigned long long mk = ca_key(a, sg), pk = ca_key(pa, ps);
+      const bool pless = pk < mk || (pk == mk && ps < sg);
+      const bool mless = mk < pk || (mk == pk && sg < ps);
+      const bool take_min = ((e & k) == 0) == ((e & j) == 0);
+      if (take_min ? pless : mless) {
+        a = pa;
+        sg = ps;
+      }
+    }
+  }
+  int incl = sg;
+#pragma unroll
+  for (int o = 1; o < S; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (e >= o) incl += y;
+  }
+  const int excl = incl - sg;
+  const bool isEnd = sg != 0 && incl == 0;
+  const unsigned long long endMask = __ballot(isEnd) & segm;
+  const unsigned long long below = endMask & ((1ull << lane) - 1ull) & segm;
+  const int sLane = below ? 64 - __clzll(below) : base;
+  const double zs = __shfl(a, sLane, 64);
+  const bool inside = isEnd && psi > zs && psi < a;
+  if (!endMask || !(__ballot(inside) & segm)) return 0;
+  const int lastEnd = 63 - __clzll(endMask);
+  const bool isStart = sg != 0 && excl == 0 && lane < lastEnd;
+  const bool keep = (isStart || isEnd) && !(didWrap && fabs(a) == kPi);
+  const unsigned long long km = __ballot(keep) & segm;
+  const int m2 = __popcll(km);
+  if (m2 == 0) return 2;
+  const int it = __popcll(__ballot(keep && a < psi) & segm);  // std::lower_bound
+  auto nth = [&](int r) -> int {  // lane of the r-th kept edge of the segment
+    unsigned long long x = km;
+    for (int t = 0; t < r; ++t) x &= x - 1ull;
+    return __ffsll((long long)x) - 1;
+  };
+  // (the shuffles are wave-wide: every lane computes its own segment's indices)
+  int idx;
+  const int lo_l = nth(it > 0 ? it - 1 : 0), hi_l = nth(it < m2 ? it : m2 - 1);
+  const double lo = __shfl(a, lo_l, 64), hi = __shfl(a, hi_l, 64);
+  if (it == 0) idx = 0;
+  else if (it == m2) idx = it - 1;
+  else idx = fabs(lo - psi) < fabs(hi - psi) ? it - 1 : it;
+  edge = idx == it ? hi : lo;
+  if (it == 0) edge = hi;  // nth(0): the first kept edge
+  return fabs(wrap_to_pi(edge - psi)) <= kPi / 2 ? 1 : 2;
+}
+
+__global__ void __launch_bounds__(kCaPT, 4) ca_pair_kernel(const CtlParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = P.n;
+  const int NW = (n + 63) >> 6;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int kW = kCaPT / 64;
+  const CaPairLayout L = ca_pair_layout(n);
+  double* q = reinterpret_cast<double*>(smem + L.q);
+  uint16_t* cl = reinterpret_cast<uint16_t*>(smem + L.cl);
+  double* cmd = reinterpret_cast<double*>(smem + L.cmd);
+  double* psiv = reinterpret_cast<double*>(smem + L.psi);
+  int* cnt = reinterpret_cast<int*>(smem + L.cnt);
+  int* off = reinterpret_cast<int*>(smem + L.off);
+  int* wr = reinterpret_cast<int*>(smem + L.wr);
+  int* flg = reinterpret_cast<int*>(smem + L.flg);
+  double* edg = reinterpret_cast<double*>(smem + L.edge);
+  unsigned long long* cmk = reinterpret_cast<unsigned long long*>(smem + L.cmk);
+  uint16_t* lists = reinterpret_cast<uint16_t*>(smem + L.lists);
+  uint16_t* pairs = reinterpret_cast<uint16_t*>(smem + L.pairs);
+  double* ang = reinterpret_cast<double*>(smem + L.ang);
+  double* sA = reinterpret_cast<double*>(smem + L.sA);
+  signed char* sS = reinterpret_cast<signed char*>(smem + L.sS);
+  double* tA = reinterpret_cast<double*>(smem + L.tA);
+  signed char* tS = reinterpret_cast<signed char*>(smem + L.tS);
+  int* misc = reinterpret_cast<int*>(smem + L.misc);  // [0] nc, [1..4] class counts, [5] modified
+  const acl_safety_params_t sp = P.s;
+  const unsigned count = *P.ca_count;
+  for (unsigned itb = blockIdx.x; itb < count; itb += gridDim.x) {
+    const int b = (int)P.ca_list[itb];
+    const double* gq = P.q + (size_t)b * n * 3;
+    for (int k = tid; k < 3 * n; k += kCaPT) q[k] = gq[k];
+    if (wave == 0) {  // the close vehicles in ascending order
+      const uint64_t* cmask = P.ca_mask + (size_t)b * NW;
+      int base = 0;
+      for (int w = 0; w < NW; ++w) {
+        const unsigned long long mw = cmask[w];
+        if ((mw >> lane) & 1ull)
+          cl[base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mw >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((unsigned)mw, 0u))] =
+              (uint16_t)(64 * w + lane);
+        base += __popcll(mw);
+      }
+      if (lane == 0) {
+        misc[0] = base;
+        misc[5] = 0;
+      }
+    }
+    __syncthreads();
+    const int nc = misc[0];
+    // A: saturated commands and psi (lanes over the close vehicles)
+    #pragma unroll 1
+    for (int k = tid; k < nc; k += kCaPT) {
+      const int v = cl[k];
+      const double* gu = P.u + ((size_t)b * n + v) * 3;
+      double c0 = gu[0], c1 = gu[1], c2 = gu[2];
+      saturate(sp, c0, c1, c2);
+      cmd[3 * k] = c0; cmd[3 * k + 1] = c1; cmd[3 * k + 2] = c2;
+      psiv[k] = atan2(c1, c0);
+      wr[k] = 0;
+      flg[k] = 0;
+    }
+    // B: candidates of every close vehicle (a wave per vehicle, lanes over j)
+    for (int k = wave; k < nc; k += kW) {
+      const int v = cl[k];
+      const double qv0 = q[3 * v], qv1 = q[3 * v + 1];
+      int c = 0;
+      for (int w = 0; w < NW; ++w) {
+        const int j = lane + 64 * w;
+        bool cand = false;
+        if (j < n && j != v) {
+          const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
+          cand = !(sqrt(dx * dx + dy * dy) > sp.d_avoid_thresh);
+        }
+        const unsigned long long m = __ballot(cand);
+        if (lane == 0) cmk[2 * k + w] = m;
+        c += __popcll(m);
+      }
+      if (lane == 0) cnt[k] = c;
+    }
+    __syncthreads();
+    if (wave == 0) {  // exclusive prefix of the counts (nc <= 128: two per lane)
+      int base = 0;
+      for (int k0 = 0; k0 < nc; k0 += 64) {
+        const int k = k0 + lane;
+        const int c = k < nc ? cnt[k] : 0;
+        int x = c;
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(x, o, 64);
+          if (lane >= o) x += y;
+        }
+        if (k < nc) off[k] = base + x - c;
+        base += __shfl(x, 63, 64);
+      }
+      if (lane == 0) off[nc] = base;
+    }
+    __syncthreads();
+    unsigned mine = 0;  // commands this thread modified (E)
+    // batches of whole vehicles with at most kCaPairCap pairs
+    for (int k0 = 0; k0 < nc;) {
+      int k1 = k0 + 1;
+      while (k1 < nc && off[k1 + 1] - off[k0] <= kCaPairCap) ++k1;
+      const int p0 = off[k0], np = off[k1] - p0;
+      // the batch's pair list (a wave per vehicle)
+      for (int k = k0 + wave; k < k1; k += kW) {
+        int base = off[k] - p0;
+        for (int w = 0; w < NW; ++w) {
+          const unsigned long long m = cmk[2 * k + w];
+          if ((m >> lane) & 1ull)
+            pairs[base + (int)__builtin_amdgcn_mbcnt_hi(
+                             (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                (uint16_t)(((k - k0) << 8) | (64 * w + lane));
+          base += __popcll(m);
+        }
+      }
+      if (tid < 4) misc[1 + tid] = 0;
+      __syncthreads();
+      // C: the sector edges of every pair
+      #pragma unroll 1
+      for (int p = tid; p < np; p += kCaPT) {
+        const int pr = pairs[p];
+        const int k = k0 + (pr >> 8), j = pr & 0xFF;
+        const int v = cl[k];
+        const double dx = q[3 * j] - q[3 * v], dy = q[3 * j + 1] - q[3 * v + 1];
+        const double dd = sqrt(dx * dx + dy * dy);
+        const double theta = atan2(dy, dx);
+        const double x = sp.r_keep_out / dd;
+        const double alpha = fabs(asin(x < 1.0 ? x : 1.0));
+        const double beg = wrap_to_pi(theta - alpha);
+        const double end = wrap_to_pi(theta + alpha);
+        ang[2 * p] = beg;
+        ang[2 * p + 1] = end;
+        if (beg > end) atomicAdd(&wr[k], 1);
+        if (beg != beg || end != end) atomicOr(&flg[k], 1);
+      }
+      __syncthreads();
+      // resolve classes: edges m = 2 cnt + 2 wraps
+      for (int k = k0 + tid; k < k1; k += kCaPT) {
+        const int m = 2 * (cnt[k] + wr[k]);
+        const int cls = (flg[k] & 1) || m > 64 ? 3 : (m > 32 ? 2 : (m > 16 ? 1 : 0));
+        if (m > 0) lists[cls * n + atomicAdd(&misc[1 + cls], 1)] = (uint16_t)k;
+      }
+      __syncthreads();
+      // D: 4 / 2 / 1 vehicles per wave
+      {
+        const int n16 = misc[1], n32 = misc[2], n64 = misc[3];
+        const int g16 = (n16 + 3) >> 2, g32 = (n32 + 1) >> 1;
+        for (int item = wave; item < g16 + g32 + n64; item += kW) {
+          int cls, slot, S;
+          if (item < g16) { cls = 0; S = 16; slot = 4 * item + (lane >> 4); }
+          else if (item < g16 + g32) { cls = 1; S = 32; slot = 2 * (item - g16) + (lane >> 5); }
+          else { cls = 2; S = 64; slot = item - g16 - g32; }
+          const int ncls = misc[1 + cls];
+          const bool has = slot < ncls;
+          const int k = has ? lists[cls * n + slot] : k0;
+          const int c2 = has ? 2 * cnt[k] : 0, m = has ? c2 + 2 * wr[k] : 0;
+          const int e = lane & (S - 1);
+          double a = 0.0;
+          int sg = 0;
+          if (e < c2) {
+            a = ang[2 * (off[k] - p0) + e];
+            sg = (e & 1) ? -1 : +1;
+          } else if (e < m) {
+            a = ((e - c2) & 1) ? kPi : -kPi;
+            sg = ((e - c2) & 1) ? -1 : +1;
+          }
+          double edge = 0.0;
+          const double psi = psiv[k];
+          int res;
+          if (S == 16) res = ca_resolve_seg<16>(lane, m, a, sg, wr[k] > 0, psi, edge);
+          else if (S == 32) res = ca_resolve_seg<32>(lane, m, a, sg, wr[k] > 0, psi, edge);
+          else res = ca_resolve_seg<64>(lane, m, a, sg, wr[k] > 0, psi, edge);
+          if (has && e == 0) {
+            flg[k] |= res << 8;
+            edg[k] = edge;
+          }
+        }
+      }
+      // more than 64 edges or a NaN angle: one vehicle at a time (wave 0) on
+      // the general and serial paths over its slots in sA / sS
+      if (wave == 0) {
+        const int ng = misc[4];
+        for (int s = 0; s < ng; ++s) {
+          const int k = lists[3 * n + s];
+          const int c2 = 2 * cnt[k], m = c2 + 2 * wr[k];
+          for (int e = lane; e < m; e += 64) {
+            if (e < c2) {
+              sA[e] = ang[2 * (off[k] - p0) + e];
+              sS[e] = (e & 1) ? -1 : +1;
+            } else {
+              sA[e] = ((e - c2) & 1) ? kPi : -kPi;
+              sS[e] = ((e - c2) & 1) ? -1 : +1;
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+          asm volatile("" ::: "memory");
+          double c0 = cmd[3 * k], c1 = cmd[3 * k + 1], c2d = cmd[3 * k + 2];
+          const double u0 = c0, u1 = c1;
+          bool mod = false;
+          if (flg[k] & 1) {
+            if (lane == 0) mod = ca_resolve_serial(m, sA, sS, wr[k] > 0, c0, c1, c2d);
+            mod = __shfl(mod ? 1 : 0, 0, 64) != 0;
+            c0 = __shfl(c0, 0, 64);
+            c1 = __shfl(c1, 0, 64);
+            c2d = __shfl(c2d, 0, 64);
+          } else {
+            mod = ca_resolve_general(lane, m, sA, sS, tA, tS, wr[k] > 0, c0, c1, c2d);
+          }
+          __builtin_amdgcn_wave_barrier();
+          asm volatile("" ::: "memory");
+          if (lane == 0 && mod) {
+            // the paths applied the command themselves: store it as a
+            // resolved outcome (3: explicit command in cmd)
+            flg[k] |= 3 << 8;
+            cmd[3 * k] = c0; cmd[3 * k + 1] = c1; cmd[3 * k + 2] = c2d;
+          }
+          (void)u0; (void)u1;
+        }
+      }
+      __syncthreads();
+      // E: the modified commands
+      #pragma unroll 1
+      for (int k = k0 + tid; k < k1; k += kCaPT) {
+        const int res = flg[k] >> 8;
+        if (!res) continue;
+        const int v = cl[k];
+        double c0 = cmd[3 * k], c1 = cmd[3 * k + 1], c2 = cmd[3 * k + 2];
+        if (res == 1) {
+          const double edge = edg[k];
+          const double umag = sqrt(c0 * c0 + c1 * c1);
+          c0 = umag * cos(edge);
+          c1 = umag * sin(edge);
+        } else if (res == 2) {
+          c0 = c1 = 0.0;
+          c2 = 0.0;
+        }
+        if (P.u_safe) {
+          double* o = P.u_safe + ((size_t)b * n + v) * 3;
+          o[0] = c0; o[1] = c1; o[2] = c2;
+        }
+        if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 1;
+        ++mine;
+      }
+      __syncthreads();  // the batch's arrays are reused
+      k0 = k1;
+    }
+    const unsigned long long mm = __ballot(mine != 0u);
+    unsigned tot = mine;
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    if (lane == 0 && mm) atomicAdd(reinterpret_cast<unsigned*>(&misc[5]), tot);
+    __syncthreads();
+    if (tid == 0 && misc[5]) {
+      reinterpret_cast<unsigned*>(&P.status[b])[2] += (unsigned)misc[5] << 16;
+      P.status[b].flags |= (uint32_t)ACL_SWARM_CA_ACTIVE;
+    }
+    __syncthreads();  // q, cl and misc are rewritten for the next listed swarm
+  }
+}
+
 // acl_control_batch's hand-off: P must be a permutation (else BAD_INPUT and
 // zero commands, as for the auction's P_in); the inverse assignment is the
 // shared row the gain kernel reads.
@@ -987,6 +1370,15 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
 #undef ACL_GAIN
   } else {
     // a fixed grid striding over the device-side count of listed swarms
+    if (P.n <= kMaxN) {
+      const int lp = ca_pair_layout(P.n).total;
+      if (lp > 64 * 1024)
+        (void)hipFuncSetAttribute((const void*)ca_pair_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lp);
+      hipLaunchKernelGGL(ca_pair_kernel, dim3(nb < ACL_CA_GRID ? nb : ACL_CA_GRID), dim3(kCaPT), lp,
+                         stream, P);
+      return hipGetLastError();
+    }
     const int lds = ca_layout(P.n).total;
     if (lds > 64 * 1024)
       (void)hipFuncSetAttribute((const void*)ca_kernel,

@@ -33,7 +33,7 @@ def main(src, dst):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "")
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     txt = open(os.path.join(src, "out_1.txt")).read()
-    m = re.search(r"B=(\d+) n=(\d+): ([0-9.]+) ms", txt)
+    m = re.search(r"(?:auction-only|solve) B=(\d+) n=(\d+): ([0-9.]+) ms", txt)
     B, n, ms = int(m.group(1)), int(m.group(2)), float(m.group(3))
     out = {"source": "rocprofv3 --pmc (two passes of SQ counters, counters only) of "
                      "`python3 scripts/auction_only.py` (scripts/gpu_pmc_auction.sh)",
