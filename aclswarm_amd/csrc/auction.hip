@@ -426,6 +426,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   // not three): thread v < n (n <= kAB) holds P_in[v] and q[v] in registers
   // until the permutation check can run.
   const bool hv = tid < n;
+  bool pbad = false;  // a formation coordinate is not finite (phase 2's fast path)
   unsigned pvr = 0u;
   double qx = 0.0, qy = 0.0, qz = 0.0;
   if (hv) {
@@ -437,6 +438,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     const double* gp = P.p + (size_t)f * n * 3;
     for (int k = tid; k < 3 * n; k += kAB) {
       const double x = gp[k];
+      pbad |= !__builtin_isfinite(x);
       p[k] = x;
       const int j = k / 3, comp = k - 3 * j;
       if (comp < 2) pq[4 * j + comp] = x;  // pq[j] = {p_j.xy, qf_j.xy}
@@ -462,6 +464,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     if (fbad) misc[M_BAD] = 1;
     *margw = (unsigned long long)__double_as_longlong(1.0);
   }
+  if (__any(pbad) && lane == 0) misc[M_PINF] = 1;
   if (hv) {
     // the permutation check; q in formation order: qf[P_in[v]] = q[v]
     const int v = tid;
@@ -633,14 +636,28 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     const int per = kAB / n;
     const int j = tid % n, v0 = tid / n;
     const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
+    // The aligned point is Eigen's 3x3 [R 0; 0 1] times p plus [t; 0]. With
+    // every coordinate of p finite, the terms 0 * p are signed zeros: they
+    // can change only the sign of a zero component of the aligned point, and
+    // every component enters the price squared, so dropping them leaves the
+    // price bit-identical (a non-finite p keeps the full expression: 0 * inf
+    // is NaN).
+    const bool pfin = misc[M_PINF] == 0;  // workgroup-uniform
     for (int v = v0; v0 < per && v < n; v += per) {
       const int ip = Pin[v];
       const double* o = out + 6 * itm[ip];
       const double* qv = qf + 3 * ip;
-      const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
-      const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
-      const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
-      const double dx = qv[0] - ax, dy = qv[1] - ay, dz = qv[2] - az;
+      double dx, dy, dz;
+      if (pfin) {
+        dx = qv[0] - ((o[0] * px + o[1] * py) + o[4]);
+        dy = qv[1] - ((o[2] * px + o[3] * py) + o[5]);
+        dz = qv[2] - pz;
+      } else {
+        const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
+        const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
+        const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
+        dx = qv[0] - ax; dy = qv[1] - ay; dz = qv[2] - az;
+      }
       const float c = acl_price((dx * dx + dy * dy) + dz * dz);  // bit-exact, see common.h
       C[v * n + j] = c;
       nonfin |= (c != c);

@@ -178,11 +178,16 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   margin_init(mp);
   double galign = 1.0;
   wstamp(P, b, 0);
+  bool pbad = false;  // a formation coordinate is not finite (phase 2's fast path)
 
   // ---------------- phase 0: load -----------------------------------------
   {
     const double* gp = P.p + (size_t)f * n * 3;
-    for (int k = tid; k < 3 * n; k += kWBlock) p[k] = gp[k];
+    for (int k = tid; k < 3 * n; k += kWBlock) {
+      const double x = gp[k];
+      pbad |= !__builtin_isfinite(x);
+      p[k] = x;
+    }
     const uint64_t* ga = P.adj + (size_t)f * n * NW;
     for (int k = tid; k < n * NW; k += kWBlock) {
       unsigned long long x = ga[k];
@@ -200,6 +205,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     *reinterpret_cast<unsigned long long*>(misc + M_MARG) =
         (unsigned long long)__double_as_longlong(1.0);
   }
+  if (__any(pbad) && lane == 0) misc[M_PINF] = 1;
   unsigned long long* seenP = seen + kWWaves * NW;
   for (int v = tid; v < n; v += kWBlock) {
     const unsigned pv = P.P_in[(size_t)b * n + v];
@@ -360,6 +366,9 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   // each tile computed once, written row-major to C and, through LDS,
   // column-major to CT (both coalesced)
   int nonfin = 0;
+  // finite p: the 0 * p terms of the aligned point dropped (bit-identical
+  // prices, see auction.hip phase 2)
+  const bool pfin = misc[M_PINF] == 0;
   for (int tv = 0; tv < n; tv += 64) {
     for (int tj = 0; tj < n; tj += 64) {
       for (int e = tid; e < 64 * 64; e += kWBlock) {
@@ -369,10 +378,17 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           const double* o = out + 6 * v;
           const double* qv = qf + 3 * Pin[v];
           const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
-          const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
-          const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
-          const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
-          const double dx = qv[0] - ax, dy = qv[1] - ay, dz = qv[2] - az;
+          double dx, dy, dz;
+          if (pfin) {
+            dx = qv[0] - ((o[0] * px + o[1] * py) + o[4]);
+            dy = qv[1] - ((o[2] * px + o[3] * py) + o[5]);
+            dz = qv[2] - pz;
+          } else {
+            const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
+            const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
+            const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
+            dx = qv[0] - ax; dy = qv[1] - ay; dz = qv[2] - az;
+          }
           const float cpr = acl_price((dx * dx + dy * dy) + dz * dz);  // bit-exact (common.h)
           tile[vv * 65 + jj] = cpr;
           C[(size_t)v * n + j] = cpr;

@@ -34,6 +34,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tile-gains", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="also time the chunk of `steps` captured once as a HIP graph and "
+                         "replayed (the per-step launches without host launch overhead)")
+    ap.add_argument("--reps", type=int, default=3, help="graph replays timed")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     gen = torch.Generator(device=dev)
@@ -52,6 +56,33 @@ def main():
     e.run(args.steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    graph = None
+    if args.graph:
+        # the same chunk captured once on a side stream and replayed: each
+        # replay advances the state by `steps` control periods with the
+        # captured step numbering (auctions at the same offsets)
+        gs = torch.cuda.Stream()
+        gs.wait_stream(torch.cuda.current_stream())
+        eg = engine.Episode(T, w["fidx"], w["q"], w["vel"], w["P_in"])
+        with torch.cuda.stream(gs):
+            eg.run(args.steps, stream=gs.cuda_stream)  # eager chunk on the capture stream
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=gs):
+            eg.run(args.steps, stream=gs.cuda_stream)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(gs):
+            g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(gs):
+            for _ in range(args.reps):
+                g.replay()
+        torch.cuda.synchronize()
+        dg = (time.perf_counter() - t0) / args.reps
+        graph = {"value": args.B * args.steps / dg, "unit": "swarm-steps/s",
+                 "ms_per_step": dg / args.steps * 1e3, "replays": args.reps,
+                 "what": f"{args.steps} steps captured once as a HIP graph, replayed"}
     st = e.status()
     ep = e.ep
     line = {
@@ -62,6 +93,7 @@ def main():
         "auctions_per_swarm": int(st["n_auctions"][0] + st["n_skipped"][0]),
         "control_dt": ep.control_dt, "auction_every": ep.auction_every,
         "dtype": "f64", "data": "synthetic (simform_workload, C3 shape)",
+        "graph": graph,
         "episode": {"converged": int((st["converged_step"] >= 0).sum()),
                     "gridlocked": int((st["gridlock_step"] >= 0).sum()),
                     "invalid_auctions": int(st["n_invalid"].sum()),

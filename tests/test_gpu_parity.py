@@ -181,6 +181,45 @@ def test_full_rounds_equal_early_exit(cuda):
     _compare(g0, ref)
 
 
+@pytest.mark.parametrize("n", [12, 140])
+def test_price_signed_zeros_and_nonfinite_points(cuda, n):
+    """The price phase drops the 0 * p terms of the aligned point when every
+    formation coordinate is finite (signed zeros only, squared away): points
+    and positions with exact +-0.0 coordinates must give the oracle's tables
+    bit for bit; a formation with an infinite or NaN coordinate keeps the full
+    expression (0 * inf = NaN). n = 140 runs the wide kernel."""
+    rng = np.random.RandomState(n)
+    adj = (rng.rand(n, n) < 0.7).astype(np.uint8)
+    adj = np.triu(adj, 1)
+    adj = adj + adj.T
+    L = 4.5 * np.sqrt(n)  # (random_positions keeps a minimum spacing)
+    pz = H.random_positions(rng, n, L)
+    pz[: n // 2, 0] = 0.0
+    pz[n // 4: n // 2, 1] = -0.0
+    pz[::3, 2] = -0.0
+    pz[1::3, 2] = 0.0
+    p_inf = pz.copy()
+    p_inf[2, 2] = np.inf
+    p_nan = pz.copy()
+    p_nan[3, 0] = np.nan
+    pts = [pz, p_inf, p_nan]
+    adjs = [adj] * 3
+    gains = [H.synth_gains(rng, adj)] * 3
+    B = 9
+    fidx = np.arange(B) % 3
+    q = np.stack([pz.copy() if b < 3 else H.random_positions(rng, n, L) for b in range(B)])
+    q[3:6, : n // 3, 0] = -0.0
+    q[3:6, n // 3: n // 2, 2] = 0.0
+    vel = np.zeros((B, n, 3))
+    P_in = np.stack([np.arange(n, dtype=np.uint16) if b % 2 else H.random_perm(rng, n)
+                     for b in range(B)])
+    gpu = _gpu_solve(pts, adjs, gains, fidx, q, vel, P_in, do_control=False)
+    ref = _oracle(pts, adjs, gains, fidx, q, vel, P_in)
+    for r in ref:  # the oracle always runs the control stage; the GPU call did not
+        r["status"]["flags"] = int(r["status"]["flags"]) & ~0x20  # ACL_SWARM_CA_ACTIVE
+    _compare(gpu, ref, check_control=False)
+
+
 def test_collision_avoidance_dense(cuda):
     """Crowded swarms: many vehicles inside d_avoid_thresh, wrap-around
     sectors, surrounded vehicles (safety.cpp:412-541)."""
