@@ -13,6 +13,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "../../include/aclswarm_amd.h"
 #include "common.h"
 #include "control_params.h"
@@ -80,23 +82,31 @@ extern "C" int acl_internal_kernel_times(double* ms, int* count) {
 }
 
 namespace acl_amd {
-// acl_swarm_stats: one workgroup strides over the records (1 MB at B = 65536:
-// microseconds), LDS accumulators, then one thread writes every output.
-constexpr int kStatsThreads = 1024, kStatsHist = 64, kStatsKeys = 11;
+// acl_swarm_stats: up to kStatsGrid workgroups stride over the 16-byte
+// records (B = 65 536: 64 per thread with one workgroup was ~0.1 ms of
+// serial loads), LDS accumulators, then integer atomics into the output
+// words (exact, order-free); extrema as u32 bit patterns (emax, and the
+// complement of the smallest margin: non-negative floats order like their
+// bits), converted by the last workgroup to finish (a done counter).
+constexpr int kStatsThreads = 1024, kStatsHist = 64, kStatsKeys = 11, kStatsGrid = 64;
 __global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_status_t* st, int B,
                                                               long long* counters, double* ext) {
+  // the 16 bytes of ext serve as scratch until the last workgroup writes
+  // them: [0] emax, [1] ~(smallest margin bits) (0 = +inf), [2] workgroups done
+  unsigned* scratch = reinterpret_cast<unsigned*>(ext);
   __shared__ unsigned long long cnt[kStatsKeys + kStatsHist];
   __shared__ unsigned emax, mmin;
+  __shared__ bool last;
   const int tid = threadIdx.x;
   for (int k = tid; k < kStatsKeys + kStatsHist; k += kStatsThreads) cnt[k] = 0ull;
   if (tid == 0) {
     emax = 0u;
-    mmin = 0x7F800000u;  // +inf: margins are non-negative floats (bits order as values)
+    mmin = 0x7F800000u;  // +inf
   }
   __syncthreads();
   unsigned long long c[kStatsKeys] = {};
   unsigned em = 0u, mm = 0x7F800000u;
-  for (int b = tid; b < B; b += kStatsThreads) {
+  for (int b = blockIdx.x * kStatsThreads + tid; b < B; b += gridDim.x * kStatsThreads) {
     const acl_swarm_status_t s = st[b];
     c[0] += 1;
     const uint32_t bits[7] = {ACL_SWARM_VALID, ACL_SWARM_AGREE, ACL_SWARM_CHANGED,
@@ -120,10 +130,19 @@ __global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_st
   atomicMin(&mmin, mm);
   __syncthreads();
   for (int k = tid; k < kStatsKeys + kStatsHist; k += kStatsThreads)
-    counters[k] = (long long)cnt[k];
+    if (cnt[k]) atomicAdd(reinterpret_cast<unsigned long long*>(counters + k), cnt[k]);
   if (tid == 0) {
-    ext[0] = B > 0 ? (double)emax : 0.0;
-    ext[1] = B > 0 ? -(double)__uint_as_float(mmin) : -1.0;
+    atomicMax(&scratch[0], emax);
+    atomicMax(&scratch[1], ~mmin);
+    __threadfence();
+    last = atomicAdd(&scratch[2], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && tid == 0) {
+    __threadfence();
+    const unsigned e = atomicAdd(&scratch[0], 0u), m = ~atomicAdd(&scratch[1], 0u);
+    ext[0] = B > 0 ? (double)e : 0.0;
+    ext[1] = B > 0 ? -(double)__uint_as_float(m) : -1.0;
   }
 }
 }  // namespace acl_amd
@@ -135,7 +154,12 @@ extern "C" acl_status_t acl_swarm_stats(const acl_swarm_status_t* status, int32_
   if (B < 0) return acl__set_error("acl_swarm_stats: B < 0");
   if (!counters || !extrema || (B > 0 && !status))
     return acl__set_error("acl_swarm_stats: null argument");
-  hipLaunchKernelGGL(stats_kernel, dim3(1), dim3(kStatsThreads), 0, (hipStream_t)stream, status, B,
+  const hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(counters, 0, ACL_STATS_COUNTERS * sizeof(int64_t), s) != hipSuccess ||
+      hipMemsetAsync(extrema, 0, 2 * sizeof(double), s) != hipSuccess)
+    return acl__set_error("acl_swarm_stats: hipMemsetAsync failed");
+  const int grid = B > 0 ? std::min(kStatsGrid, (B + kStatsThreads - 1) / kStatsThreads) : 1;
+  hipLaunchKernelGGL(stats_kernel, dim3(grid), dim3(kStatsThreads), 0, s, status, B,
                      (long long*)counters, extrema);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));
