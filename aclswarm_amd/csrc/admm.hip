@@ -71,6 +71,7 @@ struct Part {
   double *r, *c;
   double *hb, *Pm, *T;
   double *W, *S, *Sr, *X, *N0, *N1, *Y;
+  double* cs;  // [2s] column sums of |W - eps I| (w_kernel), or NULL: norm_kernel reads W
   double *G, *Pre, *Pim;  // setup (alias W, Sr, Y)
   double *A1, *Ap;        // final (alias N0, N1)
   Scal* sc;
@@ -511,7 +512,7 @@ __global__ void __launch_bounds__(kT) init_kernel(const Part* parts) {
 }
 
 // W = sym(S + (I-P)(C - S - mu X) - mu x_b) (admm_oracle.Part.run)
-__global__ void __launch_bounds__(kT) w_kernel(const Part* parts, double mu) {
+__global__ void __launch_bounds__(kT) w_kernel(const Part* parts, double mu, double eps) {
   const Part& P = parts[blockIdx.y];
   if (!P.sc->active) return;
   const int s = P.s, n2 = 2 * s;
@@ -532,9 +533,18 @@ __global__ void __launch_bounds__(kT) w_kernel(const Part* parts, double mu) {
   // element for element (each is built from symmetric operands by the same
   // operations in the same order, or as 0.5 (a + b) of a transposed pair),
   // so sym(raw) = 0.5 (x + x) = x exactly -- no transposed (uncoalesced) reads
-  for (int e = blockIdx.x * kT + threadIdx.x; e < n2 * n2; e += gridDim.x * kT) {
-    const int i = e % n2, j = e / n2;
-    P.W[e] = raw(i, j);
+  // a wave per column (coalesced), which also leaves the column's sum of
+  // |W - eps I| for norm_kernel (no second pass over W)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int j = blockIdx.x * (kT / 64) + wv; j < n2; j += gridDim.x * (kT / 64)) {
+    double a = 0.0;
+    for (int i = lane; i < n2; i += 64) {
+      const double w = raw(i, j);
+      P.W[i + (size_t)j * n2] = w;
+      a += fabs(w - (i == j ? eps : 0.0));
+    }
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if (lane == 0) P.cs[j] = a;
   }
 }
 
@@ -552,8 +562,12 @@ __global__ void __launch_bounds__(kT) norm_kernel(const Part* parts, double eps)
   double mx = 0.0;
   for (int j = threadIdx.x; j < n2; j += kT) {
     double a = 0.0;
-    const double* col = P.W + (size_t)j * n2;
-    for (int i = 0; i < n2; ++i) a += fabs(col[i] - (i == j ? eps : 0.0));
+    if (P.cs) {  // left by w_kernel
+      a = P.cs[j];
+    } else {
+      const double* col = P.W + (size_t)j * n2;
+      for (int i = 0; i < n2; ++i) a += fabs(col[i] - (i == j ? eps : 0.0));
+    }
     mx = fmax(mx, a);
   }
   for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_down(mx, o, 64));
@@ -1067,6 +1081,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       offs.push_back(take(big));        // N0 / A1
       offs.push_back(take(big));        // N1 / Ap
       offs.push_back(take(big));        // Y / Pim
+      offs.push_back(take(n2));         // cs
     }
     const size_t nd_parts = off;
     const size_t scal_off = nd_parts * sizeof(double);
@@ -1081,13 +1096,14 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       P.Q = Qbuf + p * qstride;
       P.pa = pairbuf + p * pstride;
       P.pb = P.pa + 1;
-      const size_t* o = &offs[(size_t)p * 19];
+      const size_t* o = &offs[(size_t)p * 20];
       P.Qa = base + o[0]; P.Qb = base + o[1]; P.Qbc = base + o[2]; P.Yk = base + o[3];
       P.Gam = base + o[4]; P.Li = base + o[5]; P.Ginv = base + o[6];
       P.r = base + o[7]; P.c = base + o[8];
       P.hb = base + o[9]; P.Pm = base + o[10]; P.T = base + o[11];
       P.W = base + o[12]; P.S = base + o[13]; P.Sr = base + o[14]; P.X = base + o[15];
       P.N0 = base + o[16]; P.N1 = base + o[17]; P.Y = base + o[18];
+      P.cs = base + o[19];
       P.G = P.W; P.Pre = P.Sr; P.Pim = P.Y;
       P.A1 = P.N0; P.Ap = P.N1;
       P.sc = scal + p;
@@ -1157,6 +1173,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     ACL_HIP(gemm(J_PIM2, false, true), "gemm Pim");
     hipLaunchKernelGGL(gamma_kernel, dim3(grid1((long long)maxK1 * maxK1), NP), dim3(kT), 0, st, dp);
     hipLaunchKernelGGL(chol_kernel, dim3(NP), dim3(kT), 0, st, dp);
+    }
     ACL_HIP(gemm(J_GINV, true, false), "gemm Ginv");
     hipLaunchKernelGGL(rc_kernel, dim3(NP), dim3(kT), 0, st, dp, 0, prm.mu);
     ACL_HIP(gemm(J_T, true, false), "gemm T");
@@ -1169,7 +1186,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       ACL_HIP(gemm(J_YK, false, false), "gemm Yk");
       hipLaunchKernelGGL(rc_kernel, dim3(NP), dim3(kT), 0, st, dp, 1, mu);
       ACL_HIP(gemm(J_T, true, false), "gemm T");
-      hipLaunchKernelGGL(w_kernel, gW, dim3(kT), 0, st, dp, mu);
+      hipLaunchKernelGGL(w_kernel, dim3(cdiv(n2max, kT / 64), NP), dim3(kT), 0, st, dp, mu, eps);
       ACL_HIP(hipGetLastError(), "iteration kernels");
       ACL_HIP(psd_project(JL, dp, NP, n2max, eps, fuse_err, false, X, st), "PSD projection");
       hipLaunchKernelGGL(post_kernel, dim3(std::min(grid1((long long)n2max * n2max), 64), NP),
