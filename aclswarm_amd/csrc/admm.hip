@@ -1173,7 +1173,6 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     ACL_HIP(gemm(J_PIM2, false, true), "gemm Pim");
     hipLaunchKernelGGL(gamma_kernel, dim3(grid1((long long)maxK1 * maxK1), NP), dim3(kT), 0, st, dp);
     hipLaunchKernelGGL(chol_kernel, dim3(NP), dim3(kT), 0, st, dp);
-    }
     ACL_HIP(gemm(J_GINV, true, false), "gemm Ginv");
     hipLaunchKernelGGL(rc_kernel, dim3(NP), dim3(kT), 0, st, dp, 0, prm.mu);
     ACL_HIP(gemm(J_T, true, false), "gemm T");
