@@ -378,6 +378,196 @@ __device__ __forceinline__ void runner_up_walk(int n, const unsigned (&key)[NC],
   }
 }
 
+// ---- phase 1 as its own launch (align_kernel) --------------------------------
+// The alignment is a chain of ~2n dependent sums per work item, ~55 items per
+// swarm at C3: inside the auction workgroup it ran on one wave while the
+// swarm's other seven waited at the barrier, for a fifth of the swarm's life.
+// align_kernel gives each swarm one wave (LDS ~6 KB: many swarms per CU) and
+// leaves, per swarm, the work items' (R, t), the item of every formation row
+// and the smallest alignment gap in the workspace (WsLayout::align); the
+// auction kernel reads them back. The arithmetic is the same code in the
+// same order (bit-identical R, t).
+struct AlignLayout {
+  int pq, adjF, items, itm, Pin, seen, misc, total;
+};
+__host__ __device__ inline AlignLayout make_align_layout(int n) {
+  AlignLayout L;
+  int o = 0;
+  L.pq = o;    o = a16(o + (n + 8) * 32);  // {p.x, p.y, qf.x, qf.y} per point (padded)
+  L.adjF = o;  o = a16(o + n * 16);        // [n][2] formation rows (no diagonal)
+  L.items = o; o = a16(o + n);
+  L.itm = o;   o = a16(o + n);
+  L.Pin = o;   o = a16(o + n);
+  L.seen = o;  o = a16(o + 16);
+  L.misc = o;  o = a16(o + 16);
+  L.total = o;
+  return L;
+}
+
+// The alignment work list (one wave): formation rows with an incomplete
+// closed neighbourhood ascending, then one row standing for every complete
+// one; itm[i] = the item of row i. Returns the item count.
+template <int NC>
+__device__ __forceinline__ int align_worklist(int n, const unsigned long long* adjF,
+                                              unsigned char* items, unsigned char* itm, int lane) {
+  unsigned long long cm[NC], im[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = lane + 64 * c;
+    bool comp = false;
+    if (i < n) {
+      unsigned long long r0 = adjF[2 * i], r1 = adjF[2 * i + 1];
+      if (i < 64) r0 |= 1ull << i; else r1 |= 1ull << (i - 64);
+      comp = (__popcll(r0) + __popcll(r1)) == n;
+    }
+    cm[c] = __ballot(comp);
+    im[c] = __ballot(i < n && !comp);
+  }
+  int rep = -1;
+#pragma unroll
+  for (int c = NC - 1; c >= 0; --c)
+    if (cm[c]) rep = 64 * c + __ffsll((long long)cm[c]) - 1;
+  int ninc = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) ninc += __popcll(im[c]);
+  int base = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = lane + 64 * c;
+    const int rk = base + (int)__builtin_amdgcn_mbcnt_hi(
+                              (unsigned)(im[c] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im[c], 0u));
+    if (lanebit(im[c])) {
+      items[rk] = (unsigned char)i;
+      itm[i] = (unsigned char)rk;
+    } else if (lanebit(cm[c])) {
+      itm[i] = (unsigned char)ninc;
+    }
+    base += __popcll(im[c]);
+  }
+  if (rep >= 0 && lane == 0) items[ninc] = (unsigned char)rep;
+  return ninc + (rep >= 0 ? 1 : 0);
+}
+
+// Eigen::umeyama (3.3.x) for work items k0 + lane (one wave, one lane per
+// item): pass 1 rowwise sums of src (p) and dst (qf) over the members in
+// ascending order, pass 2 sigma = one_over_n * dst_demean * src_demean^T --
+// the lazy product (scaled lhs, from the first term) when k + 4 < 20, else
+// the GEMM form (0.0 + every term, alpha after). A sum starts at -0.0, the
+// identity of IEEE addition (x + -0.0 = x for every x), which is the
+// first-element start exactly. The members' values are broadcast loads; a
+// lane adds a term only for its members (exec-masked: asm keeps the compiler
+// from turning it into selects). (R, t) of item k to out[6k]; galign takes
+// the smallest decision gap.
+template <int NC>
+__device__ __forceinline__ void align_chunk(int n, const double* pq, const unsigned long long* adjF,
+                                            const unsigned char* items, int nitems, int k0,
+                                            int lane, double* out, double& galign) {
+  const int k = k0 + lane;
+  const bool act = k < nitems;
+  const int i = act ? items[k] : 0;
+  unsigned long long r[2] = {adjF[2 * i], adjF[2 * i + 1]};
+  if (i < 64) r[0] |= 1ull << i; else r[1] |= 1ull << (i - 64);
+  if (!act) r[0] = r[1] = 0ull;
+  const int cnt = __popcll(r[0]) + __popcll(r[1]);
+  double s0 = -0.0, s1 = -0.0, s2 = -0.0, s3 = -0.0;
+  for_members<NC>(n, pq, r, [&](unsigned long long mk, const double (&v)[4]) {
+    masked_add4(mk, s0, s1, s2, s3, v[0], v[1], v[2], v[3]);
+  });
+  const double oon = 1.0 / (double)(act ? cnt : 1);
+  const double sm0 = s0 * oon, sm1 = s1 * oon, dm0 = s2 * oon, dm1 = s3 * oon;
+  const bool lazy = (cnt + 4) < 20;
+  const double scale = lazy ? oon : 1.0;  // 1.0 * x == x
+  const double a0 = lazy ? -0.0 : 0.0;
+  double a00 = a0, a01 = a0, a10 = a0, a11 = a0;  // a(di, sj)
+  for_members<NC>(n, pq, r, [&](unsigned long long mk, const double (&v)[4]) {
+    const double e0 = v[0] - sm0, e1 = v[1] - sm1;
+    const double d0 = scale * (v[2] - dm0), d1 = scale * (v[3] - dm1);
+    masked_add4(mk, a00, a01, a10, a11, d0 * e0, d0 * e1, d1 * e0, d1 * e1);
+  });
+  if (act) {
+    // column-major sigma S(di, sj)
+    const double S[4] = {lazy ? a00 : a00 * oon, lazy ? a10 : a10 * oon,
+                         lazy ? a01 : a01 * oon, lazy ? a11 : a11 * oon};
+    const double sm[2] = {sm0, sm1}, dm[2] = {dm0, dm1};
+    double R[4], t[2], g;
+    umeyama_finish(S, sm, dm, R, t, &g);
+    galign = g < galign ? g : galign;
+    double* o = out + 6 * k;
+    o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
+  }
+}
+
+template <int NC>
+__global__ void __launch_bounds__(64) align_kernel(const SolveParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = P.n;
+  const AlignLayout L = make_align_layout(n);
+  const int b = P.b0 + blockIdx.x;
+  const int lane = threadIdx.x;
+  double* pq = reinterpret_cast<double*>(smem + L.pq);
+  unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
+  unsigned char* items = smem + L.items;
+  unsigned char* itm = smem + L.itm;
+  unsigned long long* seen = reinterpret_cast<unsigned long long*>(smem + L.seen);
+  int* misc = reinterpret_cast<int*>(smem + L.misc);
+  const int f_in = P.fidx[b];
+  if (f_in < 0 || f_in >= P.F) return;  // BAD_INPUT: the auction kernel reads nothing
+  const int f = f_in;
+  const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+  const double* gp = P.p + (size_t)f * n * 3;
+  const uint64_t* ga = P.adj + (size_t)f * n * NC;
+  if (lane < 2) seen[lane] = 0ull;
+  if (lane == 0) misc[0] = 0;
+  for (int k = lane; k < 4 * (n + 8); k += 64) pq[k] = 0.0;
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  for (int j = lane; j < n; j += 64) {
+    pq[4 * j] = gp[3 * j];
+    pq[4 * j + 1] = gp[3 * j + 1];
+  }
+  for (int k = lane; k < 2 * n; k += 64) {
+    const int i = k >> 1, w = k & 1;
+    unsigned long long x = 0ull;
+    if (w < NC) {
+      x = ga[(size_t)i * NC + w];
+      if (w == NC - 1) x &= lastmask;
+    }
+    adjF[k] = x;
+  }
+  // the permutation check and q in formation order: qf[P_in[v]] = q[v]
+  for (int v = lane; v < n; v += 64) {
+    const unsigned pv = P.P_in[(size_t)b * n + v];
+    if (pv >= (unsigned)n) {
+      misc[0] = 1;
+    } else {
+      const unsigned long long bit = 1ull << (pv & 63);
+      if (atomicOr(&seen[pv >> 6], bit) & bit) misc[0] = 1;
+      const double* qv = P.q + ((size_t)b * n + v) * 3;
+      pq[4 * pv + 2] = qv[0];
+      pq[4 * pv + 3] = qv[1];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  if (misc[0]) return;  // not a permutation: BAD_INPUT (wave-uniform)
+  const int nitems = align_worklist<NC>(n, adjF, items, itm, lane);
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  unsigned char* wsa = P.ws + P.W.align + (size_t)b * P.W.align_stride;
+  double* gout = reinterpret_cast<double*>(wsa);
+  double galign = 1.0;
+  for (int k0 = 0; k0 < nitems; k0 += 64) align_chunk<NC>(n, pq, adjF, items, nitems, k0, lane, gout, galign);
+  // the swarm's smallest alignment gap, the item of every row, the count
+  const unsigned long long gb =
+      ~wave_max_u64(~(unsigned long long)__double_as_longlong(galign));  // wave minimum
+  unsigned char* gitm = wsa + (size_t)n * 48;
+  for (int i = lane; i < n; i += 64) gitm[i] = itm[i];
+  if (lane == 0) {
+    *reinterpret_cast<unsigned long long*>(wsa + (size_t)n * 48 + a16(n)) = gb;
+    *reinterpret_cast<int*>(wsa + (size_t)n * 48 + a16(n) + 8) = nitems;
+  }
+}
+
 // FUSE: phase 5, the control law of a swarm whose vehicles all adopted one
 // assignment, runs in this workgroup right after its auction (see below);
 // GM: the fused phase also reports the gate margin.
@@ -393,6 +583,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
+  // n <= 64 (kAB <= 256): the alignment stays in this workgroup (an extra
+  // launch costs the launch-bound small configurations more than it saves)
+  constexpr bool kInlineAlign = kAB <= 256;
   float* C = reinterpret_cast<float*>(smem + L.C);
   double* pq = reinterpret_cast<double*>(smem + L.pq);
   unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
@@ -418,7 +611,6 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
   MarginPair mp;
   margin_init(mp);
-  double galign = 1.0;  // this lane's alignment gap (phase 1)
   stamp_phase(P, b, tid, 0);
 
   // ---------------- phase 0: load ------------------------------------------
@@ -441,7 +633,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       pbad |= !__builtin_isfinite(x);
       p[k] = x;
       const int j = k / 3, comp = k - 3 * j;
-      if (comp < 2) pq[4 * j + comp] = x;  // pq[j] = {p_j.xy, qf_j.xy}
+      if (kInlineAlign && comp < 2) pq[4 * j + comp] = x;  // pq[j] = {p_j.xy, qf_j.xy}
     }
     const uint64_t* ga = P.adj + (size_t)f * n * NC;
     for (int k = tid; k < 2 * n; k += kAB) {
@@ -477,7 +669,10 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       if (atomicOr(&H[8 + (pv >> 6)], bit) & bit) misc[M_BAD] = 1;  // not a permutation
       Ptin[pv] = (unsigned char)v;
       qf[3 * pv] = qx; qf[3 * pv + 1] = qy; qf[3 * pv + 2] = qz;
-      pq[4 * pv + 2] = qx; pq[4 * pv + 3] = qy;
+      if (kInlineAlign) {
+        pq[4 * pv + 2] = qx;
+        pq[4 * pv + 3] = qy;
+      }
     }
   }
   __syncthreads();
@@ -523,103 +718,33 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       if (NC == 1 && lane == 0) vadj[2 * v + 1] = 0ull;
     }
   }
-  // alignment work list (wave 0): incomplete rows ascending, then one row
-  // standing for every complete closed neighbourhood
-  if (wave == 0) {
-    unsigned long long cm[NC], im[NC];
-    int base = 0;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int i = lane + 64 * c;
-      bool comp = false;
-      if (i < n) {
-        unsigned long long r0 = adjF[2 * i], r1 = adjF[2 * i + 1];
-        if (i < 64) r0 |= 1ull << i; else r1 |= 1ull << (i - 64);
-        comp = (__popcll(r0) + __popcll(r1)) == n;
-      }
-      cm[c] = __ballot(comp);
-      im[c] = __ballot(i < n && !comp);
-    }
-    int rep = -1;
-#pragma unroll
-    for (int c = NC - 1; c >= 0; --c)
-      if (cm[c]) rep = 64 * c + __ffsll((long long)cm[c]) - 1;
-    int ninc = 0;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) ninc += __popcll(im[c]);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int i = lane + 64 * c;
-      const int rk = base + (int)__builtin_amdgcn_mbcnt_hi(
-                                (unsigned)(im[c] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im[c], 0u));
-      if (lanebit(im[c])) {
-        items[rk] = (unsigned char)i;
-        itm[i] = (unsigned char)rk;
-      } else if (lanebit(cm[c])) {
-        itm[i] = (unsigned char)ninc;
-      }
-      base += __popcll(im[c]);
-    }
-    if (lane == 0) {
-      if (rep >= 0) items[ninc] = (unsigned char)rep;
-      misc[A_NITEMS] = ninc + (rep >= 0 ? 1 : 0);
-    }
+  if (kInlineAlign && wave == 0) {
+    const int ni = align_worklist<NC>(n, adjF, items, itm, lane);
+    if (lane == 0) misc[A_NITEMS] = ni;
   }
   __syncthreads();
   stamp_phase(P, b, tid, 1);
   ACL_AUCTION_STOP_AT(1);
 
-  // ---------------- phase 1: alignment --------------------------------------
-  // Eigen::umeyama (3.3.x) per work item, one lane each: pass 1 rowwise sums
-  // of src (p) and dst (qf) over the members in ascending order, pass 2
-  // sigma = one_over_n * dst_demean * src_demean^T -- the lazy product
-  // (scaled lhs, from the first term) when k + 4 < 20, else the GEMM form
-  // (0.0 + every term, alpha after). A sum starts at -0.0, the identity of
-  // IEEE addition (x + -0.0 = x for every x), which is the first-element
-  // start exactly. The members' values are broadcast loads; a lane adds a
-  // term only for its members (exec-masked branch: asm barriers keep the
-  // compiler from turning it into selects).
-  {
+  // ---------------- phase 1: alignment (align_kernel's results) -------------
+  // Auctioneer::alignFormation per distinct neighbourhood (auctioneer.cpp:
+  // 347-415) ran in align_kernel: read back the items' (R, t), the item of
+  // every formation row and the swarm's smallest alignment gap
+  if constexpr (kInlineAlign) {
     const int nitems = misc[A_NITEMS];
-    if (wave * 64 < nitems) {
-      const int k = wave * 64 + lane;
-      const bool act = k < nitems;
-      const int i = act ? items[k] : 0;
-      unsigned long long r[2] = {adjF[2 * i], adjF[2 * i + 1]};
-      if (i < 64) r[0] |= 1ull << i; else r[1] |= 1ull << (i - 64);
-      if (!act) r[0] = r[1] = 0ull;
-      const int cnt = __popcll(r[0]) + __popcll(r[1]);
-      // pass 1: rowwise sums of src (p.xy) and dst (qf.xy)
-      double s0 = -0.0, s1 = -0.0, s2 = -0.0, s3 = -0.0;
-      for_members<NC>(n, pq, r, [&](unsigned long long mk, const double (&v)[4]) {
-        masked_add4(mk, s0, s1, s2, s3, v[0], v[1], v[2], v[3]);
-      });
-      const double oon = 1.0 / (double)(act ? cnt : 1);
-      const double sm0 = s0 * oon, sm1 = s1 * oon, dm0 = s2 * oon, dm1 = s3 * oon;
-      const bool lazy = (cnt + 4) < 20;
-      const double scale = lazy ? oon : 1.0;  // 1.0 * x == x
-      const double a0 = lazy ? -0.0 : 0.0;
-      double a00 = a0, a01 = a0, a10 = a0, a11 = a0;  // a(di, sj)
-      for_members<NC>(n, pq, r, [&](unsigned long long mk, const double (&v)[4]) {
-        const double e0 = v[0] - sm0, e1 = v[1] - sm1;
-        const double d0 = scale * (v[2] - dm0), d1 = scale * (v[3] - dm1);
-        masked_add4(mk, a00, a01, a10, a11, d0 * e0, d0 * e1, d1 * e0, d1 * e1);
-      });
-      if (act) {
-        // column-major sigma S(di, sj)
-        const double S[4] = {lazy ? a00 : a00 * oon, lazy ? a10 : a10 * oon,
-                             lazy ? a01 : a01 * oon, lazy ? a11 : a11 * oon};
-        const double sm[2] = {sm0, sm1}, dm[2] = {dm0, dm1};
-        double R[4], t[2], ga;
-        umeyama_finish(S, sm, dm, R, t, &ga);
-        galign = ga;
-        double* o = out + 6 * k;
-        o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
-      }
-    }
+    double galign = 1.0;
+    if (wave * 64 < nitems) align_chunk<NC>(n, pq, adjF, items, nitems, wave * 64, lane, out, galign);
     // the alignments' gaps go into the swarm margin now: the CBAA rounds
     // prune their margin work against it (below)
     block_min_gap(margw, galign);
+  } else {
+    const unsigned char* wsa = P.ws + P.W.align + (size_t)b * P.W.align_stride;
+    const int nitems = *reinterpret_cast<const int*>(wsa + (size_t)n * 48 + a16(n) + 8);
+    const double* gout = reinterpret_cast<const double*>(wsa);
+    for (int k = tid; k < 6 * nitems; k += kAB) out[k] = gout[k];
+    for (int i = tid; i < n; i += kAB) itm[i] = wsa[(size_t)n * 48 + i];
+    if (tid == 0)
+      atomicMin(margw, *reinterpret_cast<const unsigned long long*>(wsa + (size_t)n * 48 + a16(n)));
   }
   __syncthreads();
   stamp_phase(P, b, tid, 2);
@@ -1177,6 +1302,11 @@ static hipError_t launch_auction_t(const SolveParams& P, int nb, hipStream_t str
     return hipSuccess;
   });
   if (ea != hipSuccess) return ea;
+  // phase 1 (the alignment) as its own launch, one wave per swarm
+  // (n <= 64: inside the auction workgroup)
+  if (P.n > 64)
+    hipLaunchKernelGGL((align_kernel<2>), dim3(nb), dim3(64), make_align_layout(P.n).total, stream,
+                       P);
   const int lds = auction_lds(P.n, FUSE);
   // (64 threads for n <= 32 measured no faster at C2: 0.091 vs 0.088 ms)
   if (P.n <= 32)

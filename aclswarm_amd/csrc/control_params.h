@@ -51,8 +51,11 @@ constexpr int kMaxNWide = 512;  // tables-in-HBM auction kernel (solve_wide.hip)
 //                         by each control step's epilogue)
 //   wide    [B] x (C n*n f32, CT n*n f32, T n*n u16): the CBAA tables of
 //           the n > 128 kernel, which do not fit LDS
+//   align   [B] x (out [n][6] f64 the work items' R, t; itm [n] u8 the item of
+//           each formation row; u64 smallest alignment gap; i32 item count):
+//           align_kernel's results for the n <= 128 auction kernel
 struct WsLayout {
-  size_t pt, mode, rows, u, calist, cacount, camask, wide, wide_stride, total;
+  size_t pt, mode, rows, u, calist, cacount, camask, wide, wide_stride, align, align_stride, total;
 };
 
 __host__ __device__ inline size_t ws_al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -71,6 +74,10 @@ __host__ __device__ inline WsLayout ws_layout(int n, int B) {
   W.wide = o;
   W.wide_stride = n > kMaxN ? ws_al(nb * nb * (4 + 4 + 2)) : 0;
   o += bb * W.wide_stride;
+  o = ws_al(o);
+  W.align = o;
+  W.align_stride = n <= kMaxN ? ((nb * 48 + ((nb + 15) & ~(size_t)15) + 16 + 15) & ~(size_t)15) : 0;
+  o += bb * W.align_stride;
   W.total = o;
   return W;
 }

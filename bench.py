@@ -552,11 +552,14 @@ def main():
                         "acl_amd::auction_kernel<1, 256, false, false>" if n <= 64 else
                         "acl_amd::auction_kernel<2, 512, false, false>") if n <= 128
                        else "acl_amd::solve_wide_kernel")
-        gain_sym = ("acl_amd::gain_pair_kernel<false, false>" if w["planes"] == 5
+        # n > 128: the control law is the directed walk on 1 024-thread workgroups
+        gain_sym = ("acl_amd::gain_pair_kernel<false, false>" if w["planes"] == 5 and n <= 128
+                    else f"acl_amd::gain_kernel<{w['planes']}, false, 1024>" if n > 128
                     else f"acl_amd::gain_kernel<{w['planes']}, false>")
     kern = {}
     for k, (name, sym) in enumerate((("auction", auction_sym), ("gain", gain_sym),
-                                     ("ca", "acl_amd::ca_kernel"))):
+                                     ("ca", "acl_amd::ca_pair_kernel" if n <= 128
+                                      else "acl_amd::ca_kernel"))):
         avg = kms[k] / max(kcnt[k], 1)
         ach = per_launch[name] / (avg * 1e-3) / 1e9
         pm, src = (committed_profile("pmc_traffic", n, B, sym) if args.formations == 0
@@ -566,8 +569,10 @@ def main():
                       "frac": ach / HBM_PEAK_GBS,
                       "traffic": pm["hbm_bytes"] if pm else None, "traffic_source": src}
     if fused:
-        kern["auction"]["what"] = ("fused: alignment, CBAA, adoption, then DistCntrl + "
-                                   "saturation + the collision test in the same workgroup")
+        kern["auction"]["what"] = ("fused: CBAA, adoption, then DistCntrl + saturation + the "
+                                   "collision test in the same workgroup; for n > 64 the "
+                                   "alignment runs as its own launch just before "
+                                   "(acl_amd::align_kernel<2>), timed with it")
         kern["gain"]["what"] = "directed gain kernel for swarms with per-vehicle rows only"
     # the auction kernel is LDS/VALU/SALU-issue bound: its issue rates from the
     # committed SQ counters of the same configuration (scripts/gpu_pmc_auction.sh)
@@ -620,8 +625,8 @@ def main():
                       "(solver.cpp:49-77), 5-entry records = 40 B/edge" if w["planes"] == 5 else
                       "synthetic random 3x3 blocks, 9 planes = 72 B/edge"),
             "gain_layout": "row-major 40-byte records (no formation-setup re-layout)",
-            "kernels": ("one fused auction + control launch (+ the collision-avoidance "
-                        "launch over the listed vehicles)" if fused else
+            "kernels": ("the alignment launch (n > 64), one fused auction + control launch (+ "
+                        "the collision-avoidance launch over the listed vehicles)" if fused else
                         "auction launch, gain launch, collision-avoidance launch"),
         },
         "roofline": {
