@@ -591,6 +591,13 @@ def main():
     pipe_bytes = a_all + g_all + s_all
     pipe_ach = pipe_bytes / (call_ms * 1e-3) / 1e9
     tr = [kern[k]["traffic"] for k in (("auction",) if fused else ("auction", "gain"))]
+    if fused and n > 64:
+        # the alignment launch that precedes the fused one (its inputs and the
+        # workspace round trip of its results) is in the same timed window
+        am, _ = (committed_profile("pmc_traffic", n, B, "acl_amd::align_kernel<2>")
+                 if args.formations == 0 else (None, None))
+        tr.append(am["hbm_bytes"] if am else None)
+        kern["auction"]["traffic_align_kernel"] = am["hbm_bytes"] if am else None
     pipe_traffic = sum(tr) if all(x is not None for x in tr) else None
     pipe_traffic_src = kern["auction"]["traffic_source"] if pipe_traffic is not None else None
     gk = kern["auction" if fused else "gain"]
