@@ -2,15 +2,18 @@
 //
 // Same algorithm and exactness as solve.hip (alignment, prices, CBAA to the
 // fixed point, adoption; see that file and SURVEY.md App. A), re-laid out
-// for swarms whose CBAA tables do not fit LDS: at n = 500 the price matrix
-// is 1 MB and the `who` table 0.5 MB per swarm, so both live in the solve
-// workspace (HBM, L2-resident while the swarm's workgroup runs):
+// for swarms whose CBAA tables do not fit LDS. Only the `who` table lives in
+// the solve workspace (HBM; 0.5 MB per swarm at n = 500, so the resident
+// swarms' tables stay within the last-level cache):
 //
-//   C  [v][j] f32   row-major: a vehicle's select scans its row (coalesced)
-//   CT [j][v] f32   column-major copy: a column update gathers the prices
-//                   of the column's holders from one 2 KB row
 //   T  [j][u] u16   `who` table, column-major: a dirty-column update reads
 //                   and rewrites one contiguous column in place
+//
+// The price matrix (1 MB per swarm at n = 500) is not stored: a price is
+// recomputed from LDS where it is needed (wprice: vehicle v's alignment
+// applied to formation point j, the same f64 operations as the n <= 128
+// kernel's price phase, so every price is bit-identical). Recomputing costs
+// ~40 f64 operations; reading a stored price was a random HBM access.
 //
 // LDS keeps the per-swarm state every phase touches (~150 KB at n = 512):
 // points, alignments, the formation and vehicle-space neighbourhood
@@ -27,7 +30,8 @@
 
 namespace acl_amd {
 
-enum { W_RCH = 3 /* misc[3..4]: a column changed in a round of that parity */ };
+enum { W_RCH = 3 /* misc[3..4]: a column changed in a round of that parity */,
+       W_BIG = 12 /* a coordinate or alignment entry is not below 1e100 */ };
 
 constexpr int kWBlock = 1024;
 constexpr int kWWaves = kWBlock / 64;
@@ -35,7 +39,7 @@ constexpr int kWMaxW = kMaxNWide / 64;  // 64-bit words per bitmask row
 constexpr int kWLevels = 3;
 
 struct WLayout {
-  int p, qf, out, sums, adjF, vadj, Pin, Ptin, valid, masks, seen, misc, total;
+  int p, qf, out, sums, adjF, vadj, Pin, Ptin, ccw, ccp, valid, masks, seen, misc, total;
 };
 
 __host__ __device__ inline int wal(int x) { return (x + 15) & ~15; }
@@ -47,15 +51,13 @@ __host__ __device__ inline WLayout make_wlayout(int n) {
   L.p = o;     o = wal(o + n * 24);
   L.qf = o;    o = wal(o + n * 24);   // q in formation order
   L.out = o;   o = wal(o + n * 48);   // R, t per vehicle
-  L.sums = o;                          // alignment sums, then the price tile
-  {
-    const int a = n * 64, t = 64 * 65 * 4;
-    o = wal(o + (a > t ? a : t));
-  }
+  L.sums = o;  o = wal(o + n * 64);   // alignment sums, then q in vehicle order
   L.adjF = o;  o = wal(o + n * NW * 8);
   L.vadj = o;  o = wal(o + n * NW * 8);  // [word][vehicle]: conflict-free per-lane reads
   L.Pin = o;   o = wal(o + n * 2);
   L.Ptin = o;  o = wal(o + n * 2);
+  L.ccw = o;   o = wal(o + n * 2);    // column price cache: a holder of task j
+  L.ccp = o;   o = wal(o + n * 4);    // and its price for j
   L.valid = o; o = wal(o + n);
   L.masks = o; o = wal(o + 4 * NW * 8);                // dmask[2][NW], obm[2][NW]
   L.seen = o;  o = wal(o + (kWWaves + 1) * NW * 8);   // permutation checks
@@ -64,16 +66,53 @@ __host__ __device__ inline WLayout make_wlayout(int n) {
   return L;
 }
 
+// The price of task j for vehicle v (C[v][j] of the n <= 128 kernel, bit for
+// bit): v's alignment (R, t) = out[6 v..] applied to formation point j, the
+// squared distance to v's position qv[3 v..], then acl_price (common.h).
+// pfin: every formation coordinate is finite, so the 0 * p terms of the
+// aligned point drop (auction.hip phase 2).
+struct WPrice {
+  const double* out;
+  const double* qv;
+  const double* p;
+  bool pfin;
+  __device__ __forceinline__ float operator()(int v, int j) const {
+    const double* o = out + 6 * v;
+    const double* q = qv + 3 * v;
+    const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
+    double dx, dy, dz;
+    if (pfin) {
+      dx = q[0] - ((o[0] * px + o[1] * py) + o[4]);
+      dy = q[1] - ((o[2] * px + o[3] * py) + o[5]);
+      dz = q[2] - pz;
+    } else {
+      const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
+      const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
+      const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
+      dx = q[0] - ax; dy = q[1] - ay; dz = q[2] - az;
+    }
+    return acl_price((dx * dx + dy * dy) + dz * dz);
+  }
+};
+
 // selectTaskAssignment (auctioneer.cpp:517-542) on vehicle v's row: the
-// first task j maximizing C[v][j] among C[v][j] > 0 and C[v][j] > price_j.
+// first task j maximizing C[v][j] among C[v][j] > 0 and C[v][j] > price_j
+// (price_j = C[w][j] of the task's holder w in v's table).
 // `fresh`: the row is all `none` (the START bid). Tracks the margin of the
 // decisive comparisons (include/aclswarm_amd.h) in m.
-__device__ int wide_select(int n, int NW, int v, int lane, const float* C, const float* CT,
-                           const uint16_t* T, bool fresh, MarginPair& m) {
+__device__ int wide_select(int n, int NW, int v, int lane, const WPrice& price,
+                           const uint16_t* T, const uint16_t* ccw, const float* ccp, bool fresh,
+                           MarginPair& m) {
   unsigned key[kWMaxW];
   float cvs[kWMaxW], prs[kWMaxW];
   bool other[kWMaxW];
   unsigned lm = 0u;
+  int wv[kWMaxW];
+#pragma unroll
+  for (int c = 0; c < kWMaxW; ++c) {
+    const int j = lane + 64 * c;
+    wv[c] = (fresh || c >= NW || j >= n) ? n : T[(size_t)j * n + v];
+  }
 #pragma unroll
   for (int c = 0; c < kWMaxW; ++c) {
     key[c] = 0u;
@@ -82,9 +121,11 @@ __device__ int wide_select(int n, int NW, int v, int lane, const float* C, const
     other[c] = false;
     const int j = lane + 64 * c;
     if (c < NW && j < n) {
-      const float cv = C[(size_t)v * n + j];
-      const int w = fresh ? n : T[(size_t)j * n + v];
-      const float pr = w < n ? CT[(size_t)j * n + w] : 0.0f;
+      const float cv = price(v, j);
+      const int w = wv[c];
+      // the column price cache (ccw, ccp: one holder of task j and its
+      // price, a pure function of the pair) saves most holder prices
+      const float pr = w < n ? (w == ccw[j] ? ccp[j] : price(w, j)) : 0.0f;
       if (cv > 0.0f && cv > pr) key[c] = __float_as_uint(cv);
       cvs[c] = cv;
       prs[c] = pr;
@@ -152,11 +193,13 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   double* qf = reinterpret_cast<double*>(smem + L.qf);
   double* out = reinterpret_cast<double*>(smem + L.out);
   double* sums = reinterpret_cast<double*>(smem + L.sums);
-  float* tile = reinterpret_cast<float*>(smem + L.sums);
+  double* qv = reinterpret_cast<double*>(smem + L.sums);  // after phase 1
   unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
   unsigned long long* vadj = reinterpret_cast<unsigned long long*>(smem + L.vadj);
   uint16_t* Pin = reinterpret_cast<uint16_t*>(smem + L.Pin);
   uint16_t* Ptin = reinterpret_cast<uint16_t*>(smem + L.Ptin);
+  uint16_t* ccw = reinterpret_cast<uint16_t*>(smem + L.ccw);
+  float* ccp = reinterpret_cast<float*>(smem + L.ccp);
   unsigned char* validv = smem + L.valid;
   unsigned long long* dmask = reinterpret_cast<unsigned long long*>(smem + L.masks);
   unsigned long long* obm = dmask + 2 * NW;
@@ -164,9 +207,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   int* misc = reinterpret_cast<int*>(smem + L.misc);
 
   unsigned char* wsb = P.ws + P.W.wide + (size_t)b * P.W.wide_stride;
-  float* C = reinterpret_cast<float*>(wsb);
-  float* CT = C + (size_t)n * n;
-  uint16_t* T = reinterpret_cast<uint16_t*>(CT + (size_t)n * n);
+  uint16_t* T = reinterpret_cast<uint16_t*>(wsb);
 
   // a formation index out of range is a bad input like a bad P_in (nothing
   // of the formation table is read for it)
@@ -195,6 +236,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       adjF[k] = x;
     }
     for (int k = tid; k < 4 * NW; k += kWBlock) dmask[k] = 0ull;
+    for (int k = tid; k < n; k += kWBlock) ccw[k] = (uint16_t)n;
     for (int k = tid; k < (kWWaves + 1) * NW; k += kWBlock) seen[k] = 0ull;
     if (tid < 16) misc[tid] = 0;
   }
@@ -362,49 +404,33 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   if (P.align_Rt)
     for (int k = tid; k < 6 * n; k += kWBlock) P.align_Rt[(size_t)b * n * 6 + k] = out[k];
 
-  // ---------------- phase 2: prices, in 64 x 64 tiles -----------------------
-  // each tile computed once, written row-major to C and, through LDS,
-  // column-major to CT (both coalesced)
-  int nonfin = 0;
-  // finite p: the 0 * p terms of the aligned point dropped (bit-identical
-  // prices, see auction.hip phase 2)
-  const bool pfin = misc[M_PINF] == 0;
-  for (int tv = 0; tv < n; tv += 64) {
-    for (int tj = 0; tj < n; tj += 64) {
-      for (int e = tid; e < 64 * 64; e += kWBlock) {
-        const int vv = e >> 6, jj = e & 63;
-        const int v = tv + vv, j = tj + jj;
-        if (v < n && j < n) {
-          const double* o = out + 6 * v;
-          const double* qv = qf + 3 * Pin[v];
-          const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
-          double dx, dy, dz;
-          if (pfin) {
-            dx = qv[0] - ((o[0] * px + o[1] * py) + o[4]);
-            dy = qv[1] - ((o[2] * px + o[3] * py) + o[5]);
-            dz = qv[2] - pz;
-          } else {
-            const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
-            const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
-            const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
-            dx = qv[0] - ax; dy = qv[1] - ay; dz = qv[2] - az;
-          }
-          const float cpr = acl_price((dx * dx + dy * dy) + dz * dz);  // bit-exact (common.h)
-          tile[vv * 65 + jj] = cpr;
-          C[(size_t)v * n + j] = cpr;
-          nonfin |= (cpr != cpr);
-        }
+  // ---------------- phase 2: prices -----------------------------------------
+  // Not stored (see the header): q in vehicle order for wprice, and the
+  // NaN-price test. A price is NaN only if its squared distance is (acl_price
+  // is finite on [0, inf]); with every coordinate, rotation and translation
+  // entry finite and below 1e100 in magnitude no product overflows, so no
+  // distance is NaN. Otherwise every price is evaluated once.
+  for (int k = tid; k < 3 * n; k += kWBlock) {
+    const int v = k / 3, c = k - 3 * v;
+    qv[k] = qf[3 * Pin[v] + c];
+  }
+  __syncthreads();
+  const WPrice price{out, qv, p, misc[M_PINF] == 0};
+  {
+    bool big = false;
+    for (int k = tid; k < 6 * n; k += kWBlock) big |= !(fabs(out[k]) < 1e100);
+    for (int k = tid; k < 3 * n; k += kWBlock) big |= !(fabs(p[k]) < 1e100) || !(fabs(qv[k]) < 1e100);
+    if (__any(big) && lane == 0) misc[W_BIG] = 1;
+    __syncthreads();
+    if (misc[W_BIG]) {
+      int nonfin = 0;
+      for (int e = tid; e < n * n; e += kWBlock) {
+        const float c = price(e / n, e % n);
+        nonfin |= c != c;
       }
-      __syncthreads();
-      for (int e = tid; e < 64 * 64; e += kWBlock) {
-        const int jj = e >> 6, vv = e & 63;
-        const int v = tv + vv, j = tj + jj;
-        if (v < n && j < n) CT[(size_t)j * n + v] = tile[vv * 65 + jj];
-      }
-      __syncthreads();
+      if (__any(nonfin) && lane == 0) misc[M_NONFIN] = 1;
     }
   }
-  if (__any(nonfin) && lane == 0) misc[M_NONFIN] = 1;
   for (int k = tid; k < n * n; k += kWBlock) T[k] = (uint16_t)n;  // reset: all `none`
   __syncthreads();
   const bool nonfinite = misc[M_NONFIN] != 0;
@@ -412,7 +438,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
 
   // ---------------- phase 3: CBAA ------------------------------------------
   for (int v = wave; v < n; v += kWWaves) {
-    const int task = wide_select(n, NW, v, lane, C, CT, T, true, mp);
+    const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, true, mp);
     if (task >= 0 && lane == 0) {
       T[(size_t)task * n + v] = (uint16_t)v;
       atomicOr(&dmask[NW + (task >> 6)], 1ull << (task & 63));
@@ -422,6 +448,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   int eff = 0;
 #if ACL_WIDE_PROF
   unsigned long long pf_col = 0, pf_scan = 0, pf_sel = 0, pf_bar = 0, pf_cnt = 0, pf_rounds = 0;
+  unsigned long long pf_cload = 0, pf_clvl = 0, pf_cwb = 0;
 #endif
   unsigned obf = 0u;  // per-lane outbid bits (bit c: vehicle lane + 64 c), one round
   const int max_rounds = 2 * n;
@@ -437,7 +464,6 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         WPROF_T(pc0);
         WPROF_ADD(pf_cnt, 1ull);
         const uint16_t* Tc = T + (size_t)j * n;
-        const float* CTc = CT + (size_t)j * n;
         unsigned wu[kWMaxW], key[kWMaxW], nw[kWMaxW], k1[kWMaxW], k2[kWMaxW];
         // per vehicle: st 0 = undecided, 1 = winner level found (k1), 2 =
         // done (k2 = the next level its neighbourhood holds, 0 = none);
@@ -449,14 +475,45 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           const int u = lane + 64 * c;
           const bool ok = c < NW && u < n;
           wu[c] = ok ? Tc[u] : (unsigned)n;
-          key[c] = ok ? ((wu[c] < (unsigned)n ? __float_as_uint(CTc[wu[c]]) : 0u) + 1u) : 0u;
+          key[c] = ok ? 1u : 0u;  // + the holder's price bits below (1: none)
           nw[c] = (unsigned)n;
           k1[c] = k2[c] = 0u;
           st[c] = ok ? 0 : 2;
           need[c] = false;
         }
+        {
+          // entries of one holder share its price: one (lane-uniform) price
+          // per distinct holder, the first few holders; any further ones per
+          // entry
+          bool pend[kWMaxW];
+#pragma unroll
+          for (int c = 0; c < kWMaxW; ++c) pend[c] = wu[c] < (unsigned)n;
+          for (int it = 0; it < 4; ++it) {
+            int lw = -1;
+#pragma unroll
+            for (int c = 0; c < kWMaxW; ++c) {
+              const unsigned long long bl = __ballot(pend[c]);
+              if (lw < 0 && bl) lw = __builtin_amdgcn_readlane((int)wu[c], __ffsll((long long)bl) - 1);
+            }
+            if (lw < 0) break;
+            const unsigned kk = __float_as_uint(price(lw, j)) + 1u;
+#pragma unroll
+            for (int c = 0; c < kWMaxW; ++c)
+              if (pend[c] && wu[c] == (unsigned)lw) {
+                key[c] = kk;
+                pend[c] = false;
+              }
+          }
+#pragma unroll
+          for (int c = 0; c < kWMaxW; ++c)
+            if (pend[c]) key[c] = __float_as_uint(price((int)wu[c], j)) + 1u;
+        }
+        WPROF_T(pk);
+        WPROF_ADD(pf_cload, pk - pc0);
         unsigned cap = 0xFFFFFFFFu;
         bool exhausted = false;
+        int wk0 = -1;  // the top level's holder and key (the column price cache)
+        unsigned Mk0 = 0u;
         for (int k = 0; k < kWLevels + 1; ++k) {
           unsigned lm = 0u;
 #pragma unroll
@@ -480,25 +537,42 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
 #pragma unroll
           for (int c = 0; c < kWMaxW; ++c) tl |= key[c] == Mk && wu[c] != (unsigned)wk;
           const bool tk = nonfinite || __ballot(tl) != 0ull;
+          // hit: the vehicle's closed neighbourhood holds a vehicle of this
+          // level; holder-word outer loop, so the vehicle words' LDS loads
+          // issue together, stopping once every active vehicle is hit
+          bool act[kWMaxW], hit[kWMaxW];
+#pragma unroll
+          for (int c = 0; c < kWMaxW; ++c) {
+            act[c] = st[c] < 2 && !need[c];
+            hit[c] = false;
+          }
+#pragma unroll
+          for (int w2 = 0; w2 < kWMaxW; ++w2) {
+            if (!h[w2]) continue;
+            bool pendw = false;
+#pragma unroll
+            for (int c = 0; c < kWMaxW; ++c) pendw |= act[c] && !hit[c];
+            if (__ballot(pendw) == 0ull) break;
+#pragma unroll
+            for (int c = 0; c < kWMaxW; ++c)
+              if (act[c] && !hit[c]) hit[c] = (vadj[w2 * n + lane + 64 * c] & h[w2]) != 0ull;
+          }
+          if (k == 0 && wk >= 0 && wk < n) {
+            wk0 = wk;
+            Mk0 = Mk;
+          }
           bool open = false;
 #pragma unroll
           for (int c = 0; c < kWMaxW; ++c) {
-            if (st[c] < 2 && !need[c]) {
-              const int u = lane + 64 * c;
-              bool hit = false;
-#pragma unroll
-              for (int w2 = 0; w2 < kWMaxW; ++w2)
-                if (h[w2]) hit |= (vadj[w2 * n + u] & h[w2]) != 0ull;
-              if (hit) {
-                if (st[c] == 0) {
-                  nw[c] = (unsigned)wk;
-                  k1[c] = Mk;
-                  st[c] = 1;
-                  need[c] = tk;
-                } else {
-                  k2[c] = Mk;
-                  st[c] = 2;
-                }
+            if (act[c] && hit[c]) {
+              if (st[c] == 0) {
+                nw[c] = (unsigned)wk;
+                k1[c] = Mk;
+                st[c] = 1;
+                need[c] = tk;
+              } else {
+                k2[c] = Mk;
+                st[c] = 2;
               }
             }
             open |= st[c] < 2 && !need[c];
@@ -506,6 +580,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           if (__ballot(open) == 0ull) break;
           cap = Mk;
         }
+        WPROF_T(pl);
+        WPROF_ADD(pf_clvl, pl - pk);
         bool anyneed = false;
 #pragma unroll
         for (int c = 0; c < kWMaxW; ++c) {
@@ -534,7 +610,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
                   const int uu = 64 * w2 + __ffsll((long long)mm) - 1;
                   mm &= mm - 1;
                   const unsigned wx = Tc[uu];
-                  const float px = wx < (unsigned)n ? CTc[wx] : 0.0f;
+                  const float px = wx < (unsigned)n ? price((int)wx, j) : 0.0f;
                   if (first) {
                     bp = px; bw = wx; first = false;
                   } else if (px > bp) {
@@ -569,6 +645,10 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         // a column left holding one `who` everywhere is a fixed point with no
         // runner-up: not dirty next round unless a re-select writes it (as in
         // auction.hip); the change still counts for eff_rounds
+        if (wk0 >= 0 && lane == 0) {
+          ccw[j] = (uint16_t)wk0;
+          ccp[j] = __uint_as_float(Mk0 - 1u);
+        }
         const bool anych = __ballot(ch) != 0ull, anymx = __ballot(mx) != 0ull;
         if (anych && lane == 0) {
           misc[W_RCH + par] = 1;
@@ -576,6 +656,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         }
         WPROF_T(pc1);
         WPROF_ADD(pf_col, pc1 - pc0 - (ps1 - ps0));
+        WPROF_ADD(pf_cwb, pc1 - ps1);
       }
     }
 #pragma unroll
@@ -604,7 +685,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           if ((idx2++ % kWWaves) != wave) continue;
           WPROF_T(pr0);
           WPROF_ADD(pf_cnt, 1ull << 42);
-          const int task = wide_select(n, NW, v, lane, C, CT, T, false, mp);
+          const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, false, mp);
           if (task >= 0 && lane == 0) {
             T[(size_t)task * n + v] = (uint16_t)v;
             atomicOr(&dmask[npar * NW + (task >> 6)], 1ull << (task & 63));
@@ -635,6 +716,9 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     atomicAdd(ps + 10, pf_bar);
     atomicAdd(ps + 11, pf_cnt);
     if (wave == 0) ps[12] = pf_rounds;
+    atomicAdd(ps + 13, pf_cload);
+    atomicAdd(ps + 14, pf_clvl);
+    atomicAdd(ps + 15, pf_cwb);
   }
 #endif
 

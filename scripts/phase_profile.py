@@ -86,6 +86,8 @@ if args.n > 128 and sec[:, :4].any():
     print(f"  per swarm: columns {(cnt & m21).astype(float).mean():.1f}, exact scans "
           f"{((cnt >> np.uint64(21)) & m21).astype(float).mean():.1f}, re-selects "
           f"{(cnt >> np.uint64(42)).astype(float).mean():.1f}, rounds {sec[:, 5].astype(float).mean():.1f}")
+    for k, nm in enumerate(["T load + keys", "levels", "write-back"]):
+        print(f"    column {nm:14s} wave-cycles/swarm {sec[:, 6 + k].astype(np.float64).mean():12.0f}")
 # collision avoidance (a -DACL_CA_PROF=1 build, --crowd): ca_kernel wave-cycles
 if args.crowd:
     x = st.cpu().numpy()[:, 8:12].astype(np.float64)
