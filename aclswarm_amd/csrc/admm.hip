@@ -398,6 +398,79 @@ __global__ void __launch_bounds__(kT) chol_kernel(const Part* parts) {
   }
 }
 
+// chol_kernel with the factor in LDS as a packed lower triangle (column j,
+// rows j..K1-1, at pk(j) - j + i), for systems whose triangle fits
+// (chol_lds_bytes <= 160 KiB: K1 <= 198). Every element takes the same
+// operations in the same order as in chol_kernel (pivot test, scale, the
+// trailing updates in k order, the column-per-thread substitution), so L^-1
+// is bit-identical; only the factor's home moves from global memory, where
+// the trailing update was a chain of dependent round trips, to LDS. The
+// trailing update runs one column per wave, lanes over its rows.
+constexpr int kCholT = 512;
+inline size_t chol_lds_bytes(int K1) {
+  return ((size_t)K1 * (K1 + 1) / 2 + (size_t)K1) * sizeof(double) + (size_t)K1 + 16;
+}
+
+__global__ void __launch_bounds__(kCholT) chol_lds_kernel(const Part* parts) {
+  extern __shared__ double lsm[];
+  const Part& P = parts[blockIdx.x];
+  const int K1 = P.K + 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int kW = kCholT / 64;
+  double* Lp = lsm;
+  double* d0 = Lp + (size_t)K1 * (K1 + 1) / 2;
+  unsigned char* keep = reinterpret_cast<unsigned char*>(d0 + K1);
+  __shared__ int s_keep;
+  // column j of L: col(j)[i] = L[i, j], i >= j
+  auto col = [&](int j) { return Lp + ((size_t)j * K1 - (size_t)j * (j - 1) / 2) - j; };
+  for (int j = wave; j < K1; j += kW) {
+    const double* g = P.Gam + (size_t)j * K1;
+    double* c = col(j);
+    for (int i = j + lane; i < K1; i += 64) c[i] = g[i];
+  }
+  for (int k = tid; k < K1; k += kCholT) d0[k] = P.Gam[k + (size_t)k * K1];
+  __syncthreads();
+  for (int k = 0; k < K1; ++k) {
+    double* ck = col(k);
+    if (tid == 0) {
+      const double d = ck[k];
+      s_keep = d > 1e-10 * d0[k];
+      keep[k] = (unsigned char)s_keep;
+      if (s_keep) ck[k] = sqrt(d);
+    }
+    __syncthreads();
+    const bool kp = s_keep;
+    const double piv = ck[k];
+    for (int i = k + 1 + tid; i < K1; i += kCholT) {
+      double& x = ck[i];
+      x = kp ? x / piv : 0.0;
+    }
+    if (!kp && tid == 0) ck[k] = 0.0;
+    __syncthreads();
+    if (kp) {
+      for (int j = k + 1 + wave; j < K1; j += kW) {
+        const double ljk = ck[j];
+        if (ljk == 0.0) continue;
+        double* cj = col(j);
+        for (int i = j + lane; i < K1; i += 64) cj[i] -= ck[i] * ljk;
+      }
+    }
+    __syncthreads();
+  }
+  for (int c = tid; c < K1; c += kCholT) {
+    double* x = P.Gam + (size_t)c * K1;
+    for (int i = 0; i < K1; ++i) {
+      if (i < c || !keep[c] || !keep[i]) {
+        x[i] = 0.0;
+        continue;
+      }
+      double acc = (i == c) ? 1.0 : 0.0;
+      for (int m = c; m < i; ++m) acc -= col(m)[i] * x[m];
+      x[i] = acc / col(i)[i];
+    }
+  }
+}
+
 // P_struct of a 2m x 2m block: element (i, j) of the projection of M onto
 // [a b; -b a] blocks (ADMMGainDesign2D.m:221-265).
 template <typename F>
@@ -1172,7 +1245,16 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     ACL_HIP(gemm(J_PIM1, false, true), "gemm Pim");
     ACL_HIP(gemm(J_PIM2, false, true), "gemm Pim");
     hipLaunchKernelGGL(gamma_kernel, dim3(grid1((long long)maxK1 * maxK1), NP), dim3(kT), 0, st, dp);
-    hipLaunchKernelGGL(chol_kernel, dim3(NP), dim3(kT), 0, st, dp);
+    if (chol_lds_bytes(maxK1) <= 160 * 1024) {
+      const size_t cb = chol_lds_bytes(maxK1);
+      if (cb > 64 * 1024)
+        ACL_HIP(hipFuncSetAttribute((const void*)chol_lds_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)cb),
+                "hipFuncSetAttribute");
+      hipLaunchKernelGGL(chol_lds_kernel, dim3(NP), dim3(kCholT), cb, st, dp);
+    } else {
+      hipLaunchKernelGGL(chol_kernel, dim3(NP), dim3(kT), 0, st, dp);
+    }
     ACL_HIP(gemm(J_GINV, true, false), "gemm Ginv");
     hipLaunchKernelGGL(rc_kernel, dim3(NP), dim3(kT), 0, st, dp, 0, prm.mu);
     ACL_HIP(gemm(J_T, true, false), "gemm T");

@@ -49,7 +49,7 @@ constexpr int kMaxNWide = 512;  // tables-in-HBM auction kernel (solve_wide.hip)
 //   camask  [B][NW] u64   the swarm's vehicles within d_avoid_thresh of
 //                         another (bit v of word v/64; every word rewritten
 //                         by each control step's epilogue)
-//   wide    [B] x (T n*n u16): the CBAA `who` table of
+//   wide    [B] x (T u16 in 8 x 8 tiles, ceil(n/8)^2 * 64 entries): the CBAA `who` table of
 //           the n > 128 kernel, which does not fit LDS
 //   align   [B] x (out [n][6] f64 the work items' R, t; itm [n] u8 the item of
 //           each formation row; u64 smallest alignment gap; i32 item count):
@@ -72,7 +72,7 @@ __host__ __device__ inline WsLayout ws_layout(int n, int B) {
   W.cacount = o; o = ws_al(o + 16);
   W.camask = o;  o = ws_al(o + bb * (size_t)((n + 63) >> 6) * 8);
   W.wide = o;
-  W.wide_stride = n > kMaxN ? ws_al(nb * nb * 2) : 0;
+  W.wide_stride = n > kMaxN ? ws_al((size_t)((n + 7) >> 3) * ((n + 7) >> 3) * 64 * 2) : 0;
   o += bb * W.wide_stride;
   o = ws_al(o);
   W.align = o;

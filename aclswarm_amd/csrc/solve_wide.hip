@@ -6,8 +6,11 @@
 // the solve workspace (HBM; 0.5 MB per swarm at n = 500, so the resident
 // swarms' tables stay within the last-level cache):
 //
-//   T  [j][u] u16   `who` table, column-major: a dirty-column update reads
-//                   and rewrites one contiguous column in place
+//   T  [j][u] u16   `who` table in 8 x 8 tiles (one 128-byte line: tasks
+//                   j..j+7 x vehicles u..u+7, tix): a dirty-column update
+//                   reads and rewrites its column in place (8 lines per 64
+//                   vehicles), a re-select reads its vehicle's row (8 lines
+//                   per 64 tasks instead of 64 with a column-major table)
 //
 // The price matrix (1 MB per swarm at n = 500) is not stored: a price is
 // recomputed from LDS where it is needed (wprice: vehicle v's alignment
@@ -37,6 +40,16 @@ constexpr int kWBlock = 1024;
 constexpr int kWWaves = kWBlock / 64;
 constexpr int kWMaxW = kMaxNWide / 64;  // 64-bit words per bitmask row
 constexpr int kWLevels = 3;
+
+// index of entry (task j, vehicle u) of the tiled `who` table
+__host__ __device__ __forceinline__ size_t tix(int n, int j, int u) {
+  const int n8 = (n + 7) >> 3;
+  return (((size_t)(j >> 3) * n8 + (u >> 3)) << 6) + ((j & 7) << 3) + (u & 7);
+}
+__host__ __device__ __forceinline__ int tix_size(int n) {
+  const int n8 = (n + 7) >> 3;
+  return n8 * n8 * 64;
+}
 
 struct WLayout {
   int p, qf, out, sums, adjF, vadj, Pin, Ptin, ccw, ccp, valid, masks, seen, misc, total;
@@ -108,10 +121,14 @@ __device__ int wide_select(int n, int NW, int v, int lane, const WPrice& price,
   bool other[kWMaxW];
   unsigned lm = 0u;
   int wv[kWMaxW];
+  // row v of the tiled table: task j = lane + 64 c at Tv[lo + c * 512 n8]
+  const int n8 = (n + 7) >> 3;
+  const uint16_t* Tv = T + (((v >> 3) << 6) + (v & 7));
+  const int lo = (((lane >> 3) * n8) << 6) + ((lane & 7) << 3);
 #pragma unroll
   for (int c = 0; c < kWMaxW; ++c) {
     const int j = lane + 64 * c;
-    wv[c] = (fresh || c >= NW || j >= n) ? n : T[(size_t)j * n + v];
+    wv[c] = (fresh || c >= NW || j >= n) ? n : Tv[lo + c * (n8 << 9)];
   }
 #pragma unroll
   for (int c = 0; c < kWMaxW; ++c) {
@@ -431,7 +448,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       if (__any(nonfin) && lane == 0) misc[M_NONFIN] = 1;
     }
   }
-  for (int k = tid; k < n * n; k += kWBlock) T[k] = (uint16_t)n;  // reset: all `none`
+  for (int k = tid; k < tix_size(n); k += kWBlock) T[k] = (uint16_t)n;  // reset: all `none`
   __syncthreads();
   const bool nonfinite = misc[M_NONFIN] != 0;
   wstamp(P, b, 3);
@@ -440,7 +457,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   for (int v = wave; v < n; v += kWWaves) {
     const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, true, mp);
     if (task >= 0 && lane == 0) {
-      T[(size_t)task * n + v] = (uint16_t)v;
+      T[tix(n, task, v)] = (uint16_t)v;
       atomicOr(&dmask[NW + (task >> 6)], 1ull << (task & 63));
     }
   }
@@ -463,7 +480,9 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         if ((idx++ % kWWaves) != wave) continue;
         WPROF_T(pc0);
         WPROF_ADD(pf_cnt, 1ull);
-        const uint16_t* Tc = T + (size_t)j * n;
+        // column j of the tiled table: vehicle u = lane + 64 c at Tj[tlo + 512 c]
+        uint16_t* Tj = T + (((size_t)(j >> 3) * ((n + 7) >> 3)) << 6) + ((j & 7) << 3);
+        const int tlo = ((lane >> 3) << 6) + (lane & 7);
         unsigned wu[kWMaxW], key[kWMaxW], nw[kWMaxW], k1[kWMaxW], k2[kWMaxW];
         // per vehicle: st 0 = undecided, 1 = winner level found (k1), 2 =
         // done (k2 = the next level its neighbourhood holds, 0 = none);
@@ -474,7 +493,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         for (int c = 0; c < kWMaxW; ++c) {
           const int u = lane + 64 * c;
           const bool ok = c < NW && u < n;
-          wu[c] = ok ? Tc[u] : (unsigned)n;
+          wu[c] = ok ? Tj[tlo + (c << 9)] : (unsigned)n;
           key[c] = ok ? 1u : 0u;  // + the holder's price bits below (1: none)
           nw[c] = (unsigned)n;
           k1[c] = k2[c] = 0u;
@@ -609,7 +628,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
                 while (mm) {
                   const int uu = 64 * w2 + __ffsll((long long)mm) - 1;
                   mm &= mm - 1;
-                  const unsigned wx = Tc[uu];
+                  const unsigned wx = T[tix(n, j, uu)];
                   const float px = wx < (unsigned)n ? price((int)wx, j) : 0.0f;
                   if (first) {
                     bp = px; bw = wx; first = false;
@@ -636,7 +655,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         for (int c = 0; c < kWMaxW; ++c) {
           const int u = lane + 64 * c;
           const bool ok = c < NW && u < n;
-          if (ok) T[(size_t)j * n + u] = (uint16_t)nw[c];
+          if (ok) Tj[tlo + (c << 9)] = (uint16_t)nw[c];
           // outbid (:502): a per-lane bit, published once per wave and round
           obf |= (vflag(ok) & vflag(wu[c] == (unsigned)u) & vflag(nw[c] != (unsigned)u)) << c;
           ch |= nw[c] != wu[c];
@@ -687,7 +706,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           WPROF_ADD(pf_cnt, 1ull << 42);
           const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, false, mp);
           if (task >= 0 && lane == 0) {
-            T[(size_t)task * n + v] = (uint16_t)v;
+            T[tix(n, task, v)] = (uint16_t)v;
             atomicOr(&dmask[npar * NW + (task >> 6)], 1ull << (task & 63));
           }
           WPROF_T(pr1);
@@ -737,9 +756,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   {
     bool diff = false;
     for (int j = wave; j < n; j += kWWaves) {
-      const uint16_t* Tc = T + (size_t)j * n;
-      const uint16_t t0 = Tc[0];
-      for (int u = lane; u < n; u += 64) diff |= Tc[u] != t0;
+      const uint16_t t0 = T[tix(n, j, 0)];
+      for (int u = lane; u < n; u += 64) diff |= T[tix(n, j, u)] != t0;
     }
     if (__any(diff) && lane == 0) misc[M_AGREE] = 0;
   }
@@ -752,7 +770,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     if (tid < NW) sw[tid] = 0ull;
     __syncthreads();
     for (int j = tid; j < n; j += kWBlock) {
-      const int w = T[(size_t)j * n];
+      const int w = T[tix(n, j, 0)];
       if (w >= n) misc[M_NINV] = n;
       else atomicOr(&sw[w >> 6], 1ull << (w & 63));
     }
@@ -765,7 +783,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     __syncthreads();
     const bool valid0 = misc[M_NINV] == 0;
     for (int j = tid; j < n; j += kWBlock) {
-      const int v = valid0 ? T[(size_t)j * n] : Ptin[j];
+      const int v = valid0 ? T[tix(n, j, 0)] : Ptin[j];
       validv[v] = valid0;
       if (j != Pin[v]) misc[M_CHANGED] = 1;
       P.P_out[(size_t)b * n + v] = (uint16_t)j;
@@ -782,10 +800,10 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       const int jj = lane + 64 * c;
       bool ismine = false;
       if (jj < n) {
-        const int w = T[(size_t)jj * n + v];
+        const int w = T[tix(n, jj, v)];
         if (w >= n) bad = true;
         else atomicOr(&sw[w >> 6], 1ull << (w & 63));
-        diff |= w != T[(size_t)jj * n];
+        diff |= w != T[tix(n, jj, 0)];
         ismine = w == v;
       }
       const unsigned long long mm = __ballot(ismine);
@@ -811,7 +829,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   if (P.who) {
     for (int k = tid; k < n * n; k += kWBlock) {
       const int v = k / n, jj = k - v * n;
-      const int w = T[(size_t)jj * n + v];
+      const int w = T[tix(n, jj, v)];
       P.who[(size_t)b * n * n + k] = (w >= n) ? (uint16_t)0xFFFF : (uint16_t)w;
     }
   }
@@ -823,12 +841,12 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     uint16_t* wsPt = reinterpret_cast<uint16_t*>(P.ws + P.W.pt) + (size_t)b * n;
     if (tid == 0) P.ws[P.W.mode + b] = uniform ? 0 : 1;
     if (uniform) {
-      for (int jj = tid; jj < n; jj += kWBlock) wsPt[jj] = allvalid ? T[(size_t)jj * n] : Ptin[jj];
+      for (int jj = tid; jj < n; jj += kWBlock) wsPt[jj] = allvalid ? T[tix(n, jj, 0)] : Ptin[jj];
     } else {
       uint16_t* rows = reinterpret_cast<uint16_t*>(P.ws + P.W.rows) + (size_t)b * n * n;
       for (int k = tid; k < n * n; k += kWBlock) {
         const int v = k / n, jj = k - v * n;
-        rows[k] = validv[v] ? T[(size_t)jj * n + v] : Ptin[jj];
+        rows[k] = validv[v] ? T[tix(n, jj, v)] : Ptin[jj];
       }
     }
   }
