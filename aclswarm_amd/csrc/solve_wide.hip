@@ -329,25 +329,22 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     const int v = t >> 2, c = t & 3;
     const int i = Pin[v];
     const double* src = (c < 2) ? (p + c) : (qf + (c - 2));
-    double acc = 0.0;
-    bool first = true;
+    // the neighbours' sum in ascending order, branch-free: -0.0 is the exact
+    // identity of IEEE addition (-0 + x == x for every x, signed zeros
+    // included), so starting from it and adding -0.0 for a non-neighbour
+    // gives the bits of "first term, then acc + term"
+    double acc = -0.0;
     for (int w = 0; w < NW; ++w) {
       unsigned long long bits = adjF[i * NW + w];
       if (w == (i >> 6)) bits |= 1ull << (i & 63);
-      for (int jj = 0; jj < 64; jj += 4) {
-        double val[4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          const int j = 64 * w + jj + x;
-          val[x] = (j < n) ? src[3 * j] : 0.0;
-        }
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          const int j = 64 * w + jj + x;
-          if (j < n && ((bits >> (jj + x)) & 1ull)) {
-            acc = first ? val[x] : acc + val[x];
-            first = false;
-          }
+      if (w == NW - 1 && (n & 63)) bits &= (1ull << (n & 63)) - 1ull;
+      for (int hf = 0; hf < 2; ++hf) {
+        const unsigned h = (unsigned)(bits >> (32 * hf));
+#pragma unroll 8
+        for (int jb = 0; jb < 32; ++jb) {
+          const int j = 64 * w + 32 * hf + jb;
+          const double val = src[3 * (j < n ? j : 0)];
+          acc = acc + (((h >> jb) & 1u) ? val : -0.0);
         }
       }
     }
@@ -368,30 +365,24 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     const double smj = sums[8 * v + sj] * oon;
     const double dmi = sums[8 * v + 2 + di] * oon;
     const bool lazy = (k + 4) < 20;
-    double acc = 0.0;
-    bool first = true;
+    // lazy: the first product is the sum's first term (start from -0.0, the
+    // exact additive identity); otherwise the sum starts at +0.0 (0 + the
+    // first product); a non-neighbour adds -0.0 (no change, bit for bit)
+    double acc = lazy ? -0.0 : 0.0;
     for (int w = 0; w < NW; ++w) {
       unsigned long long bits = adjF[i * NW + w];
       if (w == (i >> 6)) bits |= 1ull << (i & 63);
-      for (int jj = 0; jj < 64; jj += 4) {
-        double sv[4], dv[4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          int j = 64 * w + jj + x;
+      if (w == NW - 1 && (n & 63)) bits &= (1ull << (n & 63)) - 1ull;
+      for (int hf = 0; hf < 2; ++hf) {
+        const unsigned h = (unsigned)(bits >> (32 * hf));
+#pragma unroll 8
+        for (int jb = 0; jb < 32; ++jb) {
+          int j = 64 * w + 32 * hf + jb;
           j = j < n ? j : 0;
-          sv[x] = p[3 * j + sj];
-          dv[x] = qf[3 * j + di];
-        }
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          const int j = 64 * w + jj + x;
-          const double s0 = sv[x] - smj;
-          double d0 = dv[x] - dmi;
+          const double s0 = p[3 * j + sj] - smj;
+          double d0 = qf[3 * j + di] - dmi;
           if (lazy) d0 = oon * d0;
-          if (j < n && ((bits >> (jj + x)) & 1ull)) {
-            acc = (lazy && first) ? d0 * s0 : acc + d0 * s0;
-            first = false;
-          }
+          acc = acc + (((h >> jb) & 1u) ? d0 * s0 : -0.0);
         }
       }
     }
