@@ -32,7 +32,7 @@
  * uint16_t; for N <= 255 the semantics are identical ("who == -1" casts to
  * 0xFFFF here instead of 0xFF). acl_solve_batch accepts N <= 512 (config
  * C4 is N = 500): N <= 128 runs the LDS-resident auction kernel, larger N
- * the kernel whose CBAA tables live in the workspace.
+ * the kernel whose CBAA `who` table lives in the workspace.
  *
  * Errors. The reference has no error channel (asserts compiled out in
  * Release, aclswarm/CMakeLists.txt:7-10); an invalid auction is a flag
