@@ -45,6 +45,7 @@
 #include "common.h"
 #include "control_dev.h"
 #include "control_params.h"
+#include "pair_fused.h"
 #include "umeyama_dev.h"
 
 namespace acl_amd {
@@ -56,9 +57,6 @@ namespace acl_amd {
 #define ACL_AUCTION_LEVELS 4   // price levels per dirty column before the exact scan
 #endif
 constexpr int kAL = ACL_AUCTION_LEVELS;
-#ifndef ACL_FUSED_PREFETCH
-#define ACL_FUSED_PREFETCH 2  // the fused control phase's record prefetch (control_dev.h)
-#endif
 
 __host__ __device__ inline int a16(int x) { return (x + 15) & ~15; }
 
@@ -1262,9 +1260,15 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     return;  // diagnostic builds: the fused kernel without its control phase
 #endif
     __syncthreads();       // T, C and the hand-off reads are done
-    const PairLayout GL = make_pair_layout(n, kAW, false);
+    const FusedLayout GL = make_fused_layout(n, kAW);
     if (tid < n) reinterpret_cast<uint16_t*>(smem + GL.Pt)[tid] = (uint16_t)ptv;
-    pair_gain_swarm<kAW, false, GM, ACL_FUSED_PREFETCH>(P.ctl, b, f, smem, tid, kAB, nullptr);
+    // P.ctl through the kernel-argument segment, loaded where it is used
+    // (pair_fused.h): P is this kernel's only argument, at offset 0
+    KCtlParams* pc = (KCtlParams*)((const __attribute__((address_space(4))) char*)
+                                       __builtin_amdgcn_kernarg_segment_ptr() +
+                                   offsetof(SolveParams, ctl));
+    asm volatile("" : "+s"(pc));
+    pair_gain_fused<kAW, GM>(pc, b, f, smem, tid, kAB);
     if (!ACL_AUCTION_PROF) stamp_phase(P, b, tid, 7);  // diagnostic: end of the control phase
   }
 }
@@ -1284,7 +1288,7 @@ static int auction_lds(int n, bool fuse) {
   const int a = make_alayout(n).total;
   if (!fuse) return a;
   const int kAW = n <= 32 ? 2 : (n <= 64 ? 4 : 8);
-  const int g = make_pair_layout(n, kAW, false).total;
+  const int g = make_fused_layout(n, kAW).total;
   return a > g ? a : g;
 }
 

@@ -110,6 +110,30 @@ __device__ __forceinline__ void gain_epilogue(const CtlParams& P, int b, int n, 
 // fl(min x / thr) = min fl(x / thr) -- two divisions per swarm, not per edge).
 #define ACL_GATE_WINDOW 1e-9
 template <bool GM>
+__device__ __forceinline__ void gate_decide_t(double txy, double tz, double win, double e_xy,
+                                              double e_z, double q0, double q1, double q2,
+                                              double Ni, double Nj, double Nzi, double Nzj,
+                                              double pix, double piy, double piz, double pjx,
+                                              double pjy, double pjz, bool& gxy, bool& gz,
+                                              double& mxy, double& mz) {
+  double axy = fabs(e_xy), az = fabs(e_z);
+  const double dxy = fabs(axy - txy), dz = fabs(az - tz);
+  if (dxy < win || dz < win) {
+#pragma clang fp contract(off)
+    const double xy = sqrt(q0 * q0 + q1 * q1) - sqrt((Ni + Nj) - 2.0 * (pix * pjx + piy * pjy));
+    const double zz = sqrt(q2 * q2) - sqrt((Nzi + Nzj) - 2.0 * (piz * pjz));
+    axy = fabs(xy);
+    az = fabs(zz);
+  }
+  gxy = axy > txy;
+  gz = az > tz;
+  if (GM) {
+    mxy = fmin(mxy, fabs(axy - txy));
+    mz = fmin(mz, fabs(az - tz));
+  }
+}
+
+template <bool GM>
 __device__ __forceinline__ void gate_decide(const acl_cntrl_gains_t& g, double e_xy, double e_z,
                                             double q0, double q1, double q2, double Ni, double Nj,
                                             double Nzi, double Nzj, double pix, double piy,
@@ -130,6 +154,25 @@ __device__ __forceinline__ void gate_decide(const acl_cntrl_gains_t& g, double e
     mxy = fmin(mxy, fabs(axy - g.e_xy_thr));
     mz = fmin(mz, fabs(az - g.e_z_thr));
   }
+}
+
+// The scale terms' errors of a pair (distcntrl.cpp:67-72): e_xy = |q.xy| -
+// dstar_xy, e_z = |q.z| - dstar_z, pdistmat's Gram-formula distances from
+// the formation points (utils.h:137-147). The contractions are written out
+// (explicit fma), so every kernel that evaluates pairs gets the same bits
+// (gate margins are compared exactly between them); s2 = |q.xy|^2.
+__device__ __forceinline__ void pair_e(double q0, double q1, double q2, double Ni, double Nj,
+                                       double Nzi, double Nzj, double pix, double piy, double piz,
+                                       double pjx, double pjy, double pjz, double s2,
+                                       double& e_xy, double& e_z) {
+  const double dxy = ACL_GAIN_SQRT(__builtin_fma(-2.0, __builtin_fma(pix, pjx, piy * pjy), Ni + Nj));
+  const double dz = ACL_GAIN_SQRT(__builtin_fma(-2.0, piz * pjz, Nzi + Nzj));
+  e_xy = ACL_GAIN_SQRT(s2) - dxy;
+  e_z = fabs(q2) - dz;
+}
+
+__device__ __forceinline__ double pair_s2(double q0, double q1) {
+  return __builtin_fma(q0, q0, q1 * q1);
 }
 
 __device__ __forceinline__ double gate_margin_of(const acl_cntrl_gains_t& g, double mxy, double mz) {
@@ -552,10 +595,9 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
         q2 = qf[3 * j + 2] - qf[3 * i + 2];
         const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
         const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
-        const double dxy = ACL_GAIN_SQRT((pn[2 * i] + pn[2 * j]) - 2.0 * (pix * pjx + piy * pjy));
-        const double dz = ACL_GAIN_SQRT((pn[2 * i + 1] + pn[2 * j + 1]) - 2.0 * (piz * pjz));
-        const double e_xy = ACL_GAIN_SQRT(q0 * q0 + q1 * q1) - dxy;
-        const double e_z = fabs(q2) - dz;
+        double e_xy, e_z;
+        pair_e(q0, q1, q2, pn[2 * i], pn[2 * j], pn[2 * i + 1], pn[2 * j + 1], pix, piy, piz, pjx,
+               pjy, pjz, pair_s2(q0, q1), e_xy, e_z);
         bool gxy, gz;
         gate_decide<GM>(g, e_xy, e_z, q0, q1, q2, pn[2 * i], pn[2 * j], pn[2 * i + 1],
                         pn[2 * j + 1], pix, piy, piz, pjx, pjy, pjz, gxy, gz, gmxy, gmz);

@@ -155,3 +155,40 @@ def test_psd_projection_near_eps(N):
     for k, W in enumerate(Ws):
         err = np.abs(S2[k] - _psd_ref(W, eps)).max()
         assert err <= (1e-9 if k == 1 else 1e-12), (k, err)
+
+
+def test_admm_c5_full_batch():
+    """Config C5 at its size: F = 1024 generator formations (n = 100,
+    L = 40, noncomplete; the bench's formations, seeds 0..1023) in one
+    acl_admm_solve_batch call, which runs them as two 512-formation chunks
+    (csrc/admm.hip) with the workspace reused between them. Every formation:
+    finite, symmetric, the trace identity of the reference's design (trace
+    of the gain matrix = -(2 (n - 2) + n - 2) for a 3-D formation), both
+    designs converged (positive iteration counts). Formations from both
+    chunks (0, 511, 512, 1023 and four random ones) against the CPU
+    restatement: gains within 1e-5 relative, equal iteration counts."""
+    import torch
+    from aclswarm_amd import engine, workload
+    dev = torch.device("cuda:0")
+    F, n = 1024, 100
+    pts, adjb = workload.reference_formations(F, n, 40.0, False, 0, dev)
+    A, its = engine.admm_design(pts, adjb.to(torch.float64))
+    torch.cuda.synchronize()
+    A = A.cpu().numpy()
+    its = its.cpu().numpy()
+    p = pts.cpu().numpy()
+    adj = adjb.cpu().numpy().astype(np.float64)
+    assert np.isfinite(A).all()
+    assert (its > 0).all(), np.argwhere(its <= 0)[:8]
+    sym = np.abs(A - A.transpose(0, 2, 1)).max(axis=(1, 2))
+    assert sym.max() < 1e-9, (int(sym.argmax()), sym.max())
+    flat = np.std(p[:, :, 2], axis=1, ddof=1) < 1e-2
+    want = -(2 * (n - 2) + n - np.where(flat, 1, 2))
+    tr = np.trace(A, axis1=1, axis2=2)
+    assert np.abs(tr - want).max() < 1e-6, np.abs(tr - want).max()
+    rng = np.random.RandomState(1024)
+    sample = [0, 511, 512, 1023] + list(rng.randint(1, 511, 2)) + list(rng.randint(513, 1023, 2))
+    for f in sample:
+        Ao, ito = O.design_3d(p[f], adj[f])
+        assert AC.rel_err(A[f], Ao) < REL_TOL, (f, AC.rel_err(A[f], Ao))
+        assert tuple(int(x) for x in its[f]) == tuple(ito), (f, its[f], ito)
