@@ -236,7 +236,8 @@ __device__ __forceinline__ bool lanebit(unsigned long long m) {
 // the who-table entry of lane-vehicle row `row`, task j, and its price key
 // (price bits + 1; `none` = row n of C has price 0 -> key 1)
 __device__ __forceinline__ unsigned entry_key(const float* C, int n, int w, int j) {
-  return __float_as_uint(C[w * n + j]) + 1u;
+  // (24-bit multiply: w, n <= 128; v_mul_lo_u32 is a quarter-rate instruction)
+  return __float_as_uint(C[__umul24(w, n) + j]) + 1u;
 }
 
 // selectTaskAssignment (auctioneer.cpp:517-542) for vehicle v as a wave
@@ -257,7 +258,7 @@ __device__ __forceinline__ int wave_select(int n, int TS, int v, int lane, const
     const int jj = ok ? j : 0;
     const int w = fresh ? n : T[v * TS + jj];
     cv[c] = C[v * n + jj];
-    pr[c] = C[w * n + jj];
+    pr[c] = C[__umul24(w, n) + jj];
     key[c] = (ok && cv[c] > 0.0f && cv[c] > pr[c]) ? __float_as_uint(cv[c]) : 0u;
     oth[c] = ok && w != v;
     lm = lm > key[c] ? lm : key[c];
@@ -1018,7 +1019,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
                   const int u = 64 * w2 + __ffsll((long long)m2) - 1;
                   m2 &= m2 - 1;
                   const int wx = T[u * TS + j];
-                  const float px = C[wx * n + j];
+                  const float px = C[__umul24(wx, n) + j];
                   if (first) {
                     bp = px; bw = wx; first = false;
                   } else if (px > bp) {
@@ -1133,9 +1134,11 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   // padding bytes of a row are `none` in every row)
   {
     const unsigned* T32 = reinterpret_cast<const unsigned*>(T);
-    const int rw = TS / 4;
+    const int rw = TS / 4;  // <= 32 dwords per row (n <= 128)
     bool diff = false;
-    for (int k = tid; k < n * rw; k += kAB) diff |= T32[k] != T32[k % rw];
+    // a wave per row, lanes over its dwords (no division by rw)
+    const unsigned r0 = lane < rw ? T32[lane] : 0u;
+    for (int v = wave; v < n; v += kAW) diff |= lane < rw && T32[v * rw + lane] != r0;
     if (__any(diff) && lane == 0) misc[M_AGREE] = 0;
   }
   __syncthreads();

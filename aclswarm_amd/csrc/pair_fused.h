@@ -121,9 +121,10 @@ __device__ __forceinline__ double col3_neg(double a, double b, double c3) {
   return qn + dpp_f64_all<0x128>(qn);
 }
 
-// a constant of the pair loop, read at its use (volatile: not hoisted)
+// a constant of the pair loop, read at its use (volatile: not hoisted; the
+// LDS address space spelled out, or a volatile access becomes a flat load)
 __device__ __forceinline__ double fcst(const double* cst, int k) {
-  return *reinterpret_cast<const volatile double*>(cst + k);
+  return *((const volatile __attribute__((address_space(3))) double*)(cst) + k);
 }
 
 // The control parameters in the kernel-argument segment (address space 4:
@@ -294,7 +295,7 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
     Rec5 X, Y;
     unsigned long long mx = 0ull, my = 0ull;
     if (t0 < t1) {
-      const unsigned xij = etab[(8 * I + r) * nb + J], xji = etab[(8 * J + c) * nb + I];
+      const unsigned xij = etab[__umul24(8 * I + r, nb) + J], xji = etab[__umul24(8 * J + c, nb) + I];
       mx = rec_mask(xij, c, I == J, kTileUpIncl);
       my = rec_mask(xji, r, I == J, kTileUpStrict);
       rec_load(xij, c, mx, X);
@@ -313,8 +314,8 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
       // the next tile's etab words, read early (their latency hides here)
       unsigned xijn = 0u, xjin = 0u;
       if (more) {
-        xijn = etab[(8 * In + r) * nb + Jn];
-        xjin = etab[(8 * Jn + c) * nb + In];
+        xijn = etab[__umul24(8 * In + r, nb) + Jn];
+        xjin = etab[__umul24(8 * Jn + c, nb) + In];
       }
       const int i = 8 * I + r, j = 8 * J + c;
       const double4* pi = reinterpret_cast<const double4*>(pt + 8 * i);
