@@ -180,11 +180,11 @@ __device__ __forceinline__ void stamp_phase(const SolveParams& P, int b, int tid
 enum { PS_L0, PS_LV, PS_MB, PS_WALK, PS_SCAN, PS_WB, PS_SEL, PS_BAR, PS_N };
 struct SecProf {
   unsigned long long acc[PS_N], last;
-  unsigned cols, walks, scans;
+  unsigned cols, walks, scans, sels, selx;
   __device__ void start() {
     if (ACL_AUCTION_PROF) {
       for (int k = 0; k < PS_N; ++k) acc[k] = 0;
-      cols = walks = scans = 0;
+      cols = walks = scans = sels = selx = 0;
       last = __builtin_amdgcn_s_memtime();
     }
   }
@@ -199,8 +199,9 @@ struct SecProf {
     if (ACL_AUCTION_PROF && P.stamps && lane == 0) {
       unsigned long long* s = P.stamps + (size_t)b * 16 + 7;
       for (int k = 0; k < PS_N; ++k) atomicAdd(s + k, acc[k]);
-      atomicAdd(s + PS_N, (unsigned long long)cols | ((unsigned long long)walks << 21) |
-                               ((unsigned long long)scans << 42));
+      atomicAdd(s + PS_N, (unsigned long long)cols | ((unsigned long long)walks << 12) |
+                              ((unsigned long long)scans << 24) |
+                              ((unsigned long long)sels << 36) | ((unsigned long long)selx << 48));
     }
   }
 };
@@ -210,6 +211,36 @@ struct SecProf {
 #ifndef ACL_AUCTION_NO_MARGIN
 #define ACL_AUCTION_NO_MARGIN 0
 #endif
+// diagnostic builds: -DACL_AUCTION_NO_SELMARGIN=1 skips the selects' margin
+// tracking, -DACL_AUCTION_NO_PUBLISH=1 the per-round publication of the
+// waves' gaps (cost measurements only; margins then wrong)
+#ifndef ACL_AUCTION_NO_SELMARGIN
+#define ACL_AUCTION_NO_SELMARGIN 0
+#endif
+#ifndef ACL_AUCTION_NO_PUBLISH
+#define ACL_AUCTION_NO_PUBLISH 0
+#endif
+
+// An upper bound of margin_gap(hi, lo) in f32 for the mid-auction
+// publications of the margin word (the walk bound's Gpub): (hi - lo) is exact
+// in f32 when lo >= hi / 2 (Sterbenz), the approximate reciprocal is padded
+// by 2^-20; otherwise the gap is above 1/2 and 1 bounds it. A published value
+// at least the exact gap of a tracked pair keeps every pruning decision
+// valid, and the exact gaps published at the end make the final minimum.
+__device__ __forceinline__ float gap_ub(float hi, float lo) {
+  const float g = (hi - lo) * __builtin_amdgcn_rcpf(hi) * (1.0f + 0x1p-20f);
+  return lo >= 0.5f * hi ? fminf(g, 1.0f) : 1.0f;
+}
+
+// publish a wave's upper-bounded smallest gap (lanes' pairs m, the wave's
+// uniform pair) into the margin word: one u32 wave minimum, one LDS atomic
+__device__ __forceinline__ void publish_gap_ub(unsigned long long* margw, const MarginPair& m,
+                                               float uhi, float ulo) {
+  const float g = fminf(gap_ub(m.hi, m.lo), gap_ub(uhi, ulo));
+  const unsigned w = ~wave_max_u32(~__float_as_uint(g));  // non-negative floats: bit order
+  if ((threadIdx.x & 63) == 0)
+    atomicMin(margw, (unsigned long long)__double_as_longlong((double)__uint_as_float(w)));
+}
 
 // margin_gap of a (hi, lo) pair (common.h margin_gap)
 __device__ __forceinline__ double margin_gap_pair(float hi, float lo) {
@@ -246,7 +277,8 @@ __device__ __forceinline__ unsigned entry_key(const float* C, int n, int w, int 
 // row. Returns the selected task (wave-uniform) or -1.
 template <int NC>
 __device__ __forceinline__ int wave_select(int n, int TS, int v, int lane, const float* C,
-                                           const unsigned char* T, bool fresh, MarginPair& m) {
+                                           const unsigned char* T, bool fresh, MarginPair& m,
+                                           unsigned* selx = nullptr) {
   unsigned key[NC];
   float cv[NC], pr[NC];
   bool oth[NC];
@@ -275,15 +307,21 @@ __device__ __forceinline__ int wave_select(int n, int TS, int v, int lane, const
   const float cmax = __uint_as_float(M);
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    // the selected task vs its price; an eligible task that lost vs the
-    // maximum; a task that would win if it became eligible vs its price
-    const int j = lane + 64 * c;
-    const bool isjs = oth[c] && j == js;
-    const bool elig = oth[c] && !isjs && key[c] != 0u;
-    const bool near = oth[c] && !isjs && key[c] == 0u && cv[c] > 0.0f &&
-                      (js < 0 || cv[c] > cmax || (cv[c] == cmax && j < js));
-    margin_track_sel(m, isjs ? cv[c] : (elig ? cmax : pr[c]), isjs ? pr[c] : cv[c],
-                     isjs || elig || near);
+    // the selected task vs its price (cv, pr); an eligible task that lost vs
+    // the maximum (cmax, cv); a task that would win if it became eligible vs
+    // its price (pr, cv). (A filter against the published gap -- every pair
+    // with a gap <= G has cmax - cv <= G cmax or |cv - pr| <= G max(cv, pr)
+    // -- passed 92% of the selects at C3: the selects' gaps set the margin.)
+    if (ACL_AUCTION_PROF && selx) ++*selx;
+    if (!ACL_AUCTION_NO_SELMARGIN) {
+      const int j = lane + 64 * c;
+      const bool isjs = oth[c] && j == js;
+      const bool elig = oth[c] && !isjs && key[c] != 0u;
+      const bool near = oth[c] && !isjs && key[c] == 0u && cv[c] > 0.0f &&
+                        (js < 0 || cv[c] > cmax || (cv[c] == cmax && j < js));
+      margin_track_sel(m, isjs ? cv[c] : (elig ? cmax : pr[c]), isjs ? pr[c] : cv[c],
+                       isjs || elig || near);
+    }
   }
   return js;
 }
@@ -820,6 +858,8 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       atomicOr(&dmask[2 + (task >> 6)], 1ull << (task & 63));
     }
   }
+  // the START selects' gaps, published for round 1's walk bound
+  if (!ACL_AUCTION_NO_PUBLISH) publish_gap_ub(margw, mp, 1.0f, 0.0f);
   __syncthreads();
   ACL_AUCTION_STOP_AT(4);
 
@@ -852,6 +892,12 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     // bounded below by it cannot lower the margin, so its runner-up walk is
     // skipped (margin_gap is monotone in the pair's ratio)
     const double Gpub = __longlong_as_double((long long)*margw);
+    // the walk bound: a column's exact runner-up walk can lower the margin
+    // only if some resolving level's successor is within Gw of it, Gw = min
+    // (the published gap, the wave's own running gap); Gwf its float bound
+    // for the conservative f32 tests (at least Gw (1 + 2^-20)), refreshed after walks
+    double Gw = fmin(Gpub, margin_gap_pair(uhi, ulo));
+    float Gwf = (float)(Gw * (1.0 + 0x1p-20));
     // this wave's dirty columns: every 8th set bit in rank order
     unsigned long long mine[NC];
     {
@@ -926,7 +972,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           k1[c] = 0u;
         }
         unsigned Mk = M0, kres = 0u;  // kres: the last level that resolved a vehicle
-        float bhi = 1.0f, blo = 0.0f;  // bound pair (largest ratio)
+        // the runner-up walk is needed: a resolving level's successor within
+        // Gw (its vehicles' decision gaps are at least that level pair's)
+        bool walk = false;
         if (nonfinite) {  // NaN prices: the exact scan for every vehicle
 #pragma unroll
           for (int c = 0; c < NC; ++c) {
@@ -964,9 +1012,12 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
             if (!left || ++k == kAL) break;
             // the next level
             Mk = level_key<NC>(key, Mk);
-            if (!ACL_AUCTION_NO_MARGIN)
-              margin_track_u(bhi, blo, __uint_as_float(kres - 1u), __uint_as_float(Mk - 1u));
-            // (kres == 0: a NaN pair, no effect; Mk == 0: lo = NaN, no effect)
+            if (!ACL_AUCTION_NO_MARGIN) {
+              // gap(P(kres), P(Mk)) <= Gw, tested conservatively in f32
+              // (kres == 0: a NaN pair, no effect; Mk == 0: lo = NaN, no effect)
+              const float hk = __uint_as_float(kres - 1u), lk = __uint_as_float(Mk - 1u);
+              walk |= hk - lk <= Gwf * hk;
+            }
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
               h[c] = __ballot(key[c] == Mk);
@@ -979,19 +1030,27 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           }
         }
         sp.mark(PS_LV);
-        if (!ACL_AUCTION_NO_MARGIN && kres != 0u && cum < n) {  // the resolving level's successor
-          const unsigned Mn = level_key<NC>(key, kres);
-          margin_track_u(bhi, blo, __uint_as_float(kres - 1u), __uint_as_float(Mn - 1u));
+        if (!ACL_AUCTION_NO_MARGIN && !walk && kres != 0u && cum < n) {
+          // the last resolving level's successor (the highest key below
+          // kres) within Gw: an entry with a key in [low, kres), low the key
+          // of P(kres) (1 - Gw (1 + 2^-20)) rounded down (f64, then one f32
+          // ulp lower), so no successor within Gw is missed
+          const double lowd = (double)__uint_as_float(kres - 1u) * (1.0 - Gw * (1.0 + 0x1p-20));
+          const unsigned lowk = lowd > 0.0 ? __float_as_uint((float)lowd) : 1u;  // bits - 1 + 1
+          unsigned long long any = 0ull;
+#pragma unroll
+          for (int c = 0; c < NC; ++c) any |= __ballot(key[c] >= lowk && key[c] < kres);
+          walk = any != 0ull;
         }
-        // the exact runner-ups only where the bound could lower the wave's
-        // running minimum (an evaluation skipped here has a gap >= the bound
-        // >= a gap already tracked, so the minimum is unchanged)
-        const bool walk = !ACL_AUCTION_NO_MARGIN &&
-                          (double)blo * (double)uhi > (double)ulo * (double)bhi &&
-                          margin_gap_pair(bhi, blo) < Gpub;
+        // the exact runner-ups only where a level pair could lower the
+        // wave's running minimum or the published one (an evaluation skipped
+        // here has gaps >= its level pairs' > Gw, so the minimum is unchanged)
+        walk = walk && !ACL_AUCTION_NO_MARGIN;
         sp.mark(PS_MB);
         if (walk) {
           runner_up_walk<NC>(n, key, k1, Nd, vm, uhi, ulo);
+          Gw = fmin(Gpub, margin_gap_pair(uhi, ulo));
+          Gwf = (float)(Gw * (1.0 + 0x1p-20));
           if (ACL_AUCTION_PROF) sp.walks++;
           sp.mark(PS_WALK);
         }
@@ -1066,11 +1125,11 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       const unsigned long long ob = __ballot((fl >> c) & 1u);
       if (ob && lane == 0) atomicOr(&obm[2 * par + c], ob);
     }
-    {
+    if (!ACL_AUCTION_NO_PUBLISH) {
       // publish this wave's smallest gap so far (its lanes' select and scan
-      // evaluations, its level pair) for the next round's pruning
-      const double gl = margin_gap(mp), gu = margin_gap_pair(uhi, ulo);
-      block_min_gap(margw, gl < gu ? gl : gu);
+      // evaluations, its walks' pair) for the next round's pruning: an upper
+      // bound is enough there (gap_ub)
+      publish_gap_ub(margw, mp, uhi, ulo);
     }
     sp.mark(PS_WB);
     __syncthreads();
@@ -1095,7 +1154,8 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         while (mv) {
           const int v = 64 * c + __ffsll((long long)mv) - 1;
           mv &= mv - 1;
-          const int task = wave_select<NC>(n, TS, v, lane, C, T, false, mp);
+          const int task = wave_select<NC>(n, TS, v, lane, C, T, false, mp, &sp.selx);
+          if (ACL_AUCTION_PROF) sp.sels++;
           smem[(task >= 0 && lane == 0) ? L.T + v * TS + task : L.dummy + lane] = (unsigned char)v;
           fl |= (vflag(task >= 0) & vflag(lane == (task & 63))) << (FL_DIRTY + (task >> 6));
         }

@@ -297,6 +297,73 @@ __device__ __forceinline__ double acl_atan_k32(double x, const double* tab) {
   return (ax == __builtin_inf()) ? copysign(1.57079632679489655800e+00, x) : copysign(res, x);
 }
 
+// Rows k = 0..33 of {na, nb, da, db, a_k} for acl_atan_b: row 0 (|x| <
+// 2^-4) is atan itself (c = 0); rows 1..32 split [2^-4, 2^4) into binades of
+// four linear steps, c_k = tan of the midpoint of the step's atan range
+// (a_k = atan(c_k)), t = (|x| - c_k) / (1 + c_k |x|); row 33 (|x| >= 16):
+// t = -1 / |x|, a = pi / 2. |t| <= 0.0625 everywhere. Callers stage it in LDS.
+__device__ constexpr double kAtanBTab[34][5] = {
+    {1.0, 0.0, 0.0, 1.0, 0.0},
+    {1.0, -0.07030822983596466, 0.07030822983596466, 1.0, 0.07019272191374983},
+    {1.0, -0.08593229355760532, 0.08593229355760532, 1.0, 0.08572170749506589},
+    {1.0, -0.10155636477210132, 0.10155636477210132, 1.0, 0.10120936907422763},
+    {1.0, -0.11718044475643763, 0.11718044475643763, 1.0, 0.11664847576831361},
+    {1.0, -0.14059134139479385, 0.14059134139479385, 1.0, 0.13967586823535122},
+    {1.0, -0.1718342517380426, 0.1718342517380426, 1.0, 0.17017234595981787},
+    {1.0, -0.20307738469612643, 0.20307738469612643, 1.0, 0.2003528248467164},
+    {1.0, -0.2343207709802973, 0.2343207709802973, 1.0, 0.2301681814123011},
+    {1.0, -0.28099568840305256, 0.28099568840305256, 1.0, 0.27393176575091777},
+    {1.0, -0.34345001598898495, 0.34345001598898495, 1.0, 0.3308277693227718},
+    {1.0, -0.40590971677575227, 0.40590971677575227, 1.0, 0.3855905559339798},
+    {1.0, -0.4683749459844424, 0.4683749459844424, 1.0, 0.4380290252990967},
+    {1.0, -0.560834617207166, 0.560834617207166, 1.0, 0.5111234621721843},
+    {1.0, -0.6856796740973412, 0.6856796740973412, 1.0, 0.6010502120684234},
+    {1.0, -0.8105909435321778, 0.8105909435321778, 1.0, 0.6811655542074544},
+    {1.0, -0.9355530918915272, 0.9355530918915272, 1.0, 0.7521140815095364},
+    {1.0, -1.1172650153486017, 1.1172650153486017, 1.0, 0.8407267739843961},
+    {1.0, -1.3675814891468359, 1.3675814891468359, 1.0, 0.9394245539093364},
+    {1.0, -1.618033988749895, 1.618033988749895, 1.0, 1.0172219678978514},
+    {1.0, -1.8685170918213303, 1.8685170918213303, 1.0, 1.0793994651712322},
+    {1.0, -2.2268438420880323, 2.2268438420880323, 1.0, 1.148719333738311},
+    {1.0, -2.729944215084218, 2.729944215084218, 1.0, 1.219667861040393},
+    {1.0, -3.232440682034051, 3.232440682034051, 1.0, 1.2707712200940198},
+    {1.0, -3.734444135973819, 3.734444135973819, 1.0, 1.309157165728909},
+    {1.0, -4.44708844906985, 4.44708844906985, 1.0, 1.3496092153065242},
+    {1.0, -5.4560113489583335, 5.4560113489583335, 1.0, 1.3895242081626429},
+    {1.0, -6.462432795016398, 6.462432795016398, 1.0, 1.4172734607855013},
+    {1.0, -7.467251416997126, 7.467251416997126, 1.0, 1.437670302219434},
+    {1.0, -8.890260421989915, 8.890260421989915, 1.0, 1.4587845032759348},
+    {1.0, -10.909842172583009, 10.909842172583009, 1.0, 1.479391384605095},
+    {1.0, -12.923532073277041, 12.923532073277041, 1.0, 1.4935719784580308},
+    {1.0, -14.93362962377707, 14.93362962377707, 1.0, 1.5039331894042727},
+    {0.0, -1.0, 1.0, 0.0, 1.5707963267948966},
+};
+
+// atan for the control law's gated terms (parity bar 1e-5 relative on u):
+// the row is picked by the float bits of |x| -- exponent and the top two
+// mantissa bits, (bits >> 21) - (123 << 2) + 1 clamped to [0, 33], four
+// integer instructions -- and atan(t) = t + t z (-1/3 + z/5 - z^2/7 + z^3/9
+// - z^4/11), z = t^2, is within 4e-16 relative on |t| <= 0.0625
+// (tests/test_fastmath.py). One reciprocal with one Newton step.
+__device__ __forceinline__ double acl_atan_b(double x, const double* tab) {
+  const double ax = fabs(x);
+  int k = (int)(__float_as_uint((float)ax) >> 21) - (123 << 2) + 1;
+  k = k < 0 ? 0 : (k > 33 ? 33 : k);
+  const double* rw = tab + 5 * k;
+  const double num = __builtin_fma(rw[0], ax, rw[1]);
+  const double den = __builtin_fma(rw[2], ax, rw[3]);
+  double r = __builtin_amdgcn_rcp(den);
+  r = __builtin_fma(__builtin_fma(-den, r, 1.0), r, r);
+  const double t = num * r;
+  const double z = t * t;
+  double p = ACL_MUL_ADD_K(z, -1.0 / 11.0, 1.0 / 9.0);
+  p = ACL_FMA_K(z, p, -1.0 / 7.0);
+  p = ACL_FMA_K(z, p, 1.0 / 5.0);
+  p = ACL_FMA_K(z, p, -1.0 / 3.0);
+  const double res = rw[4] + __builtin_fma(t * z, p, t);
+  return (ax == __builtin_inf()) ? copysign(1.57079632679489655800e+00, x) : copysign(res, x);
+}
+
 // getPrice (auctioneer.cpp:546-549) from the squared distance x:
 // (float)(1.0 / (sqrt(x) + 1e-8)) with IEEE sqrt and division, bit for bit.
 // The fast path computes y = 1 / (sqrt(x) + 1e-8) with sqrt_nr and div_nr

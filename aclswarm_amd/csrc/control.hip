@@ -107,9 +107,9 @@ __global__ void __launch_bounds__(kB, kB == 256 ? (NP == 5 ? ACL_GAIN_WAVES : 4)
   double* red = reinterpret_cast<double*>(smem + L.red) + wave * 64 * 3;
   double* atab = reinterpret_cast<double*>(smem + L.atab);
 #if ACL_GAIN_FASTMATH
-  if (tid < ACL_ATAB_N) atab[tid] = kAtan32Tab[tid / 5][tid % 5];
+  for (int k = tid; k < ACL_ATAB_N; k += kB) atab[k] = ACL_ATAB[k / 5][k % 5];
 #else
-  if (tid < ACL_ATAB_N) atab[tid] = kAtanTab[tid / 6][tid % 6];
+  for (int k = tid; k < ACL_ATAB_N; k += kB) atab[k] = kAtanTab[k / 6][k % 6];
 #endif
 
   // the gate-margin word: set before the barriers below, so that every

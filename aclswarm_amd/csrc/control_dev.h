@@ -19,16 +19,18 @@ constexpr int kCtlBlock = 256;
 #define ACL_GAIN_WAVES 6  // waves per SIMD the record-layout gain kernel is built for
 #endif
 #ifndef ACL_GAIN_FASTMATH
-#define ACL_GAIN_FASTMATH 1  // 17-point atan reduction and one-step sqrt (1e-14 relative)
+#define ACL_GAIN_FASTMATH 1  // binade-indexed atan and one-step sqrt (about 1e-14 relative)
 #endif
 #if ACL_GAIN_FASTMATH
 #define ACL_GAIN_SQRT sqrt_nr1
-#define ACL_GAIN_ATAN acl_atan_k32
-#define ACL_ATAB_N 85
+#define ACL_GAIN_ATAN acl_atan_b
+#define ACL_ATAB_N 170
+#define ACL_ATAB kAtanBTab
 #else
 #define ACL_GAIN_SQRT sqrt_nr
 #define ACL_GAIN_ATAN acl_atan_tab
 #define ACL_ATAB_N 30
+#define ACL_ATAB kAtanTab
 #endif
 constexpr int kCtlWaves = kCtlBlock / 64;
 
@@ -383,9 +385,9 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
   double* uo = reinterpret_cast<double*>(smem + L.out);
   double* atab = reinterpret_cast<double*>(smem + L.atab);
 #if ACL_GAIN_FASTMATH
-  if (tid < ACL_ATAB_N) atab[tid] = kAtan32Tab[tid / 5][tid % 5];
+  for (int k = tid; k < ACL_ATAB_N; k += nthreads) atab[k] = ACL_ATAB[k / 5][k % 5];
 #else
-  if (tid < ACL_ATAB_N) atab[tid] = kAtanTab[tid / 6][tid % 6];
+  for (int k = tid; k < ACL_ATAB_N; k += nthreads) atab[k] = kAtanTab[k / 6][k % 6];
 #endif
   // gate margin word (in the dynamic layout: the fused kernel may use all
   // 160 KiB): set before the barriers below

@@ -174,7 +174,7 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
 
   // ---- setup: the caller has written Pt[tid] (thread tid reads it back
   // here, so no barrier is needed first); every other table is built here
-  if (tid < ACL_ATAB_N) atab[tid] = kAtan32Tab[tid / 5][tid % 5];
+  for (int k = tid; k < ACL_ATAB_N; k += nthreads) atab[k] = ACL_ATAB[k / 5][k % 5];
   if (GM && tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
   if (tid == 0) {
     *caw = 0u;

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 4: margin filters (new4) -- parity of the n <= 128 kernels, then a
+# same-box A/B against new3 (before) and base (round 3).
+set -o pipefail
+cd /root/repo
+mkdir -p gpurun_out
+timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_margins.py tests/test_gpu_fused.py tests/test_gpu_c3_full.py tests/test_gpu_facade.py tests/test_gpu_formats.py tests/test_gpu_episode.py > gpurun_out/r4_t3.log 2>&1 || { tail -40 gpurun_out/r4_t3.log; exit 1; }
+tail -3 gpurun_out/r4_t3.log
+bash scripts/gpu_ab.sh base new3 new4

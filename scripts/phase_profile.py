@@ -69,11 +69,15 @@ if args.n <= 128 and not args.crowd and sec[:, :8].any():
         x = sec[:, k].astype(np.float64)
         print(f"  cbaa {nm:16s} wave-cycles/swarm {x.mean():10.0f}  share {x.sum() / tot8 * 100:5.1f}%")
     cnt = sec[:, 8]
-    cols = (cnt & np.uint64((1 << 21) - 1)).astype(np.float64)
-    walks = ((cnt >> np.uint64(21)) & np.uint64((1 << 21) - 1)).astype(np.float64)
-    scans = (cnt >> np.uint64(42)).astype(np.float64)
+    f12 = lambda sh, w=12: ((cnt >> np.uint64(sh)) & np.uint64((1 << w) - 1)).astype(np.float64)
+    if os.environ.get("ACL_PROF_OLDPACK"):  # libraries before round 4: 21-bit fields
+        cols, walks, scans = f12(0, 21), f12(21, 21), f12(42, 21)
+        sels = selx = np.zeros_like(cols)
+    else:
+        cols, walks, scans, sels, selx = f12(0), f12(12), f12(24), f12(36), f12(48)
     print(f"  per swarm: columns evaluated {cols.mean():.1f}, runner-up walks {walks.mean():.1f}, "
-          f"exact scans {scans.mean():.1f}")
+          f"exact scans {scans.mean():.1f}, re-selects {sels.mean():.1f}, "
+          f"select margin evaluations (per 64-task chunk) {selx.mean():.1f}")
 # wide CBAA sections (a -DACL_WIDE_PROF=1 build, n > 128): wave-cycles summed
 # over the swarm's 16 waves
 if args.n > 128 and sec[:, :4].any():
