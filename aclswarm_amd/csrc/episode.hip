@@ -102,10 +102,14 @@ __global__ void __launch_bounds__(64) latency_kernel(int n, const int32_t* fidx,
 //   step has come completes.
 // Completion (auctioneer.cpp:250-295): an agreed valid result is adopted, an
 // agreed invalid one sets the flag, a disagreeing swarm keeps its assignment.
+// wsPt / wsMode (mode 1): the control hand-off of a swarm that adopts is
+// rebuilt here (the inverse of its new permutation), so a step where no
+// pending auction completes needs no hand-off pass over every swarm.
 __global__ void __launch_bounds__(64) adopt_kernel(int n, int step, int mode, const int32_t* lat,
                                                    uint16_t* P, const uint16_t* Pnew,
                                                    const acl_swarm_status_t* st, uint8_t* flush,
-                                                   acl_episode_status_t* est) {
+                                                   acl_episode_status_t* est, uint16_t* wsPt,
+                                                   uint8_t* wsMode) {
   const int b = blockIdx.x, tid = threadIdx.x;
   __shared__ int take;
   if (tid == 0) {
@@ -117,13 +121,13 @@ __global__ void __launch_bounds__(64) adopt_kernel(int n, int step, int mode, co
         ++e.n_skipped;
       } else {
         ++e.n_auctions;
-        if (e.pending_step >= 0) ++e.n_restarted;
+        if (lat && e.pending_step > 0) ++e.n_restarted;
         const int L = lat ? lat[b] : 0;
-        e.pending_step = L > 0 ? step + L : -1;
+        e.pending_step = L > 0 ? step + L + 1 : 0;  // completion step + 1; 0: none
         complete = L <= 0;
       }
-    } else if (e.pending_step >= 0 && e.pending_step <= step) {
-      e.pending_step = -1;
+    } else if (e.pending_step > 0 && e.pending_step - 1 <= step) {
+      e.pending_step = 0;
       complete = true;
     }
     take = 0;
@@ -137,8 +141,14 @@ __global__ void __launch_bounds__(64) adopt_kernel(int n, int step, int mode, co
     est[b] = e;
   }
   __syncthreads();
-  if (take)
-    for (int v = tid; v < n; v += 64) P[(size_t)b * n + v] = Pnew[(size_t)b * n + v];
+  if (take) {
+    for (int v = tid; v < n; v += 64) {
+      const uint16_t pv = Pnew[(size_t)b * n + v];
+      P[(size_t)b * n + v] = pv;
+      if (wsPt) wsPt[(size_t)b * n + pv] = (uint16_t)v;  // a valid permutation
+    }
+    if (wsMode && tid == 0) wsMode[b] = 0;
+  }
 }
 
 struct TrajParams {
@@ -339,6 +349,8 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
   // rebuilt on the first step of a call and after every auction (which also
   // overwrites it); the collision-avoidance count is zeroed by traj_kernel
   T.ca_count = reinterpret_cast<unsigned*>(ws + W.solve + ws_layout(n, B).cacount);
+  uint16_t* hoPt = reinterpret_cast<uint16_t*>(ws + W.solve + ws_layout(n, B).pt);
+  uint8_t* hoMode = ws + W.solve + ws_layout(n, B).mode;
   // auctions that take time: each swarm's latency in control steps
   const bool timed = ep.auction_latency != 0;
   int32_t* lat = reinterpret_cast<int32_t*>(ws + W.lat);
@@ -355,16 +367,16 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
       const acl_status_t r = acl_solve_batch(F, &sa, stream);
       if (r != ACL_OK) return r;
       hipLaunchKernelGGL(adopt_kernel, dim3(B), dim3(64), 0, s, n, step, 0,
-                         timed ? lat : nullptr, a->P, Pnew, st, a->flush, a->est);
+                         timed ? lat : nullptr, a->P, Pnew, st, a->flush, a->est, nullptr,
+                         nullptr);
       if (hipGetLastError() != hipSuccess) return acl__set_error("adopt_kernel launch failed");
       flags |= CTL_PREP | CTL_RESET;
     } else if (timed) {
-      // a pending auction completing at this step changes P: rebuild the
-      // control hand-off
+      // a pending auction completing at this step changes P: adopt_kernel
+      // rebuilds those swarms' control hand-off (inverse assignment) itself
       hipLaunchKernelGGL(adopt_kernel, dim3(B), dim3(64), 0, s, n, step, 1, lat, a->P, Pnew, st,
-                         a->flush, a->est);
+                         a->flush, a->est, hoPt, hoMode);
       if (hipGetLastError() != hipSuccess) return acl__set_error("adopt_kernel launch failed");
-      flags |= CTL_PREP;
     }
     const acl_status_t r = run_control(F, &cs, s, flags);
     if (r != ACL_OK) return r;

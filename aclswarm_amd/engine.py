@@ -335,9 +335,8 @@ class Episode:
         self.P = P.clone().contiguous()
         self.flush = torch.zeros(self.B, dtype=torch.uint8, device=dev)
         est = np.zeros(self.B, L.EPISODE_STATUS_DTYPE)
-        est["converged_step"] = -1
+        est["converged_step"] = -1  # zeroed otherwise (pending_step 0: none)
         est["gridlock_step"] = -1
-        est["pending_step"] = -1
         self.est = torch.from_numpy(est.view(np.uint8).reshape(self.B, -1).copy()).to(dev)
         Lb = int(self.ep.bufflen)
         self.ring_u = torch.zeros((self.B, Lb, self.n), dtype=torch.float64, device=dev)

@@ -167,10 +167,13 @@ typedef struct {
  *            admits.
  *   gains_tiled  optional (NULL = unused): the gain_planes == 5 records of
  *            every formation re-ordered by acl_tile_gains into 8 x 8 edge
- *            tiles (same per-formation offsets 5*gain_off[f]). The kernel that
- *            applies each undirected edge once reads it instead of `gains`
- *            when n <= 128, so that every tile it processes is one contiguous
- *            run of records. Same values, same commands, bit for bit.
+ *            tiles (same per-formation offsets 5*gain_off[f]). Only
+ *            acl_control_batch reads it (its pair kernel, n <= 128: every tile
+ *            it processes is one contiguous run of records; same commands,
+ *            bit for bit); acl_solve_batch's fused auction + control phase
+ *            always reads the row-major `gains`. The two entry points'
+ *            commands on the same assignment agree to about 1e-12 relative
+ *            (the same terms summed in another order), not bit for bit.
  */
 typedef struct {
   int32_t n;
@@ -431,7 +434,8 @@ acl_status_t acl_hungarian_batch(const acl_formations_t* formations,
  * Device pointers, updated in place so an episode can continue in chunks:
  *   fidx [B]; q, vel [B][n][3]; P [B][n] (a permutation); flush [B] u8;
  *   est [B] acl_episode_status_t; ring_u [B][bufflen][n] f64 and
- *   ring_ca [B][bufflen][n] u8 (zeroed with est before step 0).
+ *   ring_ca [B][bufflen][n] u8 (zeroed with est before step 0; in est,
+ *   converged_step and gridlock_step then set to -1).
  * Optional histories (NULL = not stored), k = local step:
  *   q_hist, vel_hist [steps][B][n][3] (state after step k), u_hist [steps][B][n][3]
  *   (DistCntrl output), ca_hist [steps][B][n], P_hist [steps][B][n]
@@ -482,9 +486,11 @@ typedef struct {
                               the reference is not carried) */
   uint32_t n_samples;      /* supervisor ticks taken */
   uint32_t n_ca_steps;     /* vehicle-steps with collision avoidance active */
-  int32_t pending_step;    /* global step at which the pending auction's result
-                              is adopted, -1 if none (auction_latency != 0; its
-                              result stays in the workspace between calls) */
+  int32_t pending_step;    /* 1 + the global step at which the pending
+                              auction's result is adopted, 0 if none
+                              (auction_latency != 0; its result stays in the
+                              workspace between calls): a zeroed status is the
+                              start of an episode */
   uint16_t n_restarted;    /* auctions restarted before they completed */
   uint16_t reserved;
 } acl_episode_status_t; /* 40 bytes */

@@ -195,8 +195,48 @@ def test_episode_auction_latency(cuda, lat):
         assert (st["n_auctions"], st["n_restarted"], st["n_skipped"]) == \
             (c["auctions"], c["restarted"], c["skipped"]), (st, c)
         assert (st["n_invalid"], st["n_disagree"]) == (c["invalid"], c["disagree"])
-        assert st["pending_step"] == auc.pending
+        assert st["pending_step"] == (auc.pending + 1 if auc.pending >= 0 else 0)
         if lat == 25:
             assert c["adopted"] == 0 and c["restarted"] == c["auctions"] - 1
         else:
             assert c["adopted"] > 0
+
+
+def test_episode_zeroed_status_mid_period(cuda):
+    """A status zeroed at the start (pending_step 0 = none; only converged_step
+    and gridlock_step -1), with auctions that take time and a first step that
+    is not an auto-auction step: the first auction counts no restart, nothing
+    completes before it, and the teacher-forced state machine agrees."""
+    import torch
+    case = dict(_cases()[0], ep=dict(auction_every=10, auction_latency=3), steps=40)
+    e, eps = _episode(case, cuda)
+    est0 = np.zeros(e.B, dtype=e.status().dtype)
+    est0["converged_step"] = -1
+    est0["gridlock_step"] = -1
+    e.est.copy_(torch.from_numpy(est0.view(np.uint8).reshape(e.B, -1).copy()))
+    e.step = 5
+    hist = e.run(case["steps"], history=True)
+    torch.cuda.synchronize()
+    h = {k: v.cpu().numpy() for k, v in hist.items()}
+    h["P"] = h["P"].view(np.uint16)
+    est = e.status()
+    ep = E.params_from_struct(eps)
+    B, n = case["q"].shape[:2]
+    for b in range(B):
+        f = case["fidx"][b]
+        p, adj, G = case["pts"][f], case["adj"][f], case["gains"][f]
+        auc = E.Auctions(3)
+        P = case["P"][b].astype(np.uint16)
+        qprev, vprev = case["q"][b], case["vel"][b]
+        for k in range(case["steps"]):
+            s = 5 + k
+            if s % ep["auction_every"] == 0:
+                P = auc.auto(s, P, lambda: O.solve(qprev, vprev, p, adj, G, P))
+            else:
+                P = auc.tick(s, P)
+            assert (h["P"][k, b] == P).all(), (b, k)
+            qprev, vprev = h["q"][k, b], h["vel"][k, b]
+        st, c = est[b], auc.counts
+        assert st["n_restarted"] == c["restarted"] == 0
+        assert (st["n_auctions"], st["n_skipped"]) == (c["auctions"], c["skipped"])
+        assert st["pending_step"] == (auc.pending + 1 if auc.pending >= 0 else 0)
