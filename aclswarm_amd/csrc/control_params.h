@@ -53,7 +53,9 @@ constexpr int kMaxNWide = 512;  // tables-in-HBM auction kernel (solve_wide.hip)
 //           the n > 128 kernel, which does not fit LDS
 //   align   [B] x (out [n][6] f64 the work items' R, t; itm [n] u8 the item of
 //           each formation row; u64 smallest alignment gap; i32 item count):
-//           align_kernel's results for the n <= 128 auction kernel
+//           align_kernel's results for the n <= 128 auction kernel; for
+//           n > 128 align_wide_kernel's (out [n][6] per vehicle, vadj
+//           [NW][n] u64, u64 gap, u32 flags)
 struct WsLayout {
   size_t pt, mode, rows, u, calist, cacount, camask, wide, wide_stride, align, align_stride, total;
 };
@@ -76,7 +78,12 @@ __host__ __device__ inline WsLayout ws_layout(int n, int B) {
   o += bb * W.wide_stride;
   o = ws_al(o);
   W.align = o;
-  W.align_stride = n <= kMaxN ? ((nb * 48 + ((nb + 15) & ~(size_t)15) + 16 + 15) & ~(size_t)15) : 0;
+  // n > 128 (align_wide_kernel, solve_wide.hip): out [n][6] f64, the
+  // vehicle-space neighbourhood masks vadj [NW][n] u64, the smallest
+  // alignment gap (u64 bits) and a flags word
+  W.align_stride = n <= kMaxN
+                       ? ((nb * 48 + ((nb + 15) & ~(size_t)15) + 16 + 15) & ~(size_t)15)
+                       : ((nb * 48 + (size_t)((n + 63) >> 6) * nb * 8 + 16 + 15) & ~(size_t)15);
   o += bb * W.align_stride;
   W.total = o;
   return W;

@@ -18,11 +18,18 @@
 // kernel's price phase, so every price is bit-identical). Recomputing costs
 // ~40 f64 operations; reading a stored price was a random HBM access.
 //
-// LDS keeps the per-swarm state every phase touches (~150 KB at n = 512):
-// points, alignments, the formation and vehicle-space neighbourhood
-// bitmasks (8 words per row), the dirty-column and outbid masks. One
-// workgroup of 16 waves per swarm; indices are u16 (the reference's u8
-// vehidx_t caps N at 255; widened as SURVEY.md 8d prescribes for C4).
+// Two launches (round 4). align_wide_kernel (one 1 024-thread workgroup per
+// swarm) loads the formation, checks P_in, and leaves in the workspace every
+// vehicle's alignment (R, t), the vehicle-space closed-neighbourhood masks
+// (8 words per vehicle) and the smallest alignment gap. solve_wide_kernel
+// (8 waves per swarm) keeps only what the CBAA rounds touch in LDS -- points,
+// q, the neighbourhood masks, the column price cache and the masks: ~62 KB at
+// n = 500, so two swarms share a CU and one's round barriers and table
+// latency hide behind the other's work (the kernel waited half its time with
+// one 16-wave swarm per CU) -- and reads the alignments from the workspace
+// (24 KB per swarm, L2-resident; wave-uniform in the selects). Indices are
+// u16 (the reference's u8 vehidx_t caps N at 255; widened as SURVEY.md 8d
+// prescribes for C4).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -36,10 +43,25 @@ namespace acl_amd {
 enum { W_RCH = 3 /* misc[3..4]: a column changed in a round of that parity */,
        W_BIG = 12 /* a coordinate or alignment entry is not below 1e100 */ };
 
-constexpr int kWBlock = 1024;
+constexpr int kWBlock = 512;    // solve_wide_kernel: 8 waves per swarm, 2 swarms per CU
 constexpr int kWWaves = kWBlock / 64;
+constexpr int kWABlock = 1024;  // align_wide_kernel
 constexpr int kWMaxW = kMaxNWide / 64;  // 64-bit words per bitmask row
 constexpr int kWLevels = 3;
+
+// align_wide_kernel's results in the workspace (WsLayout::align, per swarm)
+struct WsWide {
+  size_t out, vadj, gal, flags;
+};
+__host__ __device__ inline WsWide ws_wide(int n) {
+  const int NW = (n + 63) >> 6;
+  WsWide w;
+  w.out = 0;                                   // [n][6] f64 R, t per vehicle
+  w.vadj = (size_t)n * 48;                     // [NW][n] u64 closed neighbourhoods
+  w.gal = w.vadj + (size_t)NW * n * 8;         // u64 bits of the smallest alignment gap
+  w.flags = w.gal + 8;                         // u32: bit 0 bad input, bit 1 p not finite
+  return w;
+}
 
 // index of entry (task j, vehicle u) of the tiled `who` table
 __host__ __device__ __forceinline__ size_t tix(int n, int j, int u) {
@@ -51,21 +73,38 @@ __host__ __device__ __forceinline__ int tix_size(int n) {
   return n8 * n8 * 64;
 }
 
-struct WLayout {
-  int p, qf, out, sums, adjF, vadj, Pin, Ptin, ccw, ccp, valid, masks, seen, misc, total;
-};
-
 __host__ __device__ inline int wal(int x) { return (x + 15) & ~15; }
+
+// align_wide_kernel's LDS
+struct WALayout {
+  int p, qf, sums, adjF, Pin, seen, misc, total;
+};
+__host__ __device__ inline WALayout make_walayout(int n) {
+  const int NW = (n + 63) >> 6;
+  WALayout L;
+  int o = 0;
+  L.p = o;     o = wal(o + n * 24);
+  L.qf = o;    o = wal(o + n * 24);   // q in formation order
+  L.sums = o;  o = wal(o + n * 64);   // alignment sums
+  L.adjF = o;  o = wal(o + n * NW * 8);
+  L.Pin = o;   o = wal(o + n * 2);
+  L.seen = o;  o = wal(o + NW * 8);   // permutation check
+  L.misc = o;  o = wal(o + 64);
+  L.total = o;
+  return L;
+}
+
+// solve_wide_kernel's LDS
+struct WLayout {
+  int p, qv, vadj, Pin, Ptin, ccw, ccp, valid, masks, seen, misc, total;
+};
 
 __host__ __device__ inline WLayout make_wlayout(int n) {
   const int NW = (n + 63) >> 6;
   WLayout L;
   int o = 0;
   L.p = o;     o = wal(o + n * 24);
-  L.qf = o;    o = wal(o + n * 24);   // q in formation order
-  L.out = o;   o = wal(o + n * 48);   // R, t per vehicle
-  L.sums = o;  o = wal(o + n * 64);   // alignment sums, then q in vehicle order
-  L.adjF = o;  o = wal(o + n * NW * 8);
+  L.qv = o;    o = wal(o + n * 24);   // q in vehicle order
   L.vadj = o;  o = wal(o + n * NW * 8);  // [word][vehicle]: conflict-free per-lane reads
   L.Pin = o;   o = wal(o + n * 2);
   L.Ptin = o;  o = wal(o + n * 2);
@@ -73,7 +112,7 @@ __host__ __device__ inline WLayout make_wlayout(int n) {
   L.ccp = o;   o = wal(o + n * 4);    // and its price for j
   L.valid = o; o = wal(o + n);
   L.masks = o; o = wal(o + 4 * NW * 8);                // dmask[2][NW], obm[2][NW]
-  L.seen = o;  o = wal(o + (kWWaves + 1) * NW * 8);   // permutation checks
+  L.seen = o;  o = wal(o + kWWaves * NW * 8);         // per-wave validity checks
   L.misc = o;  o = wal(o + 64);
   L.total = o;
   return L;
@@ -196,35 +235,33 @@ __device__ __forceinline__ void wstamp(const SolveParams& P, int b, int k) {
 #define WPROF_ADD(acc, x)
 #endif
 
-__global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParams P) {
+// Phases 0-1 of the n > 128 solve, one 1 024-thread workgroup per swarm:
+// load, the permutation check, the vehicle-space closed neighbourhoods and
+// every vehicle's 2-D Umeyama alignment (Auctioneer::alignFormation,
+// auctioneer.cpp:347-415; Eigen's two sequential passes, bit for bit), left
+// in the workspace for solve_wide_kernel (WsWide).
+__global__ void __launch_bounds__(kWABlock, 1) align_wide_kernel(const SolveParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const int NW = (n + 63) >> 6;
-  const WLayout L = make_wlayout(n);
+  const WALayout L = make_walayout(n);
   const int b = P.b0 + blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  constexpr int kAW = kWABlock / 64;
 
   double* p = reinterpret_cast<double*>(smem + L.p);
   double* qf = reinterpret_cast<double*>(smem + L.qf);
-  double* out = reinterpret_cast<double*>(smem + L.out);
   double* sums = reinterpret_cast<double*>(smem + L.sums);
-  double* qv = reinterpret_cast<double*>(smem + L.sums);  // after phase 1
   unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
-  unsigned long long* vadj = reinterpret_cast<unsigned long long*>(smem + L.vadj);
   uint16_t* Pin = reinterpret_cast<uint16_t*>(smem + L.Pin);
-  uint16_t* Ptin = reinterpret_cast<uint16_t*>(smem + L.Ptin);
-  uint16_t* ccw = reinterpret_cast<uint16_t*>(smem + L.ccw);
-  float* ccp = reinterpret_cast<float*>(smem + L.ccp);
-  unsigned char* validv = smem + L.valid;
-  unsigned long long* dmask = reinterpret_cast<unsigned long long*>(smem + L.masks);
-  unsigned long long* obm = dmask + 2 * NW;
   unsigned long long* seen = reinterpret_cast<unsigned long long*>(smem + L.seen);
   int* misc = reinterpret_cast<int*>(smem + L.misc);
-
-  unsigned char* wsb = P.ws + P.W.wide + (size_t)b * P.W.wide_stride;
-  uint16_t* T = reinterpret_cast<uint16_t*>(wsb);
+  const WsWide WW = ws_wide(n);
+  unsigned char* wsa = P.ws + P.W.align + (size_t)b * P.W.align_stride;
+  double* out = reinterpret_cast<double*>(wsa + WW.out);
+  unsigned long long* vadj = reinterpret_cast<unsigned long long*>(wsa + WW.vadj);
 
   // a formation index out of range is a bad input like a bad P_in (nothing
   // of the formation table is read for it)
@@ -232,83 +269,47 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   const bool fbad = f_in < 0 || f_in >= P.F;
   const int f = fbad ? 0 : f_in;
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
-  MarginPair mp;
-  margin_init(mp);
-  double galign = 1.0;
-  wstamp(P, b, 0);
-  bool pbad = false;  // a formation coordinate is not finite (phase 2's fast path)
-
-  // ---------------- phase 0: load -----------------------------------------
+  bool pbad = false;  // a formation coordinate is not finite (the prices' fast path)
   {
     const double* gp = P.p + (size_t)f * n * 3;
-    for (int k = tid; k < 3 * n; k += kWBlock) {
+    for (int k = tid; k < 3 * n; k += kWABlock) {
       const double x = gp[k];
       pbad |= !__builtin_isfinite(x);
       p[k] = x;
     }
     const uint64_t* ga = P.adj + (size_t)f * n * NW;
-    for (int k = tid; k < n * NW; k += kWBlock) {
+    for (int k = tid; k < n * NW; k += kWABlock) {
       unsigned long long x = ga[k];
       if (k % NW == NW - 1) x &= lastmask;
       adjF[k] = x;
     }
-    for (int k = tid; k < 4 * NW; k += kWBlock) dmask[k] = 0ull;
-    for (int k = tid; k < n; k += kWBlock) ccw[k] = (uint16_t)n;
-    for (int k = tid; k < (kWWaves + 1) * NW; k += kWBlock) seen[k] = 0ull;
+    for (int k = tid; k < NW; k += kWABlock) seen[k] = 0ull;
     if (tid < 16) misc[tid] = 0;
   }
   __syncthreads();
-  if (tid == 0) {
-    misc[M_AGREE] = 1;
-    if (fbad) misc[M_BAD] = 1;
-    *reinterpret_cast<unsigned long long*>(misc + M_MARG) =
-        (unsigned long long)__double_as_longlong(1.0);
-  }
+  if (tid == 0 && fbad) misc[M_BAD] = 1;
   if (__any(pbad) && lane == 0) misc[M_PINF] = 1;
-  unsigned long long* seenP = seen + kWWaves * NW;
-  for (int v = tid; v < n; v += kWBlock) {
+  for (int v = tid; v < n; v += kWABlock) {
     const unsigned pv = P.P_in[(size_t)b * n + v];
     Pin[v] = (uint16_t)pv;
     if (pv >= (unsigned)n) {
       misc[M_BAD] = 1;
     } else {
       const unsigned long long bit = 1ull << (pv & 63);
-      const unsigned long long prev = atomicOr(&seenP[pv >> 6], bit);
+      const unsigned long long prev = atomicOr(&seen[pv >> 6], bit);
       if (prev & bit) misc[M_BAD] = 1;
-      Ptin[pv] = (uint16_t)v;
+      const double* gq = P.q + ((size_t)b * n + v) * 3;
+      qf[3 * pv] = gq[0]; qf[3 * pv + 1] = gq[1]; qf[3 * pv + 2] = gq[2];
     }
   }
   __syncthreads();
-  if (misc[M_BAD]) {
-    for (int v = tid; v < n; v += kWBlock) {
-      P.P_out[(size_t)b * n + v] = P.P_in[(size_t)b * n + v];
-      if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 0;
-    }
-    for (int k = tid; k < 3 * n; k += kWBlock) {
-      if (P.u) P.u[(size_t)b * n * 3 + k] = 0.0;
-      if (P.u_safe) P.u_safe[(size_t)b * n * 3 + k] = 0.0;
-    }
-    if (P.who)
-      for (int k = tid; k < n * n; k += kWBlock) P.who[(size_t)b * n * n + k] = 0xFFFF;
-    if (P.gate_margin && tid == 0) P.gate_margin[b] = __builtin_inf();
-    if (tid == 0) {
-      acl_swarm_status_t st = {};
-      st.flags = ACL_SWARM_BAD_INPUT;
-      st.rounds = (uint16_t)(2 * n);
-      st.margin = 1.0f;
-      P.status[b] = st;
-    }
+  unsigned* wflags = reinterpret_cast<unsigned*>(wsa + WW.flags);
+  if (misc[M_BAD]) {  // solve_wide_kernel writes the BAD_INPUT outputs
+    if (tid == 0) *wflags = 1u;
     return;
   }
-  {
-    const double* gq = P.q + (size_t)b * n * 3;
-    for (int k = tid; k < 3 * n; k += kWBlock) {
-      const int j = k / 3, c = k - 3 * j;
-      qf[k] = gq[3 * Ptin[j] + c];
-    }
-  }
   // vehicle-space closed neighbourhoods (bidIterComplete, auctioneer.cpp:419-437)
-  for (int v = wave; v < n; v += kWWaves) {
+  for (int v = wave; v < n; v += kAW) {
     const int i = Pin[v];
     for (int c = 0; c < NW; ++c) {
       const int u = lane + 64 * c;
@@ -321,18 +322,14 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       if (lane == 0) vadj[c * n + v] = m;  // word-major: lanes over vehicles read consecutive words
     }
   }
-  __syncthreads();
-  wstamp(P, b, 1);
-
-  // ---------------- phase 1: alignment (see solve.hip) --------------------
-  for (int t = tid; t < 4 * n; t += kWBlock) {
+  // alignment sums, ascending members, branch-free: -0.0 is the exact
+  // identity of IEEE addition (-0 + x == x for every x, signed zeros
+  // included), so starting from it and adding -0.0 for a non-neighbour gives
+  // the bits of "first term, then acc + term"
+  for (int t = tid; t < 4 * n; t += kWABlock) {
     const int v = t >> 2, c = t & 3;
     const int i = Pin[v];
     const double* src = (c < 2) ? (p + c) : (qf + (c - 2));
-    // the neighbours' sum in ascending order, branch-free: -0.0 is the exact
-    // identity of IEEE addition (-0 + x == x for every x, signed zeros
-    // included), so starting from it and adding -0.0 for a non-neighbour
-    // gives the bits of "first term, then acc + term"
     double acc = -0.0;
     for (int w = 0; w < NW; ++w) {
       unsigned long long bits = adjF[i * NW + w];
@@ -351,7 +348,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     sums[8 * v + c] = acc;
   }
   __syncthreads();
-  for (int t = tid; t < 4 * n; t += kWBlock) {
+  for (int t = tid; t < 4 * n; t += kWABlock) {
     const int v = t >> 2, c = t & 3;
     const int i = Pin[v];
     int k = 0;
@@ -389,7 +386,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     sums[8 * v + 4 + c] = lazy ? acc : acc * oon;
   }
   __syncthreads();
-  for (int v = tid; v < n; v += kWBlock) {
+  double galign = 1.0;
+  for (int v = tid; v < n; v += kWABlock) {
     const int i = Pin[v];
     int k = 0;
     for (int w = 0; w < NW; ++w) {
@@ -407,22 +405,115 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     double* o = out + 6 * v;
     o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
   }
+  // the swarm's smallest alignment gap and the flags
+  unsigned long long* gw = reinterpret_cast<unsigned long long*>(misc + 12);  // (8-byte aligned)
+  if (tid == 0) *gw = (unsigned long long)__double_as_longlong(1.0);
   __syncthreads();
+  block_min_gap(gw, galign);
+  __syncthreads();
+  if (tid == 0) {
+    *reinterpret_cast<unsigned long long*>(wsa + WW.gal) = *gw;
+    *wflags = misc[M_PINF] ? 2u : 0u;
+  }
+}
+
+__global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = P.n;
+  const int NW = (n + 63) >> 6;
+  const WLayout L = make_wlayout(n);
+  const int b = P.b0 + blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+
+  double* p = reinterpret_cast<double*>(smem + L.p);
+  double* qv = reinterpret_cast<double*>(smem + L.qv);
+  unsigned long long* vadj = reinterpret_cast<unsigned long long*>(smem + L.vadj);
+  uint16_t* Pin = reinterpret_cast<uint16_t*>(smem + L.Pin);
+  uint16_t* Ptin = reinterpret_cast<uint16_t*>(smem + L.Ptin);
+  uint16_t* ccw = reinterpret_cast<uint16_t*>(smem + L.ccw);
+  float* ccp = reinterpret_cast<float*>(smem + L.ccp);
+  unsigned char* validv = smem + L.valid;
+  unsigned long long* dmask = reinterpret_cast<unsigned long long*>(smem + L.masks);
+  unsigned long long* obm = dmask + 2 * NW;
+  unsigned long long* seen = reinterpret_cast<unsigned long long*>(smem + L.seen);
+  int* misc = reinterpret_cast<int*>(smem + L.misc);
+
+  unsigned char* wsb = P.ws + P.W.wide + (size_t)b * P.W.wide_stride;
+  uint16_t* T = reinterpret_cast<uint16_t*>(wsb);
+  const WsWide WW = ws_wide(n);
+  const unsigned char* wsa = P.ws + P.W.align + (size_t)b * P.W.align_stride;
+  const double* out = reinterpret_cast<const double*>(wsa + WW.out);  // global, L2-resident
+  const unsigned wflags = *reinterpret_cast<const unsigned*>(wsa + WW.flags);
+
+  const int f_in = P.fidx[b];
+  const int f = (f_in < 0 || f_in >= P.F) ? 0 : f_in;
+  MarginPair mp;
+  margin_init(mp);
+  wstamp(P, b, 0);
+
+  // ---------------- phase 0: load (align_wide_kernel's results) -------------
+  if (wflags & 1u) {
+    // P_in is not a permutation (or fidx is out of range): nothing is solved
+    for (int v = tid; v < n; v += kWBlock) {
+      P.P_out[(size_t)b * n + v] = P.P_in[(size_t)b * n + v];
+      if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 0;
+    }
+    for (int k = tid; k < 3 * n; k += kWBlock) {
+      if (P.u) P.u[(size_t)b * n * 3 + k] = 0.0;
+      if (P.u_safe) P.u_safe[(size_t)b * n * 3 + k] = 0.0;
+    }
+    if (P.who)
+      for (int k = tid; k < n * n; k += kWBlock) P.who[(size_t)b * n * n + k] = 0xFFFF;
+    if (P.gate_margin && tid == 0) P.gate_margin[b] = __builtin_inf();
+    if (tid == 0) {
+      acl_swarm_status_t st = {};
+      st.flags = ACL_SWARM_BAD_INPUT;
+      st.rounds = (uint16_t)(2 * n);
+      st.margin = 1.0f;
+      P.status[b] = st;
+    }
+    return;
+  }
+  {
+    const double* gp = P.p + (size_t)f * n * 3;
+    const double* gq = P.q + (size_t)b * n * 3;
+    for (int k = tid; k < 3 * n; k += kWBlock) {
+      p[k] = gp[k];
+      qv[k] = gq[k];
+    }
+    const unsigned long long* gv = reinterpret_cast<const unsigned long long*>(wsa + WW.vadj);
+    for (int k = tid; k < NW * n; k += kWBlock) vadj[k] = gv[k];
+    for (int v = tid; v < n; v += kWBlock) {
+      const unsigned pv = P.P_in[(size_t)b * n + v];  // a permutation (checked)
+      Pin[v] = (uint16_t)pv;
+      Ptin[pv] = (uint16_t)v;
+    }
+    for (int k = tid; k < 4 * NW; k += kWBlock) dmask[k] = 0ull;
+    for (int k = tid; k < n; k += kWBlock) ccw[k] = (uint16_t)n;
+    if (tid < 16) misc[tid] = 0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    misc[M_AGREE] = 1;
+    if (wflags & 2u) misc[M_PINF] = 1;
+    // the margin word starts at the smallest alignment gap
+    *reinterpret_cast<unsigned long long*>(misc + M_MARG) =
+        *reinterpret_cast<const unsigned long long*>(wsa + WW.gal);
+  }
+  wstamp(P, b, 1);
   wstamp(P, b, 2);
   if (P.align_Rt)
     for (int k = tid; k < 6 * n; k += kWBlock) P.align_Rt[(size_t)b * n * 6 + k] = out[k];
+  __syncthreads();
 
   // ---------------- phase 2: prices -----------------------------------------
-  // Not stored (see the header): q in vehicle order for wprice, and the
-  // NaN-price test. A price is NaN only if its squared distance is (acl_price
-  // is finite on [0, inf]); with every coordinate, rotation and translation
-  // entry finite and below 1e100 in magnitude no product overflows, so no
-  // distance is NaN. Otherwise every price is evaluated once.
-  for (int k = tid; k < 3 * n; k += kWBlock) {
-    const int v = k / 3, c = k - 3 * v;
-    qv[k] = qf[3 * Pin[v] + c];
-  }
-  __syncthreads();
+  // Not stored (see the header): the NaN-price test. A price is NaN only if
+  // its squared distance is (acl_price is finite on [0, inf]); with every
+  // coordinate, rotation and translation entry finite and below 1e100 in
+  // magnitude no product overflows, so no distance is NaN. Otherwise every
+  // price is evaluated once.
   const WPrice price{out, qv, p, misc[M_PINF] == 0};
   {
     bool big = false;
@@ -733,12 +824,9 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
 #endif
 
   wstamp(P, b, 4);
-  // swarm margin: min over every thread's CBAA pair and alignment gaps
-  {
-    const double gc = margin_gap(mp);
-    block_min_gap(reinterpret_cast<unsigned long long*>(misc + M_MARG),
-                  gc < galign ? gc : galign);
-  }
+  // swarm margin: min over every thread's CBAA pair (the alignment gaps are
+  // in the word already)
+  block_min_gap(reinterpret_cast<unsigned long long*>(misc + M_MARG), margin_gap(mp));
 
   // ---------------- phase 4: adoption --------------------------------------
   // Do all vehicles hold vehicle 0's table? T is column-major, so compare
@@ -862,14 +950,19 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
 }
 
 hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream) {
-  const WLayout L = make_wlayout(P.n);
   static PerDeviceOnce once;
   const hipError_t e = once.run([] {
-    return hipFuncSetAttribute((const void*)solve_wide_kernel,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    for (const void* k : {(const void*)align_wide_kernel, (const void*)solve_wide_kernel}) {
+      const hipError_t r =
+          hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (r != hipSuccess) return r;
+    }
+    return hipSuccess;
   });
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(solve_wide_kernel, dim3(nb), dim3(kWBlock), L.total, stream, P);
+  hipLaunchKernelGGL(align_wide_kernel, dim3(nb), dim3(kWABlock), make_walayout(P.n).total, stream,
+                     P);
+  hipLaunchKernelGGL(solve_wide_kernel, dim3(nb), dim3(kWBlock), make_wlayout(P.n).total, stream, P);
   return hipGetLastError();
 }
 
