@@ -182,6 +182,8 @@ acl_status_t run_control(const acl_formations_t* F, const acl_control_args_t* a,
 hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream, bool fuse = false);
 
 // The n > 128 auction kernel (solve_wide.hip).
-hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream);
+// fuse: the control phase runs in the auction's workgroups (P.ctl; 5-plane
+// gain records) for the swarms whose vehicles all adopted one assignment.
+hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream, bool fuse = false);
 
 }  // namespace acl_amd

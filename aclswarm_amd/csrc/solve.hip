@@ -222,14 +222,15 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
       return acl__set_error("hipMemsetAsync failed");
   }
   // The control phase runs inside the auction's workgroups (one launch, the
-  // gain stream overlapping the auctions) for 5-plane records at n <= 128;
-  // the directed gain kernel then takes the swarms with per-vehicle rows.
-  const bool fuse = a->do_control && n <= kMaxN && P.ctl.gain_planes == 5;
+  // gain stream overlapping the auctions) for 5-plane records, at any n (the
+  // wide kernel's wide_control for n > 128); the directed gain kernel then
+  // takes the swarms with per-vehicle rows.
+  const bool fuse = a->do_control && P.ctl.gain_planes == 5;
   kt_record(0, 0, s);
   if (n <= kMaxN) {
     e = launch_auction(P, a->B, s, fuse);
   } else {
-    e = launch_wide(P, a->B, s);
+    e = launch_wide(P, a->B, s, fuse);
   }
   kt_record(0, 1, s);
   if (e != hipSuccess) return acl__set_error(hipGetErrorString(e));

@@ -36,6 +36,7 @@
 #include "../../include/aclswarm_amd.h"
 #include "common.h"
 #include "control_params.h"
+#include "pair_fused.h"
 #include "umeyama_dev.h"
 
 namespace acl_amd {
@@ -213,6 +214,238 @@ __device__ int wide_select(int n, int NW, int v, int lane, const WPrice& price,
                      isjs || elig || near);
   }
   return js;
+}
+
+// ---- the fused control phase (n > 128, FUSE) --------------------------------
+// DistCntrl::compute (distcntrl.cpp:46-102), saturation (safety.cpp:185-196)
+// and the first collision test (safety.cpp:412-430) of a swarm whose
+// vehicles all adopted one assignment, in the auction's workgroup right after
+// its adoption: with two swarms per CU one swarm's gain stream (the HBM
+// bytes) runs beside the other's latency-bound rounds, instead of all of it
+// in a launch after every auction. The directed walk: a wave per formation
+// row i (vehicle Pt[i]), lanes over the 64 columns of one adjacency word per
+// pass, a lane's record = the row's base + the bits below it (v_mbcnt), the
+// next pass's 40-byte records loaded before this pass's math; the wave's sums
+// by DPP. p and q (vehicle order) stay where the auction left them; the rest
+// of the image overlays the auction's dead tables (<= 80 KB at n = 512, so two
+// swarms still share a CU). Parity as the other gain kernels: gates and gate
+// margin on the same expressions (pair_e, gate_decide_t), u / u_safe 1e-5.
+struct WCLayout {
+  int adj, rowbase, Pt, uo, atab, cst, flags, gmw, caw, total;
+};
+__host__ __device__ inline WCLayout make_wclayout(int n, int start) {
+  const int NW = (n + 63) >> 6;
+  WCLayout L;
+  int o = start;
+  L.adj = o;     o = wal(o + n * NW * 8);   // formation rows (masked past n)
+  L.rowbase = o; o = wal(o + (n + 1) * 4);  // record base of every row
+  L.Pt = o;      o = wal(o + n * 2);        // formation point -> vehicle
+  L.uo = o;      o = wal(o + n * 24);       // DistCntrl's u per vehicle
+  L.atab = o;    o = wal(o + ACL_ATAB_N * 8);
+  L.cst = o;     o = wal(o + FC_N * 8);     // the walk's constants (pair_fused.h FC_*)
+  L.flags = o;   o = wal(o + 4);            // bit 0: a q coordinate is not finite
+  L.gmw = o;     o = o + 8;
+  L.caw = o;     o = wal(o + 4);
+  L.total = o;
+  return L;
+}
+
+template <bool GM>
+__device__ __forceinline__ void wide_control(KCtlParams* Pp, int b, int f, unsigned char* smem,
+                                             const double* p, const double* q, int cstart,
+                                             const uint16_t* wsPt) {
+  KCtlParams& P = *Pp;
+  const int n = P.n;
+  const int NW = (n + 63) >> 6;
+  const WCLayout L = make_wclayout(n, cstart);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adj);
+  int* rowbase = reinterpret_cast<int*>(smem + L.rowbase);
+  uint16_t* Pt = reinterpret_cast<uint16_t*>(smem + L.Pt);
+  double* uo = reinterpret_cast<double*>(smem + L.uo);
+  double* atab = reinterpret_cast<double*>(smem + L.atab);
+  double* cst = reinterpret_cast<double*>(smem + L.cst);
+  unsigned* flags = reinterpret_cast<unsigned*>(smem + L.flags);
+  unsigned long long& gmw = *reinterpret_cast<unsigned long long*>(smem + L.gmw);
+  unsigned* caw = reinterpret_cast<unsigned*>(smem + L.caw);
+  const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+
+  for (int k = tid; k < ACL_ATAB_N; k += kWBlock) atab[k] = ACL_ATAB[k / 5][k % 5];
+  if (tid == 0) {
+    *flags = 0u;
+    *caw = 0u;
+    if (GM) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
+  }
+  if (tid < FC_N) {
+    const double thr_hi = P.s.d_avoid_thresh * (1.0 + 0x1p-40);
+    const double v[FC_N] = {P.g.K1_xy, P.g.K2_xy, P.g.K1_z, P.g.K2_z,
+                            P.g.e_xy_thr, P.g.e_z_thr, ACL_GATE_WINDOW, thr_hi * thr_hi};
+    double x = v[0];
+#pragma unroll
+    for (int k = 1; k < FC_N; ++k) x = tid == k ? v[k] : x;
+    cst[tid] = x;
+  }
+  {
+    const uint64_t* ga = P.adj + (size_t)f * n * NW;
+    for (int k = tid; k < n * NW; k += kWBlock) {
+      unsigned long long x = ga[k];
+      if (k % NW == NW - 1) x &= lastmask;
+      adjF[k] = x;
+    }
+    bool qbad = false;
+    for (int i = tid; i < n; i += kWBlock) {
+      Pt[i] = wsPt[i];
+      qbad |= !(__builtin_isfinite(q[3 * i]) && __builtin_isfinite(q[3 * i + 1]) &&
+                __builtin_isfinite(q[3 * i + 2]));
+    }
+    if (__any(qbad) && lane == 0) atomicOr(flags, 1u);
+  }
+  __syncthreads();
+  if (wave == 0) {  // record base of every row: a scan of the row popcounts
+    int base = 0;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+      const int i = i0 + lane;
+      int cnt = 0;
+      if (i < n)
+        for (int w = 0; w < NW; ++w) cnt += __popcll(adjF[i * NW + w]);
+      int x = cnt;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (i < n) rowbase[i] = base + x - cnt;
+      base += __shfl(x, 63, 64);
+    }
+    if (lane == 0) rowbase[n] = base;
+  }
+  __syncthreads();
+  const bool qfin = (*flags & 1u) == 0u;
+  const int E = __builtin_amdgcn_readfirstlane(rowbase[n]);
+  const double* G = P.gains + 5 * P.gain_off[f];
+  const __amdgpu_buffer_rsrc_t grs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 5 * E * 8, 0x00020000);
+  double gmxy = __builtin_inf(), gmz = __builtin_inf();
+  for (int i = wave; i < n; i += kWWaves) {
+    const int v = Pt[i];
+    const double pix = p[3 * i], piy = p[3 * i + 1], piz = p[3 * i + 2];
+    const double Ni = pix * pix + piy * piy, Nzi = piz * piz;
+    const double qv0 = q[3 * v], qv1 = q[3 * v + 1], qv2 = q[3 * v + 2];
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    int eb = __builtin_amdgcn_readfirstlane(rowbase[i]);  // the pass's first record
+    unsigned long long word = uni_u64(adjF[i * NW]);
+    Rec5 X;
+    load_rec5(grs, lanebit_u64(word) ? (int)__umul24((unsigned)eb + __builtin_amdgcn_mbcnt_hi(
+                                                         (unsigned)(word >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)word, 0u)),
+                                                     40u)
+                                     : 0x40000000, X);
+    int deg = 0;
+#pragma unroll 1
+    for (int t = 0; t < NW; ++t) {
+#pragma clang fp contract(fast)
+      const unsigned long long wc = word;
+      const int ebn = eb + __popcll(wc);
+      deg += __popcll(wc);
+      Rec5 Xn;
+      if (t + 1 < NW) {  // the next pass's records, before this pass's math
+        word = uni_u64(adjF[i * NW + t + 1]);
+        load_rec5(grs, lanebit_u64(word) ? (int)__umul24((unsigned)ebn + __builtin_amdgcn_mbcnt_hi(
+                                                             (unsigned)(word >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((unsigned)word, 0u)),
+                                                         40u)
+                                         : 0x40000000, Xn);
+      }
+      if (lanebit_u64(wc)) {
+        const int j = 64 * t + lane;
+        const int u = Pt[j];
+        const double q0 = q[3 * u] - qv0, q1 = q[3 * u + 1] - qv1, q2 = q[3 * u + 2] - qv2;
+        const double pjx = p[3 * j], pjy = p[3 * j + 1], pjz = p[3 * j + 2];
+        double Nj, Nzj;
+        {
+#pragma clang fp contract(off)
+          Nj = pjx * pjx + pjy * pjy;
+          Nzj = pjz * pjz;
+        }
+        double e_xy, e_z;
+        pair_e(q0, q1, q2, Ni, Nj, Nzi, Nzj, pix, piy, piz, pjx, pjy, pjz, pair_s2(q0, q1), e_xy,
+               e_z);
+        bool gxy, gz;
+        gate_decide_t<GM>(fcst(cst, FC_TXY), fcst(cst, FC_TZ), fcst(cst, FC_WIN), e_xy, e_z, q0, q1,
+                          q2, Ni, Nj, Nzi, Nzj, pix, piy, piz, pjx, pjy, pjz, gxy, gz, gmxy, gmz);
+        double Fxy = 0.0, Fz = 0.0;
+        if (gxy) Fxy = fcst(cst, FC_K1XY) * ACL_GAIN_ATAN(fcst(cst, FC_K2XY) * e_xy, atab);
+        if (gz) Fz = fcst(cst, FC_K1Z) * ACL_GAIN_ATAN(fcst(cst, FC_K2Z) * e_z, atab);
+        if (qfin) {  // A q + F q (kp per vehicle); the structural zeros drop (pair_fused.h)
+          a0 += X.a[1] * q1 + (X.a[0] * q0 + Fxy * q0);
+          a1 += X.a[3] * q1 + (X.a[2] * q0 + Fxy * q1);
+          a2 += X.a[4] * q2 + Fz * q2;
+        } else {
+          a0 += ((X.a[0] * q0 + X.a[1] * q1) + 0.0 * q2) + Fxy * q0;
+          a1 += ((X.a[2] * q0 + X.a[3] * q1) + 0.0 * q2) + Fxy * q1;
+          a2 += ((0.0 * q0 + 0.0 * q1) + X.a[4] * q2) + Fz * q2;
+        }
+      }
+      eb = ebn;
+      X = Xn;
+    }
+    a0 = wave_sum(a0);
+    a1 = wave_sum(a1);
+    a2 = wave_sum(a2);
+    if (lane == 0) {
+      const double kp = P.g.kp, kd = P.g.kd;
+      double u0 = kp * a0, u1 = kp * a1, u2 = kp * a2;
+      if (deg) {  // + kd (-vel) once per edge of the row (distcntrl.cpp:85-95)
+        const double* gv = P.vel + ((size_t)b * n + v) * 3;
+        const double cn = (double)deg;
+        u0 += cn * (kd * (-gv[0]));
+        u1 += cn * (kd * (-gv[1]));
+        u2 += cn * (kd * (-gv[2]));
+      }
+      uo[3 * v] = u0; uo[3 * v + 1] = u1; uo[3 * v + 2] = u2;
+    }
+  }
+  if (GM) {
+    const acl_cntrl_gains_t g = kgains(P);
+    gate_margin_reduce(&gmw, gate_margin_of(g, gmxy, gmz));
+  }
+  __syncthreads();
+  if (GM && tid == 0) P.gate_margin[b] = __longlong_as_double((long long)gmw);
+  // per vehicle: the command, saturation, the first collision test
+  // (gain_epilogue's semantics, control_dev.h)
+  const acl_safety_params_t sp = ksafety(P);
+  const double thr_hi = sp.d_avoid_thresh * (1.0 + 0x1p-40);
+  const double thr2hi = thr_hi * thr_hi;
+  for (int v = tid; v < n; v += kWBlock) {
+    double cmd0 = uo[3 * v], cmd1 = uo[3 * v + 1], cmd2 = uo[3 * v + 2];
+    double* gu = P.u + ((size_t)b * n + v) * 3;
+    gu[0] = cmd0; gu[1] = cmd1; gu[2] = cmd2;
+    saturate(sp, cmd0, cmd1, cmd2);
+    const double qv0 = q[3 * v], qv1 = q[3 * v + 1];
+    bool near = false;  // any j != v with !(s2 > thr2hi) (NaN included)
+    for (int j = 0; j < n; ++j) {
+      const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
+      near |= (j != v) && !(dx * dx + dy * dy > thr2hi);
+    }
+    bool close = false;
+    if (near) {
+      for (int j = 0; j < n; ++j) {
+        const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
+        const double d2 = dx * dx + dy * dy;
+        if (j != v && !(d2 > thr2hi)) close |= !(sqrt(d2) > sp.d_avoid_thresh);
+      }
+    }
+    if (P.u_safe) {
+      double* o = P.u_safe + ((size_t)b * n + v) * 3;
+      o[0] = cmd0; o[1] = cmd1; o[2] = cmd2;
+    }
+    if (P.ca_flag) P.ca_flag[(size_t)b * n + v] = 0;
+    const unsigned long long cm = __ballot(close);
+    if (lane == 0) {
+      P.ca_mask[(size_t)b * NW + (v >> 6)] = cm;
+      if (cm && atomicOr(caw, 1u) == 0u) P.ca_list[atomicAdd(P.ca_count, 1u)] = (unsigned)b;
+    }
+  }
 }
 
 // diagnostic: s_memtime at phase ends into P.stamps[b][k] (scripts/phase_profile.py)
@@ -417,6 +650,10 @@ __global__ void __launch_bounds__(kWABlock, 1) align_wide_kernel(const SolvePara
   }
 }
 
+// FUSE: the control phase of a swarm whose vehicles all adopted one
+// assignment runs in this workgroup after its adoption (wide_control);
+// GM: it also reports the gate margin.
+template <bool FUSE, bool GM>
 __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
@@ -929,6 +1166,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       }
     }
   }
+  const bool uniform_all = (misc[M_NINV] == 0 && misc[M_AGREE]) || misc[M_NINV] == n;
   if (tid == 0) {
     acl_swarm_status_t st = {};
     uint32_t fl = 0;
@@ -947,12 +1185,25 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     P.status[b] = st;
   }
   wstamp(P, b, 6);
+  if constexpr (FUSE) {
+    if (!uniform_all) return;  // workgroup-uniform: gain_kernel takes per-vehicle rows
+    __syncthreads();           // the auction's tables and the hand-off reads are done
+    KCtlParams* pc = (KCtlParams*)((const __attribute__((address_space(4))) char*)
+                                       __builtin_amdgcn_kernarg_segment_ptr() +
+                                   offsetof(SolveParams, ctl));
+    asm volatile("" : "+s"(pc));
+    wide_control<GM>(pc, b, f, smem, p, qv, L.qv + wal(n * 24),
+                     reinterpret_cast<const uint16_t*>(P.ws + P.W.pt) + (size_t)b * n);
+    wstamp(P, b, 7);
+  }
 }
 
-hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream) {
+hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream, bool fuse) {
   static PerDeviceOnce once;
   const hipError_t e = once.run([] {
-    for (const void* k : {(const void*)align_wide_kernel, (const void*)solve_wide_kernel}) {
+    for (const void* k : {(const void*)align_wide_kernel, (const void*)solve_wide_kernel<false, false>,
+                          (const void*)solve_wide_kernel<true, false>,
+                          (const void*)solve_wide_kernel<true, true>}) {
       const hipError_t r =
           hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (r != hipSuccess) return r;
@@ -962,7 +1213,18 @@ hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(align_wide_kernel, dim3(nb), dim3(kWABlock), make_walayout(P.n).total, stream,
                      P);
-  hipLaunchKernelGGL(solve_wide_kernel, dim3(nb), dim3(kWBlock), make_wlayout(P.n).total, stream, P);
+  const WLayout L = make_wlayout(P.n);
+  int lds = L.total;
+  if (fuse) {
+    const int c = make_wclayout(P.n, L.qv + wal(P.n * 24)).total;
+    lds = c > lds ? c : lds;
+  }
+  if (!fuse)
+    hipLaunchKernelGGL((solve_wide_kernel<false, false>), dim3(nb), dim3(kWBlock), lds, stream, P);
+  else if (P.ctl.gate_margin)
+    hipLaunchKernelGGL((solve_wide_kernel<true, true>), dim3(nb), dim3(kWBlock), lds, stream, P);
+  else
+    hipLaunchKernelGGL((solve_wide_kernel<true, false>), dim3(nb), dim3(kWBlock), lds, stream, P);
   return hipGetLastError();
 }
 
