@@ -22,7 +22,7 @@ FLAG_CHANGED = 0x04
 FLAG_NONFINITE = 0x08
 FLAG_BAD_INPUT = 0x10
 FLAG_CA_ACTIVE = 0x20
-ABI_VERSION = 5  # include/aclswarm_amd.h ACL_ABI_VERSION
+ABI_VERSION = 6  # include/aclswarm_amd.h ACL_ABI_VERSION
 FLAG_FRAGILE = 0x40
 FRAGILE_MARGIN = 1e-6
 
@@ -61,7 +61,8 @@ class AdmmParams(ct.Structure):
     _fields_ = [("verbose", ct.c_int32), ("thrSparseZero", ct.c_double),
                 ("thrPlanar", ct.c_double), ("epsEig", ct.c_double),
                 ("mu", ct.c_double), ("thresh", ct.c_double),
-                ("threshTr", ct.c_double), ("maxItr", ct.c_int32)]
+                ("threshTr", ct.c_double), ("maxItr", ct.c_int32),
+                ("basis", ct.c_int32)]
 
 
 class Formations(ct.Structure):

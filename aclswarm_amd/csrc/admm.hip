@@ -59,6 +59,8 @@ struct Scal {
   int skip_s0, skip_s1;  // which S product runs: the sign is in N0 (even updates) or N1
   int ns_fail_now;       // this iteration's sign iteration did not converge: Jacobi fallback
   int jacobi;            // iterations whose projection the Jacobi fallback made
+  int jacobi_fail;       // ... of which the fallback hit kJacobiSweeps unconverged
+  int pad2;
 };
 
 struct Part {
@@ -105,7 +107,7 @@ __device__ double nrm2_seq(const double* x, int len, int stride) {
 // in column-major order (2D.m:72-90).
 __global__ void __launch_bounds__(kT) basis_kernel(int n, int Fc, int f0, const double* pts,
                                                    const double* adj, double thrPlanar,
-                                                   double* Qbuf, size_t qstride,
+                                                   int basis, double* Qbuf, size_t qstride,
                                                    unsigned short* pairbuf, size_t pstride,
                                                    Info* info) {
   extern __shared__ double sm[];
@@ -160,6 +162,78 @@ __global__ void __launch_bounds__(kT) basis_kernel(int n, int Fc, int f0, const 
   __syncthreads();
   const int nct = min(np - 1, p);
   const int nrt = max(0, min(p - 2, np));
+  const int s = np - p;
+  double* Q = Qbuf + (size_t)part * qstride;
+  if (xy && basis == ACL_ADMM_BASIS_COMPLEX && n > 2) {
+    // Complex-structured complement (oracle complex_complement): reflectors
+    // H1, H2 triangularise [z, 1] (z = x + iy), w_k = H1 H2 e_k, columns
+    // (emb(w_k), emb(i w_k)). v1, v2 interleaved (re, im) per agent in A.
+    double* v1 = A;            // n complex
+    double* v2 = A + 2 * n;    // n complex, v2[0] = 0 (H2 acts on agents 1..n-1)
+    if (tid == 0) {
+      double b1 = 0.0, b2 = 0.0;
+      for (int c = 0; c < 2; ++c) {
+        double* v = c ? v2 : v1;
+        const int i0 = c;      // first agent the reflector acts on
+        for (int i = 0; i < 2 * n; ++i) v[i] = 0.0;
+        if (c == 0) {
+          for (int i = 0; i < n; ++i) { v[2 * i] = P[3 * i]; v[2 * i + 1] = P[3 * i + 1]; }
+        } else {
+          // y = H1 1 restricted to agents 1..n-1
+          double yr = 0.0, yi = 0.0;   // v1^H 1
+          for (int i = 0; i < n; ++i) { yr += v1[2 * i]; yi -= v1[2 * i + 1]; }
+          for (int i = 1; i < n; ++i) {
+            const double vr = v1[2 * i], vi = v1[2 * i + 1];
+            v[2 * i] = 1.0 - b1 * (vr * yr - vi * yi);
+            v[2 * i + 1] = -b1 * (vr * yi + vi * yr);
+          }
+        }
+        double ss = 0.0;
+        for (int i = i0; i < n; ++i) ss += v[2 * i] * v[2 * i] + v[2 * i + 1] * v[2 * i + 1];
+        const double nrm = sqrt(ss);
+        double b = 0.0;
+        if (nrm != 0.0) {
+          const double xr = v[2 * i0], xi = v[2 * i0 + 1];
+          const double a0 = sqrt(xr * xr + xi * xi);
+          const double pr = a0 > 0.0 ? xr / a0 : 1.0, pi = a0 > 0.0 ? xi / a0 : 0.0;
+          v[2 * i0] += pr * nrm;           // x0 - alpha, alpha = -phase(x0) |x|
+          v[2 * i0 + 1] += pi * nrm;
+          double vv = 0.0;
+          for (int i = i0; i < n; ++i) vv += v[2 * i] * v[2 * i] + v[2 * i + 1] * v[2 * i + 1];
+          b = 2.0 / vv;
+        }
+        if (c == 0) b1 = b; else b2 = b;
+      }
+      sv[0] = b1; sv[1] = b2;
+    }
+    __syncthreads();
+    const double b1 = sv[0], b2 = sv[1];
+    for (int k = 2 + tid; k < n; k += kT) {
+      double* u = Q + (size_t)(2 * (k - 2)) * np;       // emb(w)
+      double* ui = u + np;                              // emb(i w)
+      // H2 e_k = e_k - b2 v2 conj(v2_k)
+      const double cr = v2[2 * k], ci = -v2[2 * k + 1];
+      for (int i = 0; i < n; ++i) {
+        const double vr = v2[2 * i], vi = v2[2 * i + 1];
+        u[2 * i] = (i == k ? 1.0 : 0.0) - b2 * (vr * cr - vi * ci);
+        u[2 * i + 1] = -b2 * (vr * ci + vi * cr);
+      }
+      // H1: w -= b1 v1 (v1^H w)
+      double dr = 0.0, di = 0.0;
+      for (int i = 0; i < n; ++i) {
+        const double vr = v1[2 * i], vi = v1[2 * i + 1], wr = u[2 * i], wi = u[2 * i + 1];
+        dr += vr * wr + vi * wi;
+        di += vr * wi - vi * wr;
+      }
+      for (int i = 0; i < n; ++i) {
+        const double vr = v1[2 * i], vi = v1[2 * i + 1];
+        const double wr = u[2 * i] - b1 * (vr * dr - vi * di);
+        const double wi = u[2 * i + 1] - b1 * (vr * di + vi * dr);
+        u[2 * i] = wr; u[2 * i + 1] = wi;
+        ui[2 * i] = -wi; ui[2 * i + 1] = wr;
+      }
+    }
+  } else {
   if (tid == 0) {
     for (int q = 0; q < max(nct, nrt); ++q) {
       bool apply = false;
@@ -225,8 +299,6 @@ __global__ void __launch_bounds__(kT) basis_kernel(int n, int Fc, int f0, const 
   __syncthreads();
   // U(:, p:np) = H_0 ... H_{nct-1} e_jj, one column per thread; U(q:, q) is
   // A(q:, q) after step q (later steps never touch column q).
-  const int s = np - p;
-  double* Q = Qbuf + (size_t)part * qstride;
   for (int jj = p + tid; jj < np; jj += kT) {
     double* u = Q + (size_t)(jj - p) * np;
     for (int i = 0; i < np; ++i) u[i] = (i == jj) ? 1.0 : 0.0;
@@ -239,6 +311,7 @@ __global__ void __launch_bounds__(kT) basis_kernel(int n, int Fc, int f0, const 
       if (t != 0.0)
         for (int i = q; i < np; ++i) u[i] += t * h[i];
     }
+  }
   }
   __syncthreads();
   if (!xy) {
@@ -689,14 +762,19 @@ __global__ void __launch_bounds__(kT) nserr_kernel(const Part* parts) {
 }
 
 // after the update GEMM: count it, finish converged parts, count the rest
+// remaining[0]: parts still iterating; remaining[2]: active parts whose sign
+// iteration failed (the host skips psd_jacobi_kernel when none did)
 __global__ void __launch_bounds__(1024) nsstep_kernel(const Part* parts, int nparts, int last,
                                                       int* remaining) {
-  __shared__ int cnt;
-  if (threadIdx.x == 0) cnt = 0;
+  __shared__ int cnt, fails;
+  if (threadIdx.x == 0) { cnt = 0; fails = 0; }
   __syncthreads();
   for (int p = threadIdx.x; p < nparts; p += blockDim.x) {
     Scal& sc = *parts[p].sc;
-    if (sc.ns_done) continue;
+    if (sc.ns_done) {
+      if (!sc.inactive && sc.ns_fail_now) atomicAdd(&fails, 1);
+      continue;
+    }
     sc.ns_upd += 1;
     const int n2 = 2 * parts[p].s;
     if (sc.err2 < 1e-20 * n2 || sc.ns_upd >= kNsMax || !(sc.err2 == sc.err2)) {
@@ -708,9 +786,10 @@ __global__ void __launch_bounds__(1024) nsstep_kernel(const Part* parts, int npa
     }
     sc.err2 = 0.0;
     if (!sc.ns_done) atomicAdd(&cnt, 1);
+    else if (sc.ns_fail_now) atomicAdd(&fails, 1);
   }
   __syncthreads();
-  if (threadIdx.x == 0) *remaining = cnt;
+  if (threadIdx.x == 0) { remaining[0] = cnt; remaining[2] = fails; }
 }
 
 // the sign lives in N0 after an even number of updates, N1 after an odd one:
@@ -786,13 +865,19 @@ __global__ void __launch_bounds__(kJT) psd_jacobi_kernel(const Part* parts, doub
   }
   const double tol = 1e-30 * block_sum_all(fro, red);  // (1e-15 |A|_F)^2
   __syncthreads();
-  for (int sweep = 0; sweep < kJacobiSweeps; ++sweep) {
+  bool conv = false;
+  for (int sweep = 0; sweep <= kJacobiSweeps; ++sweep) {
     double off = 0.0;
     for (int e = tid; e < N * N; e += kJT) {
       const int i = e % N, j = e / N;
       if (i != j) off += A[e] * A[e];
     }
-    if (!(block_sum_all(off, red) > tol)) break;  // (NaN: stop, the result is NaN)
+    const double o = block_sum_all(off, red);
+    if (!(o > tol)) {              // (NaN: stop, the result is NaN -- not converged)
+      conv = o == o;
+      break;
+    }
+    if (sweep == kJacobiSweeps) break;   // off-diagonal mass left: reported below
     for (int t = 0; t < N1; ++t) {
       for (int k = tid; k < m; k += kJT) {
         int p, q;
@@ -866,7 +951,10 @@ __global__ void __launch_bounds__(kJT) psd_jacobi_kernel(const Part* parts, doub
     P.Sr[i + (size_t)j * N] = a;
     P.Sr[j + (size_t)i * N] = a;
   }
-  if (tid == 0) sc.jacobi += 1;
+  if (tid == 0) {
+    sc.jacobi += 1;
+    if (!conv) sc.jacobi_fail += 1;
+  }
 }
 
 // S = sym(Sr), Sr = (W + W sign)/2 from the GEMM; X = (S - W)/mu;
@@ -950,8 +1038,10 @@ __global__ void __launch_bounds__(kT) assemble_kernel(const Part* parts, int n, 
     G[e] = (fabs(v) > 1e-10) ? v : 0.0;
   }
   if (iters && blockIdx.x == 0 && threadIdx.x == 0) {
-    iters[2 * (f0 + fl)] = Pxy.sc->itr;
-    iters[2 * (f0 + fl) + 1] = Pz.sc->itr;
+    // negative: some PSD projection was resolved by neither the sign
+    // iteration nor kJacobiSweeps Jacobi sweeps (the gains are unreliable)
+    iters[2 * (f0 + fl)] = Pxy.sc->jacobi_fail ? -Pxy.sc->itr : Pxy.sc->itr;
+    iters[2 * (f0 + fl) + 1] = Pz.sc->jacobi_fail ? -Pz.sc->itr : Pz.sc->itr;
   }
 }
 
@@ -976,6 +1066,7 @@ struct Ctx {
   DevBuf arena0, arena1, jobs, parts;
   int* h_cnt = nullptr;  // pinned
   int* d_cnt = nullptr;
+  size_t jacobi_lds = 64 * 1024;  // psd_jacobi_kernel's dynamic-LDS limit as set
 };
 Ctx g_ctx[16];
 unsigned long long* g_flops = nullptr;  // diagnostic GEMM flop counter (device)
@@ -1028,8 +1119,8 @@ hipError_t psd_project(const JobLists& J, Part* dp, int NP, int n2max, double ep
     hipLaunchKernelGGL(nsstep_kernel, dim3(1), dim3(1024), 0, st, dp, NP,
                        it == kNsMax - 1 ? 1 : 0, X.d_cnt);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (it >= 5) {
-      if ((e = hipMemcpyAsync(X.h_cnt, X.d_cnt, sizeof(int), hipMemcpyDeviceToHost, st)) !=
+    if (it >= 5) {  // [0] still iterating, [2] failed (d_cnt[1] is check_kernel's)
+      if ((e = hipMemcpyAsync(X.h_cnt, X.d_cnt, 3 * sizeof(int), hipMemcpyDeviceToHost, st)) !=
           hipSuccess)
         return e;
       if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
@@ -1040,11 +1131,16 @@ hipError_t psd_project(const JobLists& J, Part* dp, int NP, int n2max, double ep
   hipLaunchKernelGGL(nsparity_kernel, dim3(1), dim3(1024), 0, st, dp, NP);
   if ((e = J.run(J_S, false, false, st)) != hipSuccess) return e;
   if ((e = J.run(J_S1, false, false, st)) != hipSuccess) return e;
+  // the fallback only when some part needs it (the last readback's count)
+  if (!force_jacobi && X.h_cnt[2] == 0) return hipSuccess;
   const size_t jlds = (size_t)20 * n2max;
-  if (jlds > 64 * 1024 &&
-      (e = hipFuncSetAttribute((const void*)psd_jacobi_kernel,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)jlds)) != hipSuccess)
-    return e;
+  if (jlds > X.jacobi_lds) {
+    if ((e = hipFuncSetAttribute((const void*)psd_jacobi_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)jlds)) !=
+        hipSuccess)
+      return e;
+    X.jacobi_lds = jlds;
+  }
   hipLaunchKernelGGL(psd_jacobi_kernel, dim3(NP), dim3(kJT), jlds, st, dp, eps);
   return hipGetLastError();
 }
@@ -1067,6 +1163,8 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
   acl_admm_params_t prm;
   if (params) prm = *params;
   else acl_default_admm_params(&prm);
+  if (prm.basis != ACL_ADMM_BASIS_LINPACK && prm.basis != ACL_ADMM_BASIS_COMPLEX)
+    return acl__set_error("acl_admm_solve_batch: params->basis must be ACL_ADMM_BASIS_*");
   const hipStream_t st = (hipStream_t)stream;
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -1109,7 +1207,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
               "hipFuncSetAttribute");
     hipLaunchKernelGGL(basis_kernel, dim3(NP), dim3(kT), lds, st, n, Fc, f0, pts, adj,
-                       prm.thrPlanar, Qbuf, qstride, pairbuf, pstride, d_info);
+                       prm.thrPlanar, prm.basis, Qbuf, qstride, pairbuf, pstride, d_info);
     ACL_HIP(hipGetLastError(), "basis_kernel");
     std::vector<Info> info(NP);
     ACL_HIP(hipMemcpyAsync(info.data(), d_info, NP * sizeof(Info), hipMemcpyDeviceToHost, st),
@@ -1309,7 +1407,8 @@ extern "C" void acl_internal_admm_flop_counter(unsigned long long* counter) {
 // into S = (Sr + Sr^T) / 2 exactly as an ADMM iteration makes it (Newton-
 // Schulz on the matrix cores, the Jacobi fallback where the sign iteration
 // does not converge; force_jacobi: the fallback for every matrix).
-// jacobi_used (host, may be NULL): per matrix, 1 if the fallback made it.
+// jacobi_used (host, may be NULL): per matrix, 1 if the fallback made it,
+// -1 if the fallback stopped at kJacobiSweeps unconverged.
 // Synchronous; returns 0 on success.
 extern "C" int acl_internal_psd_project(int nm, int N, const double* W, double eps, double* S,
                                         int force_jacobi, int* jacobi_used) {
@@ -1390,7 +1489,7 @@ extern "C" int acl_internal_psd_project(int nm, int N, const double* W, double e
     if (!ok) break;
     if (jacobi_used) {
       if (hipMemcpy(hs.data(), sc, nm * sizeof(Scal), hipMemcpyDeviceToHost) != hipSuccess) break;
-      for (int p = 0; p < nm; ++p) jacobi_used[p] = hs[p].jacobi;
+      for (int p = 0; p < nm; ++p) jacobi_used[p] = hs[p].jacobi_fail ? -1 : hs[p].jacobi;
     }
     rc = 0;
   } while (0);

@@ -41,6 +41,7 @@ extern "C" void acl_default_admm_params(acl_admm_params_t* a) {
   // aclswarm/lib/admm/include/admm/solver.h:18-31
   a->verbose = 0; a->thrSparseZero = 1e-8; a->thrPlanar = 1e-2; a->epsEig = 1e-5;
   a->mu = 1.0; a->thresh = 1e-4; a->threshTr = 0.10; a->maxItr = 10;
+  a->basis = ACL_ADMM_BASIS_LINPACK;
 }
 
 extern "C" void acl_formations_init(acl_formations_t* F, int32_t n, int32_t n_formations) {

@@ -184,7 +184,10 @@ def status_to_numpy(status_u8):
     return np.ascontiguousarray(arr).view(L.STATUS_DTYPE).reshape(-1)
 
 
-def admm_design(pts, adj, params=None, stream=None):
+ADMM_BASIS_LINPACK, ADMM_BASIS_COMPLEX = 0, 1   # acl_admm_params_t.basis
+
+
+def admm_design(pts, adj, params=None, stream=None, basis=None):
     """Batched ADMM formation-gain design (acl_admm_solve_batch; the
     reference's admm::Solver::solve / ADMM::calculateFormationGains,
     aclswarm/lib/admm/src/solver.cpp:28-79, aclswarm/src/admm.cpp:32-51).
@@ -193,7 +196,9 @@ def admm_design(pts, adj, params=None, stream=None):
     Returns (gains [F][3n][3n] f64 with gains[f][r][c] = GainMat(r, c),
     iters [F][2] int32: ADMM iterations of the xy and z designs; a PSD
     projection the sign iteration does not resolve is made by the Jacobi
-    eigensolver fallback).
+    eigensolver fallback). basis overrides params.basis: ADMM_BASIS_LINPACK
+    (default, the codegen's gains) or ADMM_BASIS_COMPLEX (the complex-
+    structured complement basis admm::Solver's tests need, test_admm.cpp:84-187).
     """
     lib = L.lib()
     F, n = int(pts.shape[0]), int(pts.shape[1])
@@ -203,6 +208,8 @@ def admm_design(pts, adj, params=None, stream=None):
     out = torch.empty((F, 3 * n, 3 * n), dtype=torch.float64, device=dev)
     iters = torch.empty((F, 2), dtype=torch.int32, device=dev)
     prm = params or L.default_admm_params()
+    if basis is not None:
+        prm.basis = int(basis)
     if stream is None:
         stream = torch.cuda.current_stream(dev).cuda_stream
     L.check(lib.acl_admm_solve_batch(F, n, pts.data_ptr(), adj.data_ptr(), out.data_ptr(),

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define ACL_ABI_VERSION 5
+#define ACL_ABI_VERSION 6
 
 typedef enum {
   ACL_OK = 0,
@@ -75,7 +75,17 @@ typedef struct {
   double max_vel_xy, max_vel_z, d_avoid_thresh, r_keep_out;
 } acl_safety_params_t;
 
-/* admm::Params (aclswarm/lib/admm/include/admm/solver.h:18-31). */
+/* admm::Params (aclswarm/lib/admm/include/admm/solver.h:18-31), plus the
+ * 2-D complement basis (not a reference parameter; ABI 6):
+ *   ACL_ADMM_BASIS_LINPACK (default) -- the codegen's LINPACK dsvdc columns:
+ *     gains identical to the reference's codegen ADMM (aclswarm/src/admm.cpp),
+ *     including its violation of test_admm.cpp:84-187 on that formation;
+ *   ACL_ADMM_BASIS_COMPLEX -- a complex-structured orthonormal basis of the
+ *     same complement: the design is complex-linear and meets the graph rows,
+ *     as aclswarm/test/test_admm.cpp:84-187 asserts of admm::Solver (the C++
+ *     facade's admm::Solver uses it). Same kernel, same SDP, same loop. */
+#define ACL_ADMM_BASIS_LINPACK 0
+#define ACL_ADMM_BASIS_COMPLEX 1
 typedef struct {
   int32_t verbose;
   double thrSparseZero;
@@ -85,6 +95,7 @@ typedef struct {
   double thresh;
   double threshTr;
   int32_t maxItr;
+  int32_t basis;   /* ACL_ADMM_BASIS_* */
 } acl_admm_params_t;
 
 /* Defaults: control gains from aclswarm/launch/coordination.launch:32-39,
@@ -552,7 +563,10 @@ acl_status_t acl_generate_formation_groups(int32_t F, int32_t n, const uint32_t*
  * each ADMM iteration (eigenvalues > epsEig kept, solver.cpp:296-316) is a
  * Newton-Schulz matrix-sign iteration on the matrix cores; a part whose sign
  * iteration does not converge in 64 steps (an eigenvalue within ~1e-11 |W|
- * of epsEig) is projected by a Jacobi eigendecomposition instead. */
+ * of epsEig) is projected by a Jacobi eigendecomposition instead; if that
+ * too is left unconverged after 40 sweeps the part's iters entry is the
+ * negated count (-iterations): its gains are not reliable. params->basis
+ * selects the 2-D complement basis (ACL_ADMM_BASIS_*; LINPACK by default). */
 acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double* pts,
                                   const double* adj, double* gains,
                                   int32_t* iters,

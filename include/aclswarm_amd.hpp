@@ -657,6 +657,11 @@ class Solver {
     double thresh = 1e-4;
     double threshTr = 0.10;
     size_t maxItr = 10;
+    /* not in solver.h: the 2-D complement basis (acl_admm_params_t.basis).
+     * The complex-structured basis makes solve() meet the block-structure
+     * and zero-block properties test_admm.cpp:84-187 asserts; set
+     * ACL_ADMM_BASIS_LINPACK for the codegen ADMM's exact gains. */
+    int basis = ACL_ADMM_BASIS_COMPLEX;
   };
 
   Solver() : Solver(Params()) {}
@@ -686,6 +691,7 @@ class Solver {
     p.thresh = params_.thresh;
     p.threshTr = params_.threshTr;
     p.maxItr = (int32_t)params_.maxItr;
+    p.basis = (int32_t)params_.basis;
     const size_t nn = (size_t)n * n;
     d_pts_.upload(pts_3xn, (size_t)3 * n * 8);
     d_adj_.upload(adj_nxn, nn * 8);

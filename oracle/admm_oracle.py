@@ -159,6 +159,60 @@ def kernel_2d(p_xy):
     return np.stack([qs, qsbar, one1, one2], axis=1)
 
 
+def complex_complement(p_xy):
+    """The ACL_ADMM_BASIS_COMPLEX basis of the 2-D part (not in the
+    reference): an orthonormal basis of the complement of the same kernel
+    span{qs, qsbar, one1, one2}, built complex-structured. With z = x + iy the
+    kernel is the complex span of {z, 1}; two complex Householder reflectors
+    H1, H2 triangularise [z, 1] (H = I - beta v v^H, beta = 2/|v|^2,
+    alpha = -phase(x0)|x|), w_k = H1 H2 e_k (k = 2..n-1) span the complex
+    complement, and each w_k gives the real column pair (emb(w_k),
+    emb(i w_k)), emb interleaving (Re, Im) per agent. A Q of that form
+    commutes with the 2x2 [a b; -b a] structure, so the design's output is
+    complex-linear and meets the graph rows exactly -- the properties
+    aclswarm/test/test_admm.cpp:84-187 assert, which the codegen's LINPACK
+    basis (rounding-noise sign choice, linpack_complement) violates by
+    ~1e-1 on that test's formation. Any complex-structured orthonormal basis
+    gives the same design up to rounding (the SDP and ADMM iterates are
+    equivariant under complex-unitary changes of basis). Restates
+    admm.hip basis_kernel's basis == 1 branch, same operation order."""
+    p_xy = np.asarray(p_xy, dtype=np.float64)
+    n = p_xy.shape[0]
+    z = p_xy[:, 0] + 1j * p_xy[:, 1]
+
+    def reflector(x):
+        nrm = math.sqrt(float(np.sum(x.real * x.real + x.imag * x.imag)))
+        if nrm == 0.0:
+            return None, 0.0
+        a0 = abs(x[0])
+        ph = x[0] / a0 if a0 > 0.0 else 1.0
+        v = x.copy()
+        v[0] += ph * nrm                   # x0 - alpha, alpha = -ph |x|
+        vv = float(np.sum(v.real * v.real + v.imag * v.imag))
+        return v, 2.0 / vv
+
+    v1, b1 = reflector(z)
+    y = np.ones(n, dtype=np.complex128)
+    if v1 is not None:
+        y = y - b1 * v1 * np.vdot(v1, y)
+    v2, b2 = reflector(y[1:])
+    W = np.zeros((n, n - 2), dtype=np.complex128)
+    for k in range(2, n):
+        w = np.zeros(n, dtype=np.complex128)
+        w[k] = 1.0
+        if v2 is not None:
+            w[1:] -= b2 * v2 * np.conj(v2[k - 1])
+        if v1 is not None:
+            w -= b1 * v1 * np.vdot(v1, w)
+        W[:, k - 2] = w
+    Q = np.zeros((2 * n, 2 * (n - 2)))
+    Q[0::2, 0::2] = W.real
+    Q[1::2, 0::2] = W.imag
+    Q[0::2, 1::2] = -W.imag
+    Q[1::2, 1::2] = W.real
+    return Q
+
+
 def kernel_z(qz):
     """[qz, 1], or [1] for a planar formation: std(qz) < 1e-2 with MATLAB's
     n-1 normalisation (ADMMGainDesign3D.m:30-46, codegen 3D.cpp:196)."""
@@ -317,8 +371,14 @@ class Part:
         return self.Q @ (-X22) @ self.Q.T, itr
 
 
-def design_2d(p_xy, adj, **kw):
-    Q = linpack_complement(kernel_2d(p_xy))
+BASIS_LINPACK, BASIS_COMPLEX = 0, 1     # acl_admm_params_t.basis
+
+
+def design_2d(p_xy, adj, basis=BASIS_LINPACK, **kw):
+    if basis == BASIS_COMPLEX and np.asarray(p_xy).shape[0] > 2:
+        Q = complex_complement(p_xy)
+    else:
+        Q = linpack_complement(kernel_2d(p_xy))
     pairs = []
     for (i, j) in nonedges(adj):
         pairs.append((2 * i, 2 * j))
@@ -333,12 +393,14 @@ def design_z(qz, adj, **kw):
     return Part(Q, pairs, False).run(**kw)
 
 
-def design_3d(p, adj, prune=True, **kw):
+def design_3d(p, adj, prune=True, basis=BASIS_LINPACK, **kw):
     """ADMMGainDesign3D (+ the |a| < 1e-10 zeroing of admm.cpp:50). p: n x 3.
-    Returns (Aopt 3n x 3n, (iters_xy, iters_z))."""
+    basis selects the 2-D complement basis (BASIS_LINPACK = codegen parity,
+    BASIS_COMPLEX = complex_complement). Returns (Aopt 3n x 3n,
+    (iters_xy, iters_z))."""
     p = np.asarray(p, dtype=np.float64)
     n = p.shape[0]
-    Axy, it_xy = design_2d(p[:, :2], adj, **kw)
+    Axy, it_xy = design_2d(p[:, :2], adj, basis=basis, **kw)
     Az, it_z = design_z(p[:, 2].copy(), adj, **kw)
     A = np.zeros((3 * n, 3 * n))
     for i in range(n):

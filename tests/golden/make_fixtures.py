@@ -161,6 +161,29 @@ def admm_test_fixture():
                  "adj": adj_nc, "A": noncomplete}]}
 
 
+def admm_nine_fixture():
+    # aclswarm/test/test_admm.cpp:84-187 (nineAgentSquareNonCompleteZeroBlocks,
+    # ...BlockStructure): inputs only -- the test asserts properties, not a
+    # matrix: zero 3x3 blocks at the non-edges (sum < 1e-8) and every block of
+    # the form [a b 0; -b a 0; 0 0 c] (one-sided "< 1e-8" checks, :165-171).
+    n = 9
+    adj = [[0 if i == j else 1 for j in range(n)] for i in range(n)]
+    for i, j in [(0, 6), (2, 4), (5, 7), (5, 8), (6, 7),
+                 (4, 2), (6, 0), (7, 5), (7, 6), (8, 5)]:
+        adj[i][j] = 0
+    p = [[-1.7484733199059646, 1.7306756147165174, 0.2977622220453062],
+         [6.8174866001631180, -6.2778267151168700, 1.7416024649609380],
+         [-3.8137004331127518, -2.3232057308608365, 0.4655014204423282],
+         [2.7536551200474015, -5.5700708736518450, 1.7252000594155040],
+         [-3.5935365621834463, 4.8028457222331170, 1.2981050175550286],
+         [-2.5820075847777666, 7.4136205487374910, 1.5131454738258028],
+         [0.8900655441583734, 3.2902893860285527, 1.5581930129432586],
+         [0.4370445360276376, -5.7714142992744755, 0.2531727259898202],
+         [-6.1065377928157310, -5.7852241311701940, 1.7663507973073431]]
+    return {"source": "aclswarm/test/test_admm.cpp:84-187", "tol": 1e-8,
+            "name": "nineAgentSquareNonComplete", "p": p, "adj": adj}
+
+
 SETS = [
     ("simform20_fc", 20, True, 15.0, range(0, 8)),
     ("simform20_nc", 20, False, 15.0, range(0, 8)),
@@ -170,8 +193,14 @@ SETS = [
 
 
 def main():
-    grf, assignment = _import_reference_modules()
     only = sys.argv[1:]
+    if only == ["admm"]:   # data transcribed from test_admm.cpp; no imports
+        with open(os.path.join(OUT, "admm_test_admm.json"), "w") as f:
+            json.dump(admm_test_fixture(), f)
+        with open(os.path.join(OUT, "admm_nine_agent.json"), "w") as f:
+            json.dump(admm_nine_fixture(), f)
+        return
+    grf, assignment = _import_reference_modules()
     if only:
         for name, n, fc, L, seeds in SETS:
             if name in only:
@@ -190,6 +219,8 @@ def main():
         json.dump(hungarian_fixture(assignment, grf), f)
     with open(os.path.join(OUT, "admm_test_admm.json"), "w") as f:
         json.dump(admm_test_fixture(), f)
+    with open(os.path.join(OUT, "admm_nine_agent.json"), "w") as f:
+        json.dump(admm_nine_fixture(), f)
     print("fixtures written to", OUT)
 
 

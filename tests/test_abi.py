@@ -39,6 +39,8 @@ def test_defaults_match_reference_values():
     a = L.default_admm_params()  # solver.h:18-31
     assert (a.thrSparseZero, a.thrPlanar, a.epsEig, a.mu, a.thresh, a.threshTr, a.maxItr) == \
         (1e-8, 1e-2, 1e-5, 1.0, 1e-4, 0.10, 10)
+    assert a.basis == 0   # ACL_ADMM_BASIS_LINPACK: codegen parity by default
+    assert ct.sizeof(L.AdmmParams) == 64  # basis sits in maxItr's old tail padding
     assert L.lib().acl_max_vehicles() == 512
 
 
@@ -120,14 +122,15 @@ def test_status_record_is_16_bytes():
 
 
 def test_abi_version_and_formations_init():
-    """ABI 5 (gains_tiled in acl_formations_t, margin in the status, gate
-    margins, the episode's auction latency and pending state): acl_formations_init zero-fills the struct so no optional pointer
+    """ABI 6 (ABI 5: gains_tiled in acl_formations_t, margin in the status,
+    gate margins, the episode's auction latency and pending state; ABI 6:
+    acl_admm_params_t.basis): acl_formations_init zero-fills the struct so no optional pointer
     is left as garbage; the solve rejects an empty formation table."""
     from aclswarm_amd import _lib as L
     with open(os.path.join(ROOT, "include", "aclswarm_amd.h")) as f:
-        assert "#define ACL_ABI_VERSION 5" in f.read()
+        assert "#define ACL_ABI_VERSION 6" in f.read()
     lib = L.lib()
-    assert lib.acl_abi_version() == 5 == L.ABI_VERSION  # the load-time check's inputs
+    assert lib.acl_abi_version() == 6 == L.ABI_VERSION  # the load-time check's inputs
     F = L.Formations()
     ct.memset(ct.byref(F), 0xAB, ct.sizeof(F))
     lib.acl_formations_init(ct.byref(F), 100, 7)

@@ -19,13 +19,13 @@ REL_TOL = 1e-5  # north_star: ADMM gains within 1e-5 relative (fp64)
 CASES = AC.load()
 
 
-def _gpu(ps, adjs):
+def _gpu(ps, adjs, basis=None):
     import torch
     from aclswarm_amd import engine
     dev = torch.device("cuda:0")
     pts = torch.from_numpy(np.ascontiguousarray(np.stack(ps), dtype=np.float64)).to(dev)
     adj = torch.from_numpy(np.ascontiguousarray(np.stack(adjs), dtype=np.float64)).to(dev)
-    A, its = engine.admm_design(pts, adj)
+    A, its = engine.admm_design(pts, adj, basis=basis)
     torch.cuda.synchronize()
     return A.cpu().numpy(), its.cpu().numpy()
 
@@ -61,6 +61,37 @@ def test_admm_test_admm_goldens():
                 [np.array(c["adj"], dtype=np.float64) for c in d["cases"]])
     for k, c in enumerate(d["cases"]):
         assert np.linalg.norm(A[k] - np.array(c["A"])) < d["tol"]
+
+
+def test_admm_complex_basis_nine_agent():
+    """ACL_ADMM_BASIS_COMPLEX (acl_admm_params_t.basis = 1): the nine-agent
+    formation of aclswarm/test/test_admm.cpp:84-187 meets both of that test's
+    assertions at 1e-8 (zero non-edge blocks, [a b 0; -b a 0; 0 0 c] blocks),
+    the MATLAB 12 x 12 matrices (:10-80) still match, and every result equals
+    the oracle's complex-basis design (1e-5 relative, same iteration counts)
+    on a batch mixing the fixture sizes. The default basis is covered by the
+    codegen-parity tests above; its nine-agent violation is recorded in
+    tests/test_admm.py::test_nine_agent_codegen_basis_recorded."""
+    from test_admm import nine_agent_violations
+    d = H.load_json("admm_nine_agent.json")
+    g = H.load_json("admm_test_admm.json")
+    adj9 = np.array(d["adj"], dtype=np.float64)
+    A, its = _gpu([np.array(d["p"])], [adj9], basis=O.BASIS_COMPLEX)
+    zs, worst = nine_agent_violations(A[0], adj9)
+    assert abs(zs) < d["tol"] and worst < d["tol"], (zs, worst)
+    A, its = _gpu([np.array(c["p"]) for c in g["cases"]],
+                  [np.array(c["adj"], dtype=np.float64) for c in g["cases"]],
+                  basis=O.BASIS_COMPLEX)
+    for k, c in enumerate(g["cases"]):
+        assert np.linalg.norm(A[k] - np.array(c["A"])) < g["tol"]
+    for n in (5, 9, 20):
+        cs = [c for c in CASES if c["p"].shape[0] == n][:8]
+        A, its = _gpu([c["p"] for c in cs], [c["adj"].astype(np.float64) for c in cs],
+                      basis=O.BASIS_COMPLEX)
+        for k, c in enumerate(cs):
+            Ao, ito = O.design_3d(c["p"], c["adj"], basis=O.BASIS_COMPLEX)
+            assert AC.rel_err(A[k], Ao) < REL_TOL, (c["name"], AC.rel_err(A[k], Ao))
+            assert tuple(int(x) for x in its[k]) == tuple(ito), (c["name"], its[k], ito)
 
 
 def test_admm_mixed_batch_properties():

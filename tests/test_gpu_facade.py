@@ -117,3 +117,23 @@ def test_facade_simform20(tmp_path, name):
     P_in = H.random_perm(rng, 20)
     got = _run(tmp_path, p, adj, gains, q, vel, P_in)
     _check(got, p, adj, gains, q, vel, P_in)
+
+
+def test_facade_admm_solver_nine_agent(tmp_path):
+    """The facade's admm::Solver (basis ACL_ADMM_BASIS_COMPLEX by default)
+    passes aclswarm/test/test_admm.cpp:84-187 on that test's own nine-agent
+    formation: zero non-edge blocks and [a b 0; -b a 0; 0 0 c] blocks at the
+    test's 1e-8."""
+    from test_admm import nine_agent_violations
+    pts, adj, gains, q0 = H.swarm6()
+    rng = np.random.RandomState(62)
+    q = q0 + rng.normal(0, 0.3, q0.shape)
+    vel = rng.normal(0, 0.1, q.shape)
+    P_in = H.random_perm(rng, 6)
+    d = H.load_json("admm_nine_agent.json")
+    adj9 = np.array(d["adj"], np.float64)
+    got = _run(tmp_path, pts[1], adj[1], gains[1], q, vel, P_in,
+               pts=np.array(d["p"], np.float64), adjf=adj9)
+    zs, worst = nine_agent_violations(got["A"], adj9)
+    assert abs(zs) < d["tol"] and worst < d["tol"], (zs, worst)
+    assert (got["iters"] > 0).all()
