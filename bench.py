@@ -543,17 +543,21 @@ def main():
         del outc, qc
 
     # algorithmic bytes per launch (every kernel is one launch over all B).
-    # n <= 128 with 5-plane records: the control phase runs inside the
-    # auction's workgroups (one fused launch carries every byte); the directed
-    # gain kernel then runs only for swarms with per-vehicle rows (none here).
+    # 5-plane records: the control phase runs inside the auction's workgroups
+    # (one fused launch carries every byte; n > 128: the wide kernel's
+    # wide_control); the directed gain kernel then runs only for swarms with
+    # per-vehicle rows (none here).
     a_all, g_all, s_all, e_avg = algorithmic_bytes(w, 0, B)
-    fused = n <= 128 and w["planes"] == 5
+    fused = w["planes"] == 5
     if fused:
         per_launch = {"auction": a_all + g_all, "gain": 0, "ca": s_all}
         auction_sym = ("acl_amd::auction_kernel<1, 128, true, false>" if n <= 32 else
                        "acl_amd::auction_kernel<1, 256, true, false>" if n <= 64 else
-                       "acl_amd::auction_kernel<2, 512, true, false>")
-        gain_sym = f"acl_amd::gain_kernel<{w['planes']}, false>"
+                       "acl_amd::auction_kernel<2, 512, true, false>" if n <= 128 else
+                       "acl_amd::solve_wide_kernel<true, false>")
+        gain_sym = (f"acl_amd::gain_kernel<{w['planes']}, false>" if n <= 128 else
+                    f"acl_amd::gain_kernel<{w['planes']}, false, 1024>")
+        align_sym = "acl_amd::align_kernel<2>" if n <= 128 else "acl_amd::align_wide_kernel"
     else:
         per_launch = {"auction": a_all, "gain": g_all, "ca": s_all}
         auction_sym = (("acl_amd::auction_kernel<1, 128, false, false>" if n <= 32 else
@@ -579,22 +583,31 @@ def main():
     if fused:
         kern["auction"]["what"] = ("fused: CBAA, adoption, then DistCntrl + saturation + the "
                                    "collision test in the same workgroup; for n > 64 the "
-                                   "alignment runs as its own launch just before "
-                                   "(acl_amd::align_kernel<2>), timed with it")
+                                   f"alignment runs as its own launch just before ({align_sym}), "
+                                   "timed with it")
         kern["gain"]["what"] = "directed gain kernel for swarms with per-vehicle rows only"
-    # the auction kernel is LDS/VALU/SALU-issue bound: its issue rates from the
-    # committed SQ counters of the same configuration (scripts/gpu_pmc_auction.sh)
+    # the auction kernel is bound by an issue port, not HBM: its utilisation
+    # from the committed SQ counters of the same configuration
+    # (scripts/gpu_pmc_auction.sh -> scripts/pmc_auction_summary.py).
+    # VALU: SQ_ACTIVE_INST_VALU x 4 / SIMD-cycles (fp64 VALU ops occupy a
+    # SIMD for several cycles, which instruction counts under-read);
+    # SALU and LDS: instructions per CU-cycle at one issue per cycle.
     iss, isrc = committed_profile("pmc_auction", n, B, auction_sym)
     if iss:
         kern["auction"]["issue"] = dict(iss, source=isrc)
-        # the auction's own roofline: its busiest issue port (SQ counters of
-        # the same configuration, scaled to this run's kernel time)
-        ports = {p: iss[p + "_issue_frac"] * iss_ms / kern["auction"]["avg_launch_ms"]
-                 for p in ("salu", "valu", "lds") if p + "_issue_frac" in iss
-                 for iss_ms in [iss.get("kernel_ms") or kern["auction"]["avg_launch_ms"]]}
+        # the auction's own roofline: its busiest port, scaled from the
+        # profiled kernel time to this run's
+        iss_ms = iss.get("kernel_ms") or kern["auction"]["avg_launch_ms"]
+        scale = iss_ms / kern["auction"]["avg_launch_ms"]
+        ports = {}
+        if "valu_active" in iss:
+            ports["valu-active"] = iss["valu_active"] * scale
+        for p in ("salu", "lds"):
+            if p + "_issue_frac" in iss:
+                ports[p + "-issue"] = iss[p + "_issue_frac"] * scale
         if ports:
             top = max(ports, key=ports.get)
-            kern["auction"]["roofline"] = {"bound": top + "-issue", "frac": ports[top],
+            kern["auction"]["roofline"] = {"bound": top, "frac": ports[top],
                                            "ports": ports, "source": isrc}
     pipe_bytes = a_all + g_all + s_all
     pipe_ach = pipe_bytes / (call_ms * 1e-3) / 1e9
@@ -602,7 +615,7 @@ def main():
     if fused and n > 64:
         # the alignment launch that precedes the fused one (its inputs and the
         # workspace round trip of its results) is in the same timed window
-        am, _ = (committed_profile("pmc_traffic", n, B, "acl_amd::align_kernel<2>")
+        am, _ = (committed_profile("pmc_traffic", n, B, align_sym)
                  if args.formations == 0 else (None, None))
         tr.append(am["hbm_bytes"] if am else None)
         kern["auction"]["traffic_align_kernel"] = am["hbm_bytes"] if am else None
@@ -658,8 +671,9 @@ def main():
                             "bytes_per_launch": gk["bytes_per_launch"],
                             "traffic": gk["traffic"], "traffic_source": gk["traffic_source"]},
             "note": "frac is the whole call's HBM fraction (the north-star quantity); the "
-                    "gain stream carries nearly all algorithmic bytes (`gain_kernel`); the "
-                    "auction is LDS/VALU/SALU-issue bound (kernels.auction.issue)",
+                    "gain stream carries nearly all algorithmic bytes (" +
+                    ("inside the fused auction launch" if fused else "`gain_kernel`") +
+                    "); the CBAA rounds are issue-port bound (kernels.auction.roofline)",
             "kernels": kern,
         },
         "ca_probe": ca_probe,

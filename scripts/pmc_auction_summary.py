@@ -10,6 +10,9 @@ issue. frac = instructions / (kernel time x clock x 256 CUs x that rate),
 with the kernel time of the unprofiled run (the `auction-only ... ms` line of
 out_1.txt) and the 2.4 GHz peak clock: a lower bound on the busy fraction
 when the chip clocks lower. SQ_*_CYCLES counters count quad-cycles (x4).
+VALU is reported as VALU-active as well: SQ_ACTIVE_INST_VALU x 4 / (kernel
+cycles x 256 CUs x 4 SIMDs) -- an fp64 VALU op holds its SIMD for several
+cycles, so the instruction-count model under-reads a fp64-heavy kernel.
 
 Usage: python scripts/pmc_auction_summary.py gpurun_out/pmca profiles/r2_pmc_auction.json
 """
@@ -38,7 +41,8 @@ def main(src, dst):
     out = {"source": "rocprofv3 --pmc (two passes of SQ counters, counters only) of "
                      "`python3 scripts/auction_only.py` (scripts/gpu_pmc_auction.sh)",
            "model": "frac = insts / (kernel_ms x 2.4 GHz x 256 CUs x issue rate per CU-cycle: "
-                    "SALU 1, VALU 2 (wave64 on 4 x SIMD-32), LDS 1); *_CYCLES are quad-cycles",
+                    "SALU 1, VALU 2 (wave64 on 4 x SIMD-32), LDS 1); *_CYCLES are quad-cycles; "
+                    "valu_active = SQ_ACTIVE_INST_VALU x 4 / (kernel cycles x 256 CUs x 4 SIMDs)",
            "config": {"n": n, "B_per_gpu": B, "kernel_ms": ms},
            "kernels": {}}
     for k, cv in vals.items():
@@ -50,6 +54,8 @@ def main(src, dst):
         for c, rate in RATE.items():
             if c in avg:
                 e[c.replace("SQ_INSTS_", "").lower() + "_issue_frac"] = avg[c] / (cyc * rate)
+        if "SQ_ACTIVE_INST_VALU" in avg:
+            e["valu_active"] = avg["SQ_ACTIVE_INST_VALU"] * 4.0 / (cyc * 4.0)
         if "SQ_WAVE_CYCLES" in avg and "SQ_WAIT_ANY" in avg:
             e["wait_any_share"] = avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"]
         if "SQ_WAVE_CYCLES" in avg and "SQ_ACTIVE_INST_ANY" in avg:
