@@ -1,14 +1,26 @@
 // solve.hip -- host entry points of the batched solve (C ABI).
 //
-// acl_solve_batch runs three stream-ordered launches:
-//   1. the auction kernel over all B swarms -- auction.hip for n <= 128
-//      (one workgroup per swarm, every table in LDS), solve_wide.hip for
-//      128 < n <= 512 (tables in the workspace);
-//   2. the gain kernel (DistCntrl::compute, distcntrl.cpp:46-102) and
-//   3. the collision-avoidance kernel over the vehicles the gain kernel
-//      listed (Safety, safety.cpp:172-197, 412-541) -- control.hip.
-// acl_control_batch runs 2-3 for a given assignment; acl_tile_gains
-// re-lays 5-plane gain records for the tiled pair kernel.
+// acl_solve_batch enqueues, stream-ordered, over all B swarms:
+//   1. the alignment launch (n > 64): align_kernel<2> (auction.hip, one wave
+//      per swarm) for 64 < n <= 128, align_wide_kernel (solve_wide.hip, one
+//      1 024-thread workgroup per swarm) for n > 128; n <= 64 aligns inside
+//      the auction workgroup;
+//   2. the auction launch: auction_kernel (auction.hip, n <= 128, every CBAA
+//      table in LDS) or solve_wide_kernel (solve_wide.hip, n <= 512, the
+//      `who` table in the workspace). With 5-entry gain records and
+//      do_control it is FUSED: a swarm whose vehicles all adopted one
+//      assignment runs DistCntrl::compute (distcntrl.cpp:46-102), saturation
+//      and the first collision test (safety.cpp:172-197, 412-430) in its own
+//      workgroup after adoption (pair_fused.h for n <= 128, wide_control for
+//      n > 128);
+//   3. the gain launch (control.hip): the directed walk for the swarms the
+//      fused phase did not take (per-vehicle assignments, 9-plane records,
+//      or every swarm when not fused) -- an early exit for the others;
+//   4. the collision-avoidance launch (control.hip: ca_pair_kernel for
+//      n <= 128, ca_kernel above) over the vehicles step 2/3 listed
+//      (Safety::collisionAvoidance, safety.cpp:412-541).
+// acl_control_batch runs 3-4 for a given assignment (the pair kernel for
+// uniform swarms); acl_tile_gains re-lays 5-entry records for it.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>

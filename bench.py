@@ -595,10 +595,10 @@ def main():
     iss, isrc = committed_profile("pmc_auction", n, B, auction_sym)
     if iss:
         kern["auction"]["issue"] = dict(iss, source=isrc)
-        # the auction's own roofline: its busiest port, scaled from the
-        # profiled kernel time to this run's
-        iss_ms = iss.get("kernel_ms") or kern["auction"]["avg_launch_ms"]
-        scale = iss_ms / kern["auction"]["avg_launch_ms"]
+        # the auction's own roofline: its busiest port as profiled (a ratio
+        # of the profiled run's counters to its own kernel time; this run's
+        # `avg_launch_ms` also spans the alignment launch)
+        scale = 1.0
         ports = {}
         if "valu_active" in iss:
             ports["valu-active"] = iss["valu_active"] * scale

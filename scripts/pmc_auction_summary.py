@@ -7,8 +7,8 @@ Issue model (MI355X_MICROARCH.md; cdna_hip_programming.md "CU = 4 x SIMD-32"):
 per CU and cycle at most one scalar instruction, two wave64 vector
 instructions (four SIMD-32 units, 2 cycles each) and one LDS instruction
 issue. frac = instructions / (kernel time x clock x 256 CUs x that rate),
-with the kernel time of the unprofiled run (the `auction-only ... ms` line of
-out_1.txt) and the 2.4 GHz peak clock: a lower bound on the busy fraction
+with the kernel's mean duration from the kernel-trace pass of the same
+command (trace.csv; else the call time of out_1.txt) and the 2.4 GHz peak clock: a lower bound on the busy fraction
 when the chip clocks lower. SQ_*_CYCLES counters count quad-cycles (x4).
 VALU is reported as VALU-active as well: SQ_ACTIVE_INST_VALU x 4 / (kernel
 cycles x 256 CUs x 4 SIMDs) -- an fp64 VALU op holds its SIMD for several
@@ -45,10 +45,21 @@ def main(src, dst):
                     "valu_active = SQ_ACTIVE_INST_VALU x 4 / (kernel cycles x 256 CUs x 4 SIMDs)",
            "config": {"n": n, "B_per_gpu": B, "kernel_ms": ms},
            "kernels": {}}
+    # the kernel's own duration from the kernel-trace pass (trace.csv), when
+    # present; otherwise the whole solve call's time (an upper bound)
+    kdur = collections.defaultdict(list)
+    tp = os.path.join(src, "trace.csv")
+    if os.path.exists(tp):
+        for r in csv.DictReader(open(tp)):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            kdur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
     for k, cv in vals.items():
         avg = {c: sum(v) / len(v) for c, v in cv.items()}
-        cyc = ms * 1e-3 * CLOCK_HZ * CUS
-        e = {"kernel_ms": ms, "per_dispatch": avg,
+        kms = sum(kdur[k]) / len(kdur[k]) if kdur.get(k) else ms
+        cyc = kms * 1e-3 * CLOCK_HZ * CUS
+        e = {"kernel_ms": kms, "call_ms": ms,
+             "kernel_ms_source": "trace.csv (kernel-trace pass)" if kdur.get(k) else "call time",
+             "per_dispatch": avg,
              "per_swarm": {c: avg[c] / B for c in ("SQ_INSTS_SALU", "SQ_INSTS_VALU", "SQ_INSTS_LDS")
                            if c in avg}}
         for c, rate in RATE.items():
