@@ -115,7 +115,7 @@ EPISODE_STATUS_DTYPE = np.dtype([("converged_step", "<i4"), ("gridlock_step", "<
                                  ("n_skipped", "<u2"), ("n_disagree", "<u2"),
                                  ("n_samples", "<u4"), ("n_ca_steps", "<u4"),
                                  ("pending_step", "<i4"), ("n_restarted", "<u2"),
-                                 ("reserved", "<u2")])
+                                 ("per_vehicle", "<u2")])
 
 
 class EpisodeArgs(ct.Structure):

@@ -1288,6 +1288,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         const int v = k / n, jj = k - v * n;
         rows[k] = validv[v] ? T[v * TS + jj] : Ptin[jj];
       }
+      for (int v = tid; v < n; v += kAB) P.ws[P.W.vvalid + (size_t)b * n + v] = validv[v];
     }
     if (tid == 0) {
       acl_swarm_status_t st = {};

@@ -1261,7 +1261,8 @@ __global__ void __launch_bounds__(kCaPT, 4) ca_pair_kernel(const CtlParams P) {
 
 // acl_control_batch's hand-off: P must be a permutation (else BAD_INPUT and
 // zero commands, as for the auction's P_in); the inverse assignment is the
-// shared row the gain kernel reads.
+// shared row the gain kernel reads. Episodes: swarms flagged in P.keep keep
+// their per-vehicle rows; the others' P is also copied to P.seed_out.
 __global__ void __launch_bounds__(256) control_prep_kernel(const CtlParams P,
                                                            const uint16_t* Pg) {
   __shared__ unsigned long long seen[kMaxNWide / 64];
@@ -1270,6 +1271,14 @@ __global__ void __launch_bounds__(256) control_prep_kernel(const CtlParams P,
   if (tid < kMaxNWide / 64) seen[tid] = 0ull;
   if (tid == 0) bad = 0;
   __syncthreads();
+  if (P.keep && P.keep[(size_t)b * P.keep_stride]) {
+    // an episode swarm flying per-vehicle tables (already in wsRows)
+    if (tid == 0) {
+      const_cast<uint8_t*>(P.wsMode)[b] = 1;
+      P.status[b] = acl_swarm_status_t{};
+    }
+    return;
+  }
   uint16_t* wsPt = const_cast<uint16_t*>(P.wsPt) + (size_t)b * n;
   const int f = P.fidx[b];
   if (tid == 0 && (f < 0 || f >= P.F)) bad = 1;  // formation index out of range
@@ -1282,6 +1291,7 @@ __global__ void __launch_bounds__(256) control_prep_kernel(const CtlParams P,
       if (atomicOr(&seen[pv >> 6], bit) & bit) bad = 1;
       wsPt[pv] = (uint16_t)v;
     }
+    if (P.seed_out) P.seed_out[(size_t)b * n + v] = (uint16_t)pv;
   }
   __syncthreads();
   if (tid == 0) {

@@ -57,7 +57,8 @@ constexpr int kMaxNWide = 512;  // tables-in-HBM auction kernel (solve_wide.hip)
 //           n > 128 align_wide_kernel's (out [n][6] per vehicle, vadj
 //           [NW][n] u64, u64 gap, u32 flags)
 struct WsLayout {
-  size_t pt, mode, rows, u, calist, cacount, camask, wide, wide_stride, align, align_stride, total;
+  size_t pt, mode, rows, vvalid, u, calist, cacount, camask, wide, wide_stride, align, align_stride,
+      total;
 };
 
 __host__ __device__ inline size_t ws_al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -69,6 +70,7 @@ __host__ __device__ inline WsLayout ws_layout(int n, int B) {
   W.pt = o;      o = ws_al(o + bb * nb * 2);
   W.mode = o;    o = ws_al(o + bb);
   W.rows = o;    o = ws_al(o + bb * nb * nb * 2);
+  W.vvalid = o;  o = ws_al(o + bb * nb);  // [B][n] u8: vehicle's own table valid (rows swarms)
   W.u = o;       o = ws_al(o + bb * nb * 3 * 8);
   W.calist = o;  o = ws_al(o + bb * 4);
   W.cacount = o; o = ws_al(o + 16);
@@ -118,6 +120,12 @@ struct CtlParams {
   int F;                // formations in the table (fidx range check of the hand-off)
   double* gate_margin;  // [B] optional: min | |e| - thr | / thr of the swarm's gates
   unsigned long long* stamps;  // diagnostic (SolveParams::stamps; NULL = off)
+  // control_prep_kernel, episodes only (NULL otherwise): a swarm with
+  // keep[b * keep_stride] != 0 flies per-vehicle tables already in wsRows
+  // (mode 1, no permutation check); seed_out[b] <- P for the others
+  const uint8_t* keep = nullptr;
+  int keep_stride = 0;
+  uint16_t* seed_out = nullptr;
 };
 
 struct SolveParams {
@@ -172,9 +180,14 @@ hipError_t launch_control_prep(const CtlParams& P, const uint16_t* Pgiven, int n
 // kernel (permutation check, inverse assignment, status), CTL_RESET zeroes
 // the collision-avoidance count first; without them the hand-off of the
 // previous call with the same P and workspace is reused (acl_episode_batch).
-enum { CTL_PREP = 1, CTL_RESET = 2 };
+// CTL_MIXED: some swarms may hold per-vehicle tables (mode 1): the directed
+// gain kernel runs after the pair kernel for them.
+enum { CTL_PREP = 1, CTL_RESET = 2, CTL_MIXED = 4 };
 acl_status_t run_control(const acl_formations_t* F, const acl_control_args_t* a, hipStream_t s,
                          int flags);
+// the control stage's parameters for (F, a) (argument checks as
+// acl_control_batch); ACL_OK or the error set
+acl_status_t ctl_params(const acl_formations_t* F, const acl_control_args_t* a, CtlParams& C);
 
 // The n <= 128 auction kernel (auction.hip).
 // fuse: the control phase runs in the auction's workgroups (P.ctl; 5-plane

@@ -20,6 +20,7 @@
 // one IEEE rounding, so the trajectory step and the supervisor's window sums
 // are bit-identical to the restatement in oracle/episode_oracle.py.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/aclswarm_amd.h"
@@ -31,10 +32,14 @@ namespace acl_amd {
 
 constexpr int kEpBlock = 128;
 
-// Episode workspace: the solve/control workspace, then the auction's output
-// and the control stage's output of the current step.
+// Episode workspace: the auction's solve workspace, the control stage's own
+// hand-off region (the head of a WsLayout: pt, mode, rows, ...; kept apart
+// so that an auction still pending does not overwrite the tables the
+// vehicles fly meanwhile), the auction's output, the control stage's output
+// of the current step, and the next auction's P_in (`seed`: the last agreed
+// assignment, which differs from P while a swarm flies per-vehicle tables).
 struct EpLayout {
-  size_t solve, Pnew, st, cst, u, us, ca, lat, total;
+  size_t solve, ctl, seed, Pnew, st, cst, u, us, ca, lat, total;
 };
 
 inline EpLayout ep_layout(int n, int B) {
@@ -42,6 +47,8 @@ inline EpLayout ep_layout(int n, int B) {
   const size_t nb = (size_t)n, bb = (size_t)B;
   size_t o = 0;
   L.solve = o; o = ws_al(o + ws_layout(n, B).total);
+  L.ctl = o;   o = ws_al(o + ws_layout(n, B).wide);  // pt .. camask: what run_control uses
+  L.seed = o;  o = ws_al(o + bb * nb * 2);
   L.Pnew = o;  o = ws_al(o + bb * nb * 2);
   L.st = o;    o = ws_al(o + bb * sizeof(acl_swarm_status_t));
   L.cst = o;   o = ws_al(o + bb * sizeof(acl_swarm_status_t));
@@ -100,54 +107,106 @@ __global__ void __launch_bounds__(64) latency_kernel(int n, const int32_t* fidx,
 //   -- and completes after lat[b] steps (lat == NULL or 0: now).
 // mode 1 (every other step when auctions take time): a pending auction whose
 //   step has come completes.
-// Completion (auctioneer.cpp:250-295): an agreed valid result is adopted, an
-// agreed invalid one sets the flag, a disagreeing swarm keeps its assignment.
-// wsPt / wsMode (mode 1): the control hand-off of a swarm that adopts is
-// rebuilt here (the inverse of its new permutation), so a step where no
-// pending auction completes needs no hand-off pass over every swarm.
-__global__ void __launch_bounds__(64) adopt_kernel(int n, int step, int mode, const int32_t* lat,
-                                                   uint16_t* P, const uint16_t* Pnew,
-                                                   const acl_swarm_status_t* st, uint8_t* flush,
-                                                   acl_episode_status_t* est, uint16_t* wsPt,
-                                                   uint8_t* wsMode) {
-  const int b = blockIdx.x, tid = threadIdx.x;
-  __shared__ int take;
+// Completion, each vehicle as auctioneer.cpp:250-295 (oracle
+// episode_oracle.adopt): agreed and valid -- every vehicle adopts the one
+// table (P, seed, the control stage's shared row); agreed and invalid -- all
+// keep theirs and the swarm skips its next auto-auction; disagreement -- each
+// vehicle whose own final table is valid adopts it (its row of the auction's
+// per-vehicle hand-off, vvalid), the others keep their own, and the swarm
+// flies per-vehicle tables (control mode 1, est.per_vehicle) until an agreed
+// valid auction. The control hand-off (ctlPt / ctlMode / ctlRows, and the
+// control status cst) is written here, so no hand-off pass runs per step.
+struct AdoptArgs {
+  int n, step, mode;
+  const int32_t* lat;
+  uint16_t* P;
+  uint16_t* seed;
+  const uint16_t* Pnew;
+  const acl_swarm_status_t* st;
+  const uint16_t* sRows;   // the auction's per-vehicle rows / validity (solve workspace)
+  const uint8_t* sValid;
+  uint8_t* flush;
+  acl_episode_status_t* est;
+  uint16_t* ctlPt;
+  uint8_t* ctlMode;
+  uint16_t* ctlRows;
+  acl_swarm_status_t* cst;
+};
+
+__global__ void __launch_bounds__(256) adopt_kernel(const AdoptArgs A) {
+  const int b = blockIdx.x, tid = threadIdx.x, n = A.n;
+  __shared__ int take;  // 0 none, 1 one table, 2 per vehicle
   if (tid == 0) {
-    acl_episode_status_t e = est[b];
+    acl_episode_status_t e = A.est[b];
     bool complete = false;
-    if (mode == 0) {
-      if (flush[b] != 0) {
-        flush[b] = 0;
+    if (A.mode == 0) {
+      if (A.flush[b] != 0) {
+        A.flush[b] = 0;
         ++e.n_skipped;
       } else {
         ++e.n_auctions;
-        if (lat && e.pending_step > 0) ++e.n_restarted;
-        const int L = lat ? lat[b] : 0;
-        e.pending_step = L > 0 ? step + L + 1 : 0;  // completion step + 1; 0: none
+        if (A.lat && e.pending_step > 0) ++e.n_restarted;
+        const int L = A.lat ? A.lat[b] : 0;
+        e.pending_step = L > 0 ? A.step + L + 1 : 0;  // completion step + 1; 0: none
         complete = L <= 0;
       }
-    } else if (e.pending_step > 0 && e.pending_step - 1 <= step) {
+    } else if (e.pending_step > 0 && e.pending_step - 1 <= A.step) {
       e.pending_step = 0;
       complete = true;
     }
     take = 0;
     if (complete) {
-      const uint32_t flags = st[b].flags;
-      const bool valid = (flags & ACL_SWARM_VALID) != 0, agree = (flags & ACL_SWARM_AGREE) != 0;
-      if (agree && valid) take = 1;
-      else if (agree) { flush[b] = 1; ++e.n_invalid; }
-      else ++e.n_disagree;
+      const acl_swarm_status_t s = A.st[b];
+      const bool valid = (s.flags & ACL_SWARM_VALID) != 0, agree = (s.flags & ACL_SWARM_AGREE) != 0;
+      if (agree && valid) {
+        take = 1;
+        e.per_vehicle = 0;
+      } else if (agree) {
+        A.flush[b] = 1;
+        ++e.n_invalid;
+      } else {
+        ++e.n_disagree;
+        if (s.n_invalid < n && !(s.flags & ACL_SWARM_BAD_INPUT)) take = 2;
+      }
     }
-    est[b] = e;
+    A.est[b] = e;
   }
   __syncthreads();
-  if (take) {
-    for (int v = tid; v < n; v += 64) {
-      const uint16_t pv = Pnew[(size_t)b * n + v];
-      P[(size_t)b * n + v] = pv;
-      if (wsPt) wsPt[(size_t)b * n + pv] = (uint16_t)v;  // a valid permutation
+  if (take == 0) return;
+  const size_t bn = (size_t)b * n;
+  if (take == 1) {
+    for (int v = tid; v < n; v += 256) {
+      const uint16_t pv = A.Pnew[bn + v];
+      A.P[bn + v] = pv;
+      A.seed[bn + v] = pv;
+      A.ctlPt[bn + pv] = (uint16_t)v;  // a valid permutation
     }
-    if (wsMode && tid == 0) wsMode[b] = 0;
+    if (tid == 0) {
+      A.ctlMode[b] = 0;
+      A.cst[b] = acl_swarm_status_t{};
+    }
+    return;
+  }
+  // per vehicle: the rows of vehicles with a valid table; the others keep
+  // theirs (their row as flown so far: the shared row while the swarm was
+  // uniform, else their own)
+  const bool was_rows = A.ctlMode[b] != 0;
+  const uint16_t* pt = A.ctlPt + bn;
+  uint16_t* rows = A.ctlRows + bn * n;
+  const uint16_t* srows = A.sRows + bn * n;
+  const uint8_t* vv = A.sValid + bn;
+  for (size_t k = tid; k < (size_t)n * n; k += 256) {
+    const int v = (int)(k / n), jj = (int)(k - (size_t)v * n);
+    if (vv[v]) rows[k] = srows[k];
+    else if (!was_rows) rows[k] = pt[jj];
+  }
+  for (int v = tid; v < n; v += 256)
+    if (vv[v]) A.P[bn + v] = A.Pnew[bn + v];  // the vehicle's own point in its table
+  __syncthreads();
+  if (tid == 0) {
+    A.ctlMode[b] = 1;
+    A.est[b].per_vehicle = 1;
+    A.cst[b] = acl_swarm_status_t{};
   }
 }
 
@@ -330,27 +389,53 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
   double* us = reinterpret_cast<double*>(ws + W.us);
   uint8_t* ca = ws + W.ca;
 
+  uint16_t* seed = reinterpret_cast<uint16_t*>(ws + W.seed);
+  const WsLayout WS = ws_layout(n, B);
+  unsigned char* wc = ws + W.ctl;  // the control stage's hand-off region
+
   acl_solve_args_t sa = {};
-  sa.B = B; sa.fidx = a->fidx; sa.q = a->q; sa.vel = a->vel; sa.P_in = a->P; sa.P_out = Pnew;
+  sa.B = B; sa.fidx = a->fidx; sa.q = a->q; sa.vel = a->vel; sa.P_in = seed; sa.P_out = Pnew;
   sa.status = st; sa.workspace = ws + W.solve;
   sa.cntrl = a->cntrl; sa.safety = a->safety; sa.early_exit = 1; sa.do_control = 0;
   acl_control_args_t cs = {};
   cs.B = B; cs.fidx = a->fidx; cs.q = a->q; cs.vel = a->vel; cs.P = a->P;
   cs.u = u; cs.u_safe = us; cs.ca_flag = ca;
   cs.status = reinterpret_cast<acl_swarm_status_t*>(ws + W.cst);
-  cs.workspace = ws + W.solve; cs.cntrl = a->cntrl; cs.safety = a->safety;
+  cs.workspace = wc; cs.cntrl = a->cntrl; cs.safety = a->safety;
 
   TrajParams T;
   T.n = n; T.B = B; T.q = a->q; T.vel = a->vel; T.u = u; T.us = us; T.ca = ca; T.P = a->P;
   T.est = a->est; T.ring_u = a->ring_u; T.ring_ca = a->ring_ca;
   T.q_hist = a->q_hist; T.vel_hist = a->vel_hist; T.u_hist = a->u_hist; T.ca_hist = a->ca_hist; T.P_hist = a->P_hist;
   T.ep = ep;
-  // the control hand-off (inverse assignment) depends only on P: it is
-  // rebuilt on the first step of a call and after every auction (which also
-  // overwrites it); the collision-avoidance count is zeroed by traj_kernel
-  T.ca_count = reinterpret_cast<unsigned*>(ws + W.solve + ws_layout(n, B).cacount);
-  uint16_t* hoPt = reinterpret_cast<uint16_t*>(ws + W.solve + ws_layout(n, B).pt);
-  uint8_t* hoMode = ws + W.solve + ws_layout(n, B).mode;
+  // the collision-avoidance count is zeroed by traj_kernel after each step
+  T.ca_count = reinterpret_cast<unsigned*>(wc + WS.cacount);
+
+  // The call's hand-off, before its first auction: swarms flying one
+  // assignment get the inverse of P (permutation check, as
+  // acl_control_batch) and seed = P; swarms flying per-vehicle tables
+  // (est.per_vehicle, from an earlier call on this workspace) keep theirs.
+  {
+    CtlParams C;
+    const acl_status_t r = ctl_params(F, &cs, C);
+    if (r != ACL_OK) return r;
+    C.keep = reinterpret_cast<const uint8_t*>(a->est) + offsetof(acl_episode_status_t, per_vehicle);
+    C.keep_stride = (int)sizeof(acl_episode_status_t);
+    C.seed_out = seed;
+    if (hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
+      return acl__set_error("hipMemsetAsync failed");
+    if (launch_control_prep(C, a->P, B, s) != hipSuccess)
+      return acl__set_error("control_prep launch failed");
+  }
+  AdoptArgs A;
+  A.n = n; A.lat = nullptr; A.P = a->P; A.seed = seed; A.Pnew = Pnew; A.st = st;
+  A.sRows = reinterpret_cast<const uint16_t*>(ws + W.solve + WS.rows);
+  A.sValid = ws + W.solve + WS.vvalid;
+  A.flush = a->flush; A.est = a->est;
+  A.ctlPt = reinterpret_cast<uint16_t*>(wc + WS.pt);
+  A.ctlMode = wc + WS.mode;
+  A.ctlRows = reinterpret_cast<uint16_t*>(wc + WS.rows);
+  A.cst = cs.status;
   // auctions that take time: each swarm's latency in control steps
   const bool timed = ep.auction_latency != 0;
   int32_t* lat = reinterpret_cast<int32_t*>(ws + W.lat);
@@ -359,26 +444,25 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
                        F->adj, ep.auction_latency < 0 ? -1 : ep.auction_latency, ep.control_dt,
                        lat);
     if (hipGetLastError() != hipSuccess) return acl__set_error("latency_kernel launch failed");
+    A.lat = lat;
   }
   for (int k = 0; k < a->steps; ++k) {
     const int step = a->step0 + k;
-    int flags = k == 0 ? (CTL_PREP | CTL_RESET) : 0;
+    A.step = step;
     if (step % ep.auction_every == 0) {
       const acl_status_t r = acl_solve_batch(F, &sa, stream);
       if (r != ACL_OK) return r;
-      hipLaunchKernelGGL(adopt_kernel, dim3(B), dim3(64), 0, s, n, step, 0,
-                         timed ? lat : nullptr, a->P, Pnew, st, a->flush, a->est, nullptr,
-                         nullptr);
+      A.mode = 0;
+      hipLaunchKernelGGL(adopt_kernel, dim3(B), dim3(256), 0, s, A);
       if (hipGetLastError() != hipSuccess) return acl__set_error("adopt_kernel launch failed");
-      flags |= CTL_PREP | CTL_RESET;
     } else if (timed) {
-      // a pending auction completing at this step changes P: adopt_kernel
-      // rebuilds those swarms' control hand-off (inverse assignment) itself
-      hipLaunchKernelGGL(adopt_kernel, dim3(B), dim3(64), 0, s, n, step, 1, lat, a->P, Pnew, st,
-                         a->flush, a->est, hoPt, hoMode);
+      // a pending auction completing at this step: adopt_kernel writes those
+      // swarms' control hand-off itself
+      A.mode = 1;
+      hipLaunchKernelGGL(adopt_kernel, dim3(B), dim3(256), 0, s, A);
       if (hipGetLastError() != hipSuccess) return acl__set_error("adopt_kernel launch failed");
     }
-    const acl_status_t r = run_control(F, &cs, s, flags);
+    const acl_status_t r = run_control(F, &cs, s, CTL_MIXED);
     if (r != ACL_OK) return r;
     T.step = step;
     T.k = k;

@@ -256,8 +256,8 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   return ACL_OK;
 }
 
-acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_args_t* a,
-                                  hipStream_t s, int flags) {
+acl_status_t acl_amd::ctl_params(const acl_formations_t* F, const acl_control_args_t* a,
+                                 CtlParams& C) {
   using namespace acl_amd;
   if (!F || !a) return acl__set_error("acl_control_batch: null argument");
   const int n = F->n;
@@ -272,7 +272,7 @@ acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_a
   if (F->n_formations < 1) return acl__set_error("acl_control_batch: n_formations < 1");
   const WsLayout W = ws_layout(n, a->B);
   unsigned char* ws = (unsigned char*)a->workspace;
-  CtlParams C;
+  C = CtlParams{};
   C.n = n; C.B = a->B; C.b0 = 0;
   C.p = F->p; C.adj = F->adj; C.gains = F->gains; C.gain_off = F->gain_off;
   C.gain_planes = F->gain_planes == 5 ? 5 : 9;
@@ -293,6 +293,16 @@ acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_a
   C.all_uniform = 1;  // the hand-off of a given P is one assignment per swarm
   C.F = F->n_formations;
   C.gate_margin = a->gate_margin;
+  return ACL_OK;
+}
+
+acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_args_t* a,
+                                  hipStream_t s, int flags) {
+  using namespace acl_amd;
+  CtlParams C;
+  const acl_status_t st = ctl_params(F, a, C);
+  if (st != ACL_OK || a->B == 0) return st;
+  if (flags & CTL_MIXED) C.all_uniform = 0;
   if ((flags & CTL_RESET) && hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
     return acl__set_error("hipMemsetAsync failed");
   hipError_t e = hipSuccess;

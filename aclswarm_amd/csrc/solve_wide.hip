@@ -1164,6 +1164,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         const int v = k / n, jj = k - v * n;
         rows[k] = validv[v] ? T[tix(n, jj, v)] : Ptin[jj];
       }
+      for (int v = tid; v < n; v += kWBlock) P.ws[P.W.vvalid + (size_t)b * n + v] = validv[v];
     }
   }
   const bool uniform_all = (misc[M_NINV] == 0 && misc[M_AGREE]) || misc[M_NINV] == n;

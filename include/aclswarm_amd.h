@@ -425,11 +425,16 @@ acl_status_t acl_hungarian_batch(const acl_formations_t* formations,
  *      (CoordinationROS::autoauctionCb, coordination_ros.cpp:322-359): a swarm
  *      whose previous auction converged on an invalid assignment flushes and
  *      skips this one (:339-345, Auctioneer::flush); otherwise CBAA from the
- *      current q with the carried assignment P (acl_solve_batch's auction),
- *      adopted when valid and agreed (auctioneer.cpp:283-292); an invalid
- *      result sets `flush`;
- *   2. DistCntrl::compute with P and vel (controlCb, coordination_ros.cpp:
- *      365-378), Safety::cmdinCb saturation and collisionAvoidance
+ *      current q (acl_solve_batch's auction, P_in = the swarm's last agreed
+ *      assignment), and each vehicle's adoption as auctioneer.cpp:250-295:
+ *      an agreed valid result is adopted by every vehicle; an agreed invalid
+ *      one sets `flush`; on disagreement each vehicle whose own final table
+ *      is valid adopts it and the others keep theirs -- the swarm then flies
+ *      per-vehicle tables (est.per_vehicle) until an agreed valid auction
+ *      (model limit: the next auction aligns every vehicle with the last
+ *      agreed assignment, where the reference's vehicles each use their own);
+ *   2. DistCntrl::compute with each vehicle's table and vel (controlCb,
+ *      coordination_ros.cpp:365-378), Safety::cmdinCb saturation and collisionAvoidance
  *      (safety.cpp:172-197,412-541) -> the velocity goal;
  *   3. Safety::makeSafeTraj(control_dt, goal) (safety.cpp:330-408): rate
  *      limits on the goal velocity, room-bound clamps, goal position
@@ -443,15 +448,19 @@ acl_status_t acl_hungarian_batch(const acl_formations_t* formations,
  *      orig_zero_vel_thr, gridlocked <=> some vehicle's window mean CA flag >
  *      avg_active_ca_thr (means: sequential sum oldest -> newest, / bufflen).
  * Device pointers, updated in place so an episode can continue in chunks:
- *   fidx [B]; q, vel [B][n][3]; P [B][n] (a permutation); flush [B] u8;
+ *   fidx [B]; q, vel [B][n][3]; P [B][n] (vehicle -> its formation point:
+ *   a permutation at the start; while a swarm flies per-vehicle tables,
+ *   each vehicle's point in its own table); flush [B] u8;
  *   est [B] acl_episode_status_t; ring_u [B][bufflen][n] f64 and
  *   ring_ca [B][bufflen][n] u8 (zeroed with est before step 0; in est,
  *   converged_step and gridlock_step then set to -1).
  * Optional histories (NULL = not stored), k = local step:
  *   q_hist, vel_hist [steps][B][n][3] (state after step k), u_hist [steps][B][n][3]
  *   (DistCntrl output), ca_hist [steps][B][n], P_hist [steps][B][n]
- *   (assignment used by step k's controller).
- * workspace: acl_episode_workspace_bytes(n, B) bytes. */
+ *   (each vehicle's point in the table used by step k's controller).
+ * workspace: acl_episode_workspace_bytes(n, B) bytes. A continuing call
+ * must get the same workspace when an auction is pending or a swarm flies
+ * per-vehicle tables (both live there; est says which). */
 typedef struct {
   double control_dt;       /* 0.01 s (coordination.launch:25, safety.cpp:38) */
   int32_t auction_every;   /* autoauction_dt / control_dt = 1.2 / 0.01 = 120
@@ -492,9 +501,8 @@ typedef struct {
   uint16_t n_auctions;     /* auctions run */
   uint16_t n_invalid;      /* auctions that converged on an invalid assignment */
   uint16_t n_skipped;      /* auctions skipped by the flush rule */
-  uint16_t n_disagree;     /* valid auctions whose vehicles ended on different
-                              tables (P kept: the per-vehicle divergent state of
-                              the reference is not carried) */
+  uint16_t n_disagree;     /* auctions whose vehicles ended on different
+                              tables (each adopted its own valid one) */
   uint32_t n_samples;      /* supervisor ticks taken */
   uint32_t n_ca_steps;     /* vehicle-steps with collision avoidance active */
   int32_t pending_step;    /* 1 + the global step at which the pending
@@ -503,7 +511,9 @@ typedef struct {
                               workspace between calls): a zeroed status is the
                               start of an episode */
   uint16_t n_restarted;    /* auctions restarted before they completed */
-  uint16_t reserved;
+  uint16_t per_vehicle;    /* 1: the swarm's vehicles fly different tables
+                              (kept in the workspace) since a disagreeing
+                              auction; 0 after an agreed valid one */
 } acl_episode_status_t; /* 40 bytes */
 
 typedef struct {

@@ -7,8 +7,9 @@ What it restates, in the order one lockstep control period applies it:
   * CoordinationROS::autoauctionCb (aclswarm/src/coordination_ros.cpp:322-359):
     every `auction_every` steps, a swarm whose last auction converged on an
     invalid assignment flushes and skips (:339-345); otherwise CBAA from the
-    current q (pyoracle.solve, the restatement of auctioneer.cpp) and
-    adoption of a valid agreed result (auctioneer.cpp:283-292);
+    current q (pyoracle.solve, the restatement of auctioneer.cpp) and each
+    vehicle's adoption of its own final table when it is valid
+    (auctioneer.cpp:250-295; `adopt`, `SwarmState`);
   * DistCntrl::compute + Safety::cmdinCb + collisionAvoidance for every
     vehicle (pyoracle.control / saturate / collision_avoidance, i.e.
     distcntrl.cpp:46-102, safety.cpp:172-197,412-541);
@@ -115,36 +116,95 @@ class Supervisor:
         return self.converged, self.gridlocked
 
 
-def control_step(q, vel, p, adj, gains, P, g=None, s=None):
+def control_step(q, vel, p, adj, gains, P, g=None, s=None, tables=None):
     """DistCntrl::compute + cmdinCb + collisionAvoidance for every vehicle of
-    one swarm with assignment P (vehicle -> point). Returns u, u_safe, ca."""
+    one swarm. P: vehicle -> point (each vehicle's own point); tables: None
+    (one assignment, inverse of P) or [n][n] per-vehicle inverse tables
+    (row v: vehicle v's formation point -> vehicle). Returns u, u_safe, ca."""
     n = q.shape[0]
-    Pt = np.zeros(n, np.uint16)
-    Pt[np.asarray(P, np.int64)] = np.arange(n, dtype=np.uint16)
+    if tables is None:
+        Pt = inverse(P)
     u = np.zeros((n, 3))
     us = np.zeros((n, 3))
     ca = np.zeros(n, np.uint8)
     for v in range(n):
-        u[v] = O.control(v, q, vel[v], Pt, adj, gains, p, g)
+        Ptv = Pt if tables is None else np.asarray(tables[v], np.uint16)
+        u[v] = O.control(v, q, vel[v], Ptv, adj, gains, p, g)
         c = O.saturate(u[v], s)
         us[v], mod = O.collision_avoidance(v, q, c, s)
         ca[v] = mod
     return u, us, ca
 
 
-def adopt(P, flush, res):
-    """autoauctionCb's flush rule + adoption for one swarm after an auction
-    result `res` (pyoracle.solve). Returns (P, flush, event) with event one
-    of 'skipped', 'adopted', 'invalid', 'disagree'."""
+def inverse(P):
+    P = np.asarray(P, np.int64)
+    Pt = np.zeros(len(P), np.uint16)
+    Pt[P] = np.arange(len(P), dtype=np.uint16)
+    return Pt
+
+
+def is_perm(w):
+    w = np.asarray(w, np.int64)
+    return bool(((w >= 0) & (w < len(w))).all()) and len(set(w.tolist())) == len(w)
+
+
+class SwarmState:
+    """One swarm's assignment state across auctions: P (each vehicle's own
+    formation point), seed (the last agreed assignment: the next auction's
+    P_in) and tables (None while every vehicle holds one assignment, else
+    [n][n] per-vehicle inverse tables)."""
+
+    def __init__(self, P):
+        self.P = np.array(P, np.uint16)
+        self.seed = self.P.copy()
+        self.tables = None
+
+    def copy(self):
+        c = SwarmState(self.P)
+        c.seed = self.seed.copy()
+        c.tables = None if self.tables is None else self.tables.copy()
+        return c
+
+
+def adopt(state, flush, res):
+    """autoauctionCb's flush rule + each vehicle's adoption
+    (auctioneer.cpp:250-295) for one swarm after an auction result `res`
+    (pyoracle.solve from state.seed). Mutates `state`; returns (flush, event)
+    with event one of 'skipped', 'adopted', 'invalid', 'disagree'.
+
+    agree + valid: every vehicle adopts the one table. agree + invalid: every
+    vehicle keeps its table and the swarm skips its next auto-auction
+    (coordination_ros.cpp:339-345). Disagreement: each vehicle whose own final
+    table is a permutation adopts it (its row of `who`), the others keep
+    theirs; the swarm then flies per-vehicle tables until an agreed valid
+    auction (seed unchanged: the model seeds every vehicle's next alignment
+    with the last agreed assignment, where the reference aligns each vehicle
+    with its own P_)."""
     if flush:
-        return P, 0, "skipped"
+        return 0, "skipped"
     fl = res["status"]["flags"]
     valid, agree = bool(fl & 0x01), bool(fl & 0x02)
     if agree and valid:
-        return res["P_out"].astype(np.uint16).copy(), 0, "adopted"
+        state.P = res["P_out"].astype(np.uint16).copy()
+        state.seed = state.P.copy()
+        state.tables = None
+        return 0, "adopted"
     if agree:
-        return P, 1, "invalid"
-    return P, 0, "disagree"
+        return 1, "invalid"
+    who = res["who"]
+    n = len(state.P)
+    vv = [is_perm(who[v]) for v in range(n)]
+    if any(vv):
+        cur = (np.tile(inverse(state.P), (n, 1)) if state.tables is None
+               else state.tables.copy())
+        P = state.P.copy()
+        for v in range(n):
+            if vv[v]:
+                cur[v] = who[v]
+                P[v] = int(np.nonzero(who[v] == v)[0][0])
+        state.tables = cur.astype(np.uint16)
+        state.P = P
+    return 0, "disagree"
 
 
 AUCTIONEER_DT = 0.001  # coordination.launch:23: one bid processed per tick
@@ -178,40 +238,41 @@ class Auctions:
         self.res = None
         self.counts = dict(skipped=0, auctions=0, adopted=0, invalid=0, disagree=0, restarted=0)
 
-    def auto(self, step, P, solve):
-        """An auto-auction step; solve() runs CBAA from the current state."""
+    def auto(self, step, state, solve):
+        """An auto-auction step; solve(seed) runs CBAA from the current q
+        with P_in = state.seed. Mutates `state`."""
         if self.flush:
             self.flush = 0
             self.counts["skipped"] += 1
-            return P
+            return state
         self.counts["auctions"] += 1
         if self.pending >= 0:
             self.counts["restarted"] += 1
-        self.res = solve()
+        self.res = solve(state.seed)
         if self.latency <= 0:
             self.pending = -1
-            return self._complete(P)
+            return self._complete(state)
         self.pending = step + self.latency
-        return P
+        return state
 
-    def tick(self, step, P):
+    def tick(self, step, state):
         """Any other step: a pending auction whose step has come completes."""
         if 0 <= self.pending <= step:
             self.pending = -1
-            return self._complete(P)
-        return P
+            return self._complete(state)
+        return state
 
-    def _complete(self, P):
-        P2, self.flush, ev = adopt(P, 0, self.res)
+    def _complete(self, state):
+        self.flush, ev = adopt(state, 0, self.res)
         self.counts[ev] += 1
-        return P2
+        return state
 
 
 def run_episode(q, vel, P, p, adj, gains, steps, ep, step0=0, g=None, s=None):
     """The whole closed loop for one swarm on the CPU (small cases only)."""
     q = np.array(q, np.float64)
     vel = np.array(vel, np.float64)
-    P = np.array(P, np.uint16)
+    st = SwarmState(P)
     sup = Supervisor(q.shape[0], ep)
     auc = Auctions(auction_latency_steps(q.shape[0], adj, ep))
     conv_step = grid_step = -1
@@ -219,10 +280,10 @@ def run_episode(q, vel, P, p, adj, gains, steps, ep, step0=0, g=None, s=None):
     for k in range(steps):
         step = step0 + k
         if step % ep["auction_every"] == 0:
-            P = auc.auto(step, P, lambda: O.solve(q, vel, p, adj, gains, P, g, s))
+            auc.auto(step, st, lambda seed: O.solve(q, vel, p, adj, gains, seed, g, s))
         else:
-            P = auc.tick(step, P)
-        u, us, ca = control_step(q, vel, p, adj, gains, P, g, s)
+            auc.tick(step, st)
+        u, us, ca = control_step(q, vel, p, adj, gains, st.P, g, s, st.tables)
         q, vel = make_safe_traj(q, vel, us, ep)
         if step % ep["sample_every"] == 0:
             r = sup.tick(u, ca)
@@ -232,5 +293,5 @@ def run_episode(q, vel, P, p, adj, gains, steps, ep, step0=0, g=None, s=None):
                 if r[1] and grid_step < 0:
                     grid_step = step
         qs.append(q.copy())
-    return dict(q=q, vel=vel, P=P, flush=auc.flush, counts=auc.counts, converged_step=conv_step,
+    return dict(q=q, vel=vel, P=st.P, tables=st.tables, flush=auc.flush, counts=auc.counts, converged_step=conv_step,
                 gridlock_step=grid_step, q_hist=np.array(qs))

@@ -109,15 +109,50 @@ def test_supervisor_window_rules():
 def test_adopt_rule():
     P = np.arange(4, dtype=np.uint16)
     newP = np.array([1, 0, 3, 2], np.uint16)
-    ok = {"P_out": newP, "status": {"flags": 0x03}}
-    bad = {"P_out": newP, "status": {"flags": 0x02}}
-    dis = {"P_out": newP, "status": {"flags": 0x01}}
-    assert (E.adopt(P, 0, ok)[0] == newP).all()
-    P2, fl, ev = E.adopt(P, 0, bad)
-    assert (P2 == P).all() and fl == 1 and ev == "invalid"
-    P3, fl, ev = E.adopt(P, 1, ok)                   # flushed: skipped, flag cleared
-    assert (P3 == P).all() and fl == 0 and ev == "skipped"
-    assert E.adopt(P, 0, dis)[2] == "disagree"
+    who_new = np.tile(E.inverse(newP), (4, 1))
+    ok = {"P_out": newP, "status": {"flags": 0x03}, "who": who_new}
+    bad = {"P_out": newP, "status": {"flags": 0x02}, "who": who_new}
+    st = E.SwarmState(P)
+    assert E.adopt(st, 0, ok) == (0, "adopted") and (st.P == newP).all() and st.tables is None
+    assert (st.seed == newP).all()
+    st = E.SwarmState(P)
+    assert E.adopt(st, 0, bad) == (1, "invalid") and (st.P == P).all()
+    assert E.adopt(st, 1, ok) == (0, "skipped") and (st.P == P).all()   # flushed: skipped
+    # disagreement: vehicles 0 and 1 end on valid but different tables,
+    # vehicles 2 and 3 on invalid ones (a task nobody holds)
+    who = np.array([[1, 0, 3, 2], [0, 1, 2, 3], [1, 0, 4, 4], [4, 4, 4, 4]], np.uint16)
+    dis = {"P_out": np.array([1, 1, 2, 3], np.uint16), "status": {"flags": 0x00}, "who": who}
+    st = E.SwarmState(P)
+    assert E.adopt(st, 0, dis) == (0, "disagree")
+    assert st.P.tolist() == [1, 1, 2, 3]          # own points: 0 and 1 adopted, 2, 3 kept
+    assert st.tables[0].tolist() == [1, 0, 3, 2] and st.tables[1].tolist() == [0, 1, 2, 3]
+    assert st.tables[2].tolist() == [0, 1, 2, 3] and st.tables[3].tolist() == [0, 1, 2, 3]
+    assert (st.seed == P).all()                   # the next auction's P_in
+    # a second disagreement: the invalid vehicle keeps its own previous row
+    who2 = np.array([[4, 4, 4, 4], [2, 3, 0, 1], [3, 2, 1, 0], [0, 1, 2, 3]], np.uint16)
+    E.adopt(st, 0, {"P_out": None, "status": {"flags": 0x00}, "who": who2})
+    assert st.tables[0].tolist() == [1, 0, 3, 2] and st.P[0] == 1
+    assert st.tables[1].tolist() == [2, 3, 0, 1] and st.P[1] == 3
+    # agreement clears the per-vehicle state
+    assert E.adopt(st, 0, ok) == (0, "adopted") and st.tables is None
+
+
+def test_per_vehicle_control_uses_each_table():
+    """control_step with per-vehicle tables equals control_step with each
+    vehicle's own assignment, vehicle by vehicle."""
+    rng = np.random.RandomState(2)
+    pts, adj, gains, q0 = H.swarm6()
+    n = 6
+    q = q0 + rng.normal(0, 0.3, q0.shape)
+    vel = rng.normal(0, 0.1, q.shape)
+    Ps = [H.random_perm(rng, n) for _ in range(n)]
+    tables = np.stack([E.inverse(P) for P in Ps])
+    own = np.array([Ps[v][v] for v in range(n)], np.uint16)
+    u, us, ca = E.control_step(q, vel, pts[0], adj[0], gains[0], own, tables=tables)
+    for v in range(n):
+        uv, usv, cav = E.control_step(q, vel, pts[0], adj[0], gains[0], Ps[v])
+        np.testing.assert_array_equal(u[v], uv[v])
+        np.testing.assert_array_equal(us[v], usv[v])
 
 
 def test_cpu_episode_swarm6_flies_towards_formation():

@@ -42,7 +42,35 @@ def _cases():
               q=q, vel=rng.normal(0, 0.2, (B, 20, 3)),
               P=np.stack([H.random_perm(rng, 20) for _ in range(B)]),
               steps=160, ep=dict(auction_every=40, bufflen=20))
-    return [a, b_]
+    return [a, b_, _chain_case()]
+
+
+def _chain_case():
+    """Chain (path-graph) formations, n = 10: lockstep CBAA needs more than
+    the reference's 2n rounds to reach consensus along a chain for many
+    starts, so auctions end with vehicles on different tables, some of them
+    valid (found with the CPU oracle; the GPU auction is bit-exact with it)."""
+    rng = np.random.RandomState(21)
+    n, B = 10, 6
+    pts, adjs, gains, qs = [], [], [], []
+    while len(qs) < B:
+        adj = np.zeros((n, n), np.uint8)
+        perm = rng.permutation(n)
+        for x, y in zip(perm[:-1], perm[1:]):
+            adj[x, y] = adj[y, x] = 1
+        p = np.c_[rng.uniform(-5, 5, (n, 2)), rng.uniform(0, 2, n)]
+        q = np.c_[rng.uniform(-5, 5, (n, 2)), np.ones(n)]
+        P0 = np.arange(n, dtype=np.uint16)
+        r = O.solve(q, np.zeros((n, 3)), p, adj, np.zeros((3 * n, 3 * n)), P0)
+        who = r["who"]
+        nvalid = sum(E.is_perm(who[v]) for v in range(n))
+        if r["status"]["flags"] & 0x02 or nvalid == 0:
+            continue
+        pts.append(p); adjs.append(adj); gains.append(H.synth_gains(rng, adj)); qs.append(q)
+    return dict(name="chain10_disagree", pts=pts, adj=adjs, gains=gains, fidx=np.arange(B),
+                q=np.stack(qs), vel=np.zeros((B, n, 3)),
+                P=np.stack([np.arange(n, dtype=np.uint16)] * B), steps=90,
+                ep=dict(auction_every=30, bufflen=10), disagree=True)
 
 
 def _episode(case, dev):
@@ -60,8 +88,11 @@ def _episode(case, dev):
     return e, ep
 
 
-@pytest.mark.parametrize("ci", [0, 1])
+@pytest.mark.parametrize("ci", [0, 1, 2])
 def test_episode_teacher_forced_parity(cuda, ci):
+    """ci 2: chain formations whose 2n-round auctions end with vehicles on
+    different tables -- each vehicle adopts its own valid table
+    (auctioneer.cpp:250-295) and flies it until an agreed auction."""
     import torch
     case = _cases()[ci]
     e, eps = _episode(case, cuda)
@@ -72,22 +103,22 @@ def test_episode_teacher_forced_parity(cuda, ci):
     est = e.status()
     ep = E.params_from_struct(eps)
     B, n = case["q"].shape[:2]
-    n_adopt = n_ca = 0
+    n_adopt = n_ca = n_dis = 0
     for b in range(B):
         f = case["fidx"][b]
         p, adj, G = case["pts"][f], case["adj"][f], case["gains"][f]
         qprev, vprev = case["q"][b], case["vel"][b]
-        P, flush = case["P"][b].astype(np.uint16), 0
+        state, flush = E.SwarmState(case["P"][b]), 0
         sup = E.Supervisor(n, ep)
         counts = dict(skipped=0, adopted=0, invalid=0, disagree=0)
         conv = grid = -1
         for k in range(case["steps"]):
             if k % ep["auction_every"] == 0:
-                res = O.solve(qprev, vprev, p, adj, G, P)
-                P, flush, ev = E.adopt(P, flush, res)
+                res = O.solve(qprev, vprev, p, adj, G, state.seed)
+                flush, ev = E.adopt(state, flush, res)
                 counts[ev] += 1
-            assert (h["P"][k, b] == P).all(), (b, k)
-            u, us, ca = E.control_step(qprev, vprev, p, adj, G, P)
+            assert (h["P"][k, b] == state.P).all(), (b, k)
+            u, us, ca = E.control_step(qprev, vprev, p, adj, G, state.P, tables=state.tables)
             np.testing.assert_allclose(h["u"][k, b], u, rtol=U_RTOL, atol=U_RTOL)
             assert (h["ca"][k, b] == ca).all(), (b, k)
             qn, vn = E.make_safe_traj(qprev, vprev, us, ep)
@@ -108,8 +139,13 @@ def test_episode_teacher_forced_parity(cuda, ci):
         assert st["converged"] == int(sup.converged) and st["gridlocked"] == int(sup.gridlocked)
         assert st["n_samples"] == sup.n_samples
         assert st["n_ca_steps"] == int(h["ca"][:, b].sum())
+        assert st["per_vehicle"] == int(state.tables is not None)
         n_adopt += counts["adopted"]
-    assert n_adopt > 0
+        n_dis += counts["disagree"]
+    if case.get("disagree"):
+        assert n_dis > 0         # the chain formations end auctions on different tables
+    else:
+        assert n_adopt > 0
     if ci == 1:
         assert n_ca > 0          # the dense starts exercise collision avoidance
 
@@ -145,9 +181,12 @@ def test_episode_closed_loop_matches_cpu_episode(cuda):
         assert est[b]["converged_step"] == r["converged_step"]
 
 
-def test_episode_chunks_equal_one_call(cuda):
+@pytest.mark.parametrize("ci", [1, 2])
+def test_episode_chunks_equal_one_call(cuda, ci):
+    """ci 2: per-vehicle tables carried across the call boundary in the
+    workspace."""
     import torch
-    case = _cases()[1]
+    case = _cases()[ci]
     e1, _ = _episode(case, cuda)
     e1.run(case["steps"])
     e2, _ = _episode(case, cuda)
@@ -158,8 +197,8 @@ def test_episode_chunks_equal_one_call(cuda):
         assert torch.equal(getattr(e1, k), getattr(e2, k)), k
 
 
-@pytest.mark.parametrize("lat", [-1, 3, 25])
-def test_episode_auction_latency(cuda, lat):
+@pytest.mark.parametrize("lat,ci", [(-1, 0), (3, 0), (25, 0), (7, 2)])
+def test_episode_auction_latency(cuda, lat, ci):
     """Auctions that take time (acl_episode_params_t::auction_latency): the
     reference timing (-1: ceil(2 n d_max 1 ms / control_dt), 4-6 steps for
     the swarm6 formations), a fixed 3 steps, and 25 steps > the auto-auction period of 10
@@ -168,7 +207,8 @@ def test_episode_auction_latency(cuda, lat):
     own state at each auto-auction and must give the assignment the GPU's
     controller used at every step, and the same counters."""
     import torch
-    case = dict(_cases()[0], ep=dict(auction_every=10, auction_latency=lat), steps=64)
+    per_vehicle = ci == 2    # chain formations: pending auctions end in disagreement
+    case = dict(_cases()[ci], ep=dict(auction_every=10, auction_latency=lat), steps=64)
     e, eps = _episode(case, cuda)
     hist = e.run(40, history=True)
     hist2 = e.run(24, history=True)  # a pending auction crosses the call boundary
@@ -182,23 +222,27 @@ def test_episode_auction_latency(cuda, lat):
         f = case["fidx"][b]
         p, adj, G = case["pts"][f], case["adj"][f], case["gains"][f]
         auc = E.Auctions(E.auction_latency_steps(n, adj, ep))
-        P = case["P"][b].astype(np.uint16)
+        state = E.SwarmState(case["P"][b])
         qprev, vprev = case["q"][b], case["vel"][b]
         for k in range(case["steps"]):
             if k % ep["auction_every"] == 0:
-                P = auc.auto(k, P, lambda: O.solve(qprev, vprev, p, adj, G, P))
+                auc.auto(k, state, lambda seed: O.solve(qprev, vprev, p, adj, G, seed))
             else:
-                P = auc.tick(k, P)
-            assert (h["P"][k, b] == P).all(), (lat, b, k)
+                auc.tick(k, state)
+            assert (h["P"][k, b] == state.P).all(), (lat, b, k)
+            if per_vehicle:
+                u, _, _ = E.control_step(qprev, vprev, p, adj, G, state.P, tables=state.tables)
+                np.testing.assert_allclose(h["u"][k, b], u, rtol=U_RTOL, atol=U_RTOL)
             qprev, vprev = h["q"][k, b], h["vel"][k, b]
         st, c = est[b], auc.counts
         assert (st["n_auctions"], st["n_restarted"], st["n_skipped"]) == \
             (c["auctions"], c["restarted"], c["skipped"]), (st, c)
         assert (st["n_invalid"], st["n_disagree"]) == (c["invalid"], c["disagree"])
         assert st["pending_step"] == (auc.pending + 1 if auc.pending >= 0 else 0)
+        assert st["per_vehicle"] == int(state.tables is not None)
         if lat == 25:
             assert c["adopted"] == 0 and c["restarted"] == c["auctions"] - 1
-        else:
+        elif not per_vehicle:
             assert c["adopted"] > 0
 
 
@@ -226,15 +270,15 @@ def test_episode_zeroed_status_mid_period(cuda):
         f = case["fidx"][b]
         p, adj, G = case["pts"][f], case["adj"][f], case["gains"][f]
         auc = E.Auctions(3)
-        P = case["P"][b].astype(np.uint16)
+        state = E.SwarmState(case["P"][b])
         qprev, vprev = case["q"][b], case["vel"][b]
         for k in range(case["steps"]):
             s = 5 + k
             if s % ep["auction_every"] == 0:
-                P = auc.auto(s, P, lambda: O.solve(qprev, vprev, p, adj, G, P))
+                auc.auto(s, state, lambda seed: O.solve(qprev, vprev, p, adj, G, seed))
             else:
-                P = auc.tick(s, P)
-            assert (h["P"][k, b] == P).all(), (b, k)
+                auc.tick(s, state)
+            assert (h["P"][k, b] == state.P).all(), (b, k)
             qprev, vprev = h["q"][k, b], h["vel"][k, b]
         st, c = est[b], auc.counts
         assert st["n_restarted"] == c["restarted"] == 0
