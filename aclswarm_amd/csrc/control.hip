@@ -83,18 +83,16 @@ __host__ __device__ inline GainLayout make_gain_layout(int n, int waves = kCtlWa
 
 // GM: the caller asked for the gate margin (acl_solve_args_t::gate_margin)
 template <int NP, bool GM, int kB>
-__global__ void __launch_bounds__(kB, kB == 256 ? (NP == 5 ? ACL_GAIN_WAVES : 4) : 1) gain_kernel(const CtlParams P) {
+__device__ void gain_swarm(const CtlParams& P, int b) {
   constexpr int kW = kB / 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const int NW = (n + 63) >> 6;
   const GainLayout L = make_gain_layout(n, kW);
-  const int b = P.b0 + blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   if (P.status[b].flags & ACL_SWARM_BAD_INPUT) return;  // auction kernel zeroed outputs
-  if (P.only_nonuniform && P.wsMode[b] == 0) return;    // gain_pair_kernel's swarms
 
   double* q = reinterpret_cast<double*>(smem + L.q);
   double* p = reinterpret_cast<double*>(smem + L.p);
@@ -320,6 +318,23 @@ __global__ void __launch_bounds__(kB, kB == 256 ? (NP == 5 ? ACL_GAIN_WAVES : 4)
   gain_epilogue(P, b, n, q, uo, &caw, tid, kB);
 }
 
+// One workgroup per swarm; with only_nonuniform (the swarms holding
+// per-vehicle assignments, after the pair kernel or the fused auction took
+// the others) a small grid strides over the launch's swarms, so a launch
+// that finds none costs a few hundred workgroups, not one per swarm.
+template <int NP, bool GM, int kB>
+__global__ void __launch_bounds__(kB, kB == 256 ? (NP == 5 ? ACL_GAIN_WAVES : 4) : 1) gain_kernel(const CtlParams P) {
+  if (P.only_nonuniform) {
+    for (int b = P.b0 + blockIdx.x; b < P.b0 + P.nb; b += gridDim.x) {
+      if (P.wsMode[b] == 0) continue;  // workgroup-uniform
+      gain_swarm<NP, GM, kB>(P, b);
+      __syncthreads();  // the LDS image is rewritten for the next swarm
+    }
+    return;
+  }
+  gain_swarm<NP, GM, kB>(P, P.b0 + blockIdx.x);
+}
+
 
 // ---- gain_pair_kernel: DistCntrl::compute once per undirected edge ----------
 // (pair_gain_swarm, control_dev.h) for the uniform swarms of acl_control_batch
@@ -328,14 +343,17 @@ __global__ void __launch_bounds__(kB, kB == 256 ? (NP == 5 ? ACL_GAIN_WAVES : 4)
 #define ACL_GAIN_PAIR_WAVES 5
 #endif
 
-template <bool kTiled, bool GM>
-__global__ void __launch_bounds__(kCtlBlock, ACL_GAIN_PAIR_WAVES) gain_pair_kernel(const CtlParams P) {
+// kPB threads per swarm: 256, or 64 for n <= 32 (a 20-vehicle swarm has
+// six 8 x 8 tiles: one wave, a quarter of the waves to launch per call)
+template <bool kTiled, bool GM, int kPB>
+__global__ void __launch_bounds__(kPB, kPB == kCtlBlock ? ACL_GAIN_PAIR_WAVES : 8)
+    gain_pair_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = P.b0 + blockIdx.x;
   if (P.status[b].flags & ACL_SWARM_BAD_INPUT) return;
   if (P.wsMode[b] != 0) return;  // per-vehicle assignments: gain_kernel
-  pair_gain_swarm<kCtlWaves, kTiled, GM, 1>(P, b, P.fidx[b], smem, threadIdx.x, kCtlBlock,
-                                               P.wsPt + (size_t)b * P.n);
+  pair_gain_swarm<kPB / 64, kTiled, GM, 1>(P, b, P.fidx[b], smem, threadIdx.x, kPB,
+                                           P.wsPt + (size_t)b * P.n);
 }
 
 // acl_tile_gains: one workgroup per formation copies every 40-byte record
@@ -720,7 +738,7 @@ __device__ __forceinline__ bool ca_resolve_serial(int nslot, double* caA, signed
 }
 
 #ifndef ACL_CA_GRID
-#define ACL_CA_GRID 2048
+#define ACL_CA_GRID 1024
 #endif
 // diagnostic build (-DACL_CA_PROF=1, scripts/phase_profile.py --crowd): wave
 // cycles of the sector build, the resolution and the rest into
@@ -1328,22 +1346,51 @@ hipError_t launch_control_prep(const CtlParams& P, const uint16_t* Pgiven, int n
 #define ACL_WIDE_DIRECTED 1
 #endif
 
+// the strided grid of a gain launch over per-vehicle swarms only
+constexpr int kNonuniformGrid = 256;
+
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream) {
+  // the control kernels' dynamic-LDS limit, once per device (not per launch)
+  static PerDeviceOnce once;
+  const hipError_t ea = once.run([] {
+    for (const void* k :
+         {(const void*)gain_pair_kernel<true, true, kCtlBlock>,
+          (const void*)gain_pair_kernel<true, false, kCtlBlock>,
+          (const void*)gain_pair_kernel<false, true, kCtlBlock>,
+          (const void*)gain_pair_kernel<false, false, kCtlBlock>,
+          (const void*)gain_kernel<5, true, 1024>, (const void*)gain_kernel<5, false, 1024>,
+          (const void*)gain_kernel<9, true, 1024>, (const void*)gain_kernel<9, false, 1024>,
+          (const void*)gain_kernel<5, true, kCtlBlock>, (const void*)gain_kernel<5, false, kCtlBlock>,
+          (const void*)gain_kernel<9, true, kCtlBlock>, (const void*)gain_kernel<9, false, kCtlBlock>,
+          (const void*)ca_pair_kernel, (const void*)ca_kernel}) {
+      hipFuncAttributes fa;
+      hipError_t r = hipFuncGetAttributes(&fa, k);
+      if (r != hipSuccess) return r;
+      r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - (int)fa.sharedSizeBytes);
+      if (r != hipSuccess) return r;
+    }
+    return hipSuccess;
+  });
+  if (ea != hipSuccess) return ea;
   if (which == 0 || which == 2) {
     CtlParams Q = P;
+    Q.nb = nb;
     Q.only_nonuniform = which == 2 ? 1 : 0;
     if (which == 0 && P.gain_planes == 5 && ACL_GAIN_PAIR && (P.n <= kMaxN || !ACL_WIDE_DIRECTED)) {
       // uniform swarms: one evaluation per undirected edge; then gain_kernel
       // for the swarms whose vehicles hold different assignments
       const bool tiled = P.gains_tiled != nullptr && P.n <= kMaxN;
-      const PairLayout PL = make_pair_layout(P.n, kCtlWaves, tiled);
+      const bool small = P.n <= 32;
+      const PairLayout PL = make_pair_layout(P.n, small ? 1 : kCtlWaves, tiled);
       const bool gm = P.gate_margin != nullptr;
 #define ACL_PAIR(T_, G_)                                                                     \
   do {                                                                                       \
-    if (PL.total > 64 * 1024)                                                                \
-      (void)hipFuncSetAttribute((const void*)gain_pair_kernel<T_, G_>,                       \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, PL.total);       \
-    hipLaunchKernelGGL((gain_pair_kernel<T_, G_>), dim3(nb), dim3(kCtlBlock), PL.total, stream, Q); \
+    if (small)                                                                               \
+      hipLaunchKernelGGL((gain_pair_kernel<T_, G_, 64>), dim3(nb), dim3(64), PL.total, stream, Q); \
+    else                                                                                     \
+      hipLaunchKernelGGL((gain_pair_kernel<T_, G_, kCtlBlock>), dim3(nb), dim3(kCtlBlock), PL.total, \
+                         stream, Q);                                                         \
   } while (0)
       if (tiled && gm) ACL_PAIR(true, true);
       else if (tiled) ACL_PAIR(true, false);
@@ -1358,18 +1405,13 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
     const bool big = P.n > kMaxN;
     const GainLayout L = make_gain_layout(P.n, big ? 16 : kCtlWaves);
     const bool gm = P.gate_margin != nullptr;
+    const int gb = Q.only_nonuniform ? (nb < kNonuniformGrid ? nb : kNonuniformGrid) : nb;
 #define ACL_GAIN(NP_, G_)                                                                    \
   do {                                                                                       \
     if (big) {                                                                               \
-      if (L.total > 64 * 1024)                                                               \
-        (void)hipFuncSetAttribute((const void*)gain_kernel<NP_, G_, 1024>,                   \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, L.total);      \
-      hipLaunchKernelGGL((gain_kernel<NP_, G_, 1024>), dim3(nb), dim3(1024), L.total, stream, Q); \
+      hipLaunchKernelGGL((gain_kernel<NP_, G_, 1024>), dim3(gb), dim3(1024), L.total, stream, Q); \
     } else {                                                                                 \
-      if (L.total > 64 * 1024)                                                               \
-        (void)hipFuncSetAttribute((const void*)gain_kernel<NP_, G_, kCtlBlock>,              \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, L.total);      \
-      hipLaunchKernelGGL((gain_kernel<NP_, G_, kCtlBlock>), dim3(nb), dim3(kCtlBlock), L.total, \
+      hipLaunchKernelGGL((gain_kernel<NP_, G_, kCtlBlock>), dim3(gb), dim3(kCtlBlock), L.total, \
                          stream, Q);                                                         \
     }                                                                                        \
   } while (0)
@@ -1382,17 +1424,11 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
     // a fixed grid striding over the device-side count of listed swarms
     if (P.n <= kMaxN) {
       const int lp = ca_pair_layout(P.n).total;
-      if (lp > 64 * 1024)
-        (void)hipFuncSetAttribute((const void*)ca_pair_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lp);
       hipLaunchKernelGGL(ca_pair_kernel, dim3(nb < ACL_CA_GRID ? nb : ACL_CA_GRID), dim3(kCaPT), lp,
                          stream, P);
       return hipGetLastError();
     }
     const int lds = ca_layout(P.n).total;
-    if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute((const void*)ca_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(ca_kernel, dim3(nb < ACL_CA_GRID ? nb : ACL_CA_GRID), dim3(64 * kCaWaves),
                        lds, stream, P);
   }

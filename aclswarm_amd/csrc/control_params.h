@@ -116,6 +116,7 @@ struct CtlParams {
   acl_cntrl_gains_t g;
   acl_safety_params_t s;
   int only_nonuniform;  // set by launch_control: gain_kernel skips uniform swarms
+  int nb;               // set by launch_control: swarms [b0, b0 + nb) of this launch
   int all_uniform;      // every swarm has one assignment (given P): no gain_kernel pass
   int F;                // formations in the table (fidx range check of the hand-off)
   double* gate_margin;  // [B] optional: min | |e| - thr | / thr of the swarm's gates

@@ -30,7 +30,7 @@ extern "C" acl_status_t acl__set_error(const char* msg);
 
 namespace acl_amd {
 
-constexpr int kEpBlock = 128;
+constexpr int kEpBlock = 128;  // traj_kernel threads (64 for n <= 64: fewer waves per step)
 
 // Episode workspace: the auction's solve workspace, the control stage's own
 // hand-off region (the head of a WsLayout: pt, mode, rows, ...; kept apart
@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(kEpBlock) traj_kernel(const TrajParams T) {
   const int L = ep.bufflen;
   const double dt = ep.control_dt;
   int nca = 0;
-  for (int v = tid; v < n; v += kEpBlock) {
+  for (int v = tid; v < n; v += (int)blockDim.x) {
     const size_t iv = (size_t)b * n + v;
     double gp[3] = {T.q[3 * iv], T.q[3 * iv + 1], T.q[3 * iv + 2]};
     double gv[3] = {T.vel[3 * iv], T.vel[3 * iv + 1], T.vel[3 * iv + 2]};
@@ -467,7 +467,7 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
     T.step = step;
     T.k = k;
     T.tick = (step % ep.sample_every) == 0;
-    hipLaunchKernelGGL(traj_kernel, dim3(B), dim3(kEpBlock), 0, s, T);
+    hipLaunchKernelGGL(traj_kernel, dim3(B), dim3(n <= 64 ? 64 : kEpBlock), 0, s, T);
     if (hipGetLastError() != hipSuccess) return acl__set_error("traj_kernel launch failed");
   }
   return ACL_OK;

@@ -46,7 +46,7 @@ enum { W_RCH = 3 /* misc[3..4]: a column changed in a round of that parity */,
 
 constexpr int kWBlock = 512;    // solve_wide_kernel: 8 waves per swarm, 2 swarms per CU
 constexpr int kWWaves = kWBlock / 64;
-constexpr int kWABlock = 1024;  // align_wide_kernel
+constexpr int kWABlock = 512;   // align_wide_kernel: a lane per vehicle, two swarms per CU
 constexpr int kWMaxW = kMaxNWide / 64;  // 64-bit words per bitmask row
 constexpr int kWLevels = 3;
 
@@ -78,7 +78,7 @@ __host__ __device__ inline int wal(int x) { return (x + 15) & ~15; }
 
 // align_wide_kernel's LDS
 struct WALayout {
-  int p, qf, sums, adjF, Pin, seen, misc, total;
+  int p, qf, adjF, Pin, seen, misc, total;
 };
 __host__ __device__ inline WALayout make_walayout(int n) {
   const int NW = (n + 63) >> 6;
@@ -86,7 +86,6 @@ __host__ __device__ inline WALayout make_walayout(int n) {
   int o = 0;
   L.p = o;     o = wal(o + n * 24);
   L.qf = o;    o = wal(o + n * 24);   // q in formation order
-  L.sums = o;  o = wal(o + n * 64);   // alignment sums
   L.adjF = o;  o = wal(o + n * NW * 8);
   L.Pin = o;   o = wal(o + n * 2);
   L.seen = o;  o = wal(o + NW * 8);   // permutation check
@@ -449,7 +448,8 @@ __device__ __forceinline__ void wide_control(KCtlParams* Pp, int b, int f, unsig
 }
 
 // diagnostic: s_memtime at phase ends into P.stamps[b][k] (scripts/phase_profile.py)
-__device__ __forceinline__ void wstamp(const SolveParams& P, int b, int k) {
+template <class SP>
+__device__ __forceinline__ void wstamp(SP& P, int b, int k) {
   if (P.stamps && threadIdx.x == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
 }
 
@@ -468,12 +468,15 @@ __device__ __forceinline__ void wstamp(const SolveParams& P, int b, int k) {
 #define WPROF_ADD(acc, x)
 #endif
 
-// Phases 0-1 of the n > 128 solve, one 1 024-thread workgroup per swarm:
-// load, the permutation check, the vehicle-space closed neighbourhoods and
-// every vehicle's 2-D Umeyama alignment (Auctioneer::alignFormation,
-// auctioneer.cpp:347-415; Eigen's two sequential passes, bit for bit), left
-// in the workspace for solve_wide_kernel (WsWide).
-__global__ void __launch_bounds__(kWABlock, 1) align_wide_kernel(const SolveParams P) {
+// Phases 0-1 of the n > 128 solve, one 512-thread workgroup per swarm (a
+// ~58 KB LDS image: two swarms per CU): load, the permutation check, the
+// vehicle-space closed neighbourhoods and every vehicle's 2-D Umeyama
+// alignment (Auctioneer::alignFormation, auctioneer.cpp:347-415; Eigen's two
+// sequential passes, bit for bit), left in the workspace for
+// solve_wide_kernel (WsWide). The alignment: a lane per vehicle, its four
+// sums of each pass as four independent chains over the same members (the
+// members' values are wave-uniform LDS broadcasts, one ds_read2 per pair).
+__global__ void __launch_bounds__(kWABlock, 2) align_wide_kernel(const SolveParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const int NW = (n + 63) >> 6;
@@ -486,7 +489,6 @@ __global__ void __launch_bounds__(kWABlock, 1) align_wide_kernel(const SolvePara
 
   double* p = reinterpret_cast<double*>(smem + L.p);
   double* qf = reinterpret_cast<double*>(smem + L.qf);
-  double* sums = reinterpret_cast<double*>(smem + L.sums);
   unsigned long long* adjF = reinterpret_cast<unsigned long long*>(smem + L.adjF);
   uint16_t* Pin = reinterpret_cast<uint16_t*>(smem + L.Pin);
   unsigned long long* seen = reinterpret_cast<unsigned long long*>(smem + L.seen);
@@ -558,80 +560,77 @@ __global__ void __launch_bounds__(kWABlock, 1) align_wide_kernel(const SolvePara
   // alignment sums, ascending members, branch-free: -0.0 is the exact
   // identity of IEEE addition (-0 + x == x for every x, signed zeros
   // included), so starting from it and adding -0.0 for a non-neighbour gives
-  // the bits of "first term, then acc + term"
-  for (int t = tid; t < 4 * n; t += kWABlock) {
-    const int v = t >> 2, c = t & 3;
-    const int i = Pin[v];
-    const double* src = (c < 2) ? (p + c) : (qf + (c - 2));
-    double acc = -0.0;
-    for (int w = 0; w < NW; ++w) {
-      unsigned long long bits = adjF[i * NW + w];
-      if (w == (i >> 6)) bits |= 1ull << (i & 63);
-      if (w == NW - 1 && (n & 63)) bits &= (1ull << (n & 63)) - 1ull;
-      for (int hf = 0; hf < 2; ++hf) {
-        const unsigned h = (unsigned)(bits >> (32 * hf));
-#pragma unroll 8
-        for (int jb = 0; jb < 32; ++jb) {
-          const int j = 64 * w + 32 * hf + jb;
-          const double val = src[3 * (j < n ? j : 0)];
-          acc = acc + (((h >> jb) & 1u) ? val : -0.0);
-        }
-      }
-    }
-    sums[8 * v + c] = acc;
-  }
-  __syncthreads();
-  for (int t = tid; t < 4 * n; t += kWABlock) {
-    const int v = t >> 2, c = t & 3;
-    const int i = Pin[v];
-    int k = 0;
-    for (int w = 0; w < NW; ++w) {
-      unsigned long long bits = adjF[i * NW + w];
-      if (w == (i >> 6)) bits |= 1ull << (i & 63);
-      k += __popcll(bits);
-    }
-    const double oon = 1.0 / (double)k;
-    const int di = c >> 1, sj = c & 1;
-    const double smj = sums[8 * v + sj] * oon;
-    const double dmi = sums[8 * v + 2 + di] * oon;
-    const bool lazy = (k + 4) < 20;
-    // lazy: the first product is the sum's first term (start from -0.0, the
-    // exact additive identity); otherwise the sum starts at +0.0 (0 + the
-    // first product); a non-neighbour adds -0.0 (no change, bit for bit)
-    double acc = lazy ? -0.0 : 0.0;
-    for (int w = 0; w < NW; ++w) {
-      unsigned long long bits = adjF[i * NW + w];
-      if (w == (i >> 6)) bits |= 1ull << (i & 63);
-      if (w == NW - 1 && (n & 63)) bits &= (1ull << (n & 63)) - 1ull;
-      for (int hf = 0; hf < 2; ++hf) {
-        const unsigned h = (unsigned)(bits >> (32 * hf));
-#pragma unroll 8
-        for (int jb = 0; jb < 32; ++jb) {
-          int j = 64 * w + 32 * hf + jb;
-          j = j < n ? j : 0;
-          const double s0 = p[3 * j + sj] - smj;
-          double d0 = qf[3 * j + di] - dmi;
-          if (lazy) d0 = oon * d0;
-          acc = acc + (((h >> jb) & 1u) ? d0 * s0 : -0.0);
-        }
-      }
-    }
-    sums[8 * v + 4 + c] = lazy ? acc : acc * oon;
-  }
-  __syncthreads();
+  // the bits of "first term, then acc + term". Lane = vehicle v; the four
+  // chains of a pass (x and y of p, of q) are independent.
   double galign = 1.0;
   for (int v = tid; v < n; v += kWABlock) {
     const int i = Pin[v];
+    unsigned long long rowb[kWMaxW];
     int k = 0;
-    for (int w = 0; w < NW; ++w) {
-      unsigned long long bits = adjF[i * NW + w];
+#pragma unroll
+    for (int w = 0; w < kWMaxW; ++w) {
+      unsigned long long bits = w < NW ? adjF[i * NW + w] : 0ull;
       if (w == (i >> 6)) bits |= 1ull << (i & 63);
+      if (w == NW - 1 && (n & 63)) bits &= (1ull << (n & 63)) - 1ull;
+      rowb[w] = bits;
       k += __popcll(bits);
     }
+    double s0 = -0.0, s1 = -0.0, s2 = -0.0, s3 = -0.0;
+#pragma unroll
+    for (int w = 0; w < kWMaxW; ++w) {
+      if (w >= NW) break;
+      for (int hf = 0; hf < 2; ++hf) {
+        const unsigned h = (unsigned)(rowb[w] >> (32 * hf));
+#pragma unroll 4
+        for (int jb = 0; jb < 32; ++jb) {
+          int j = 64 * w + 32 * hf + jb;
+          j = j < n ? j : 0;
+          const double px = p[3 * j], py = p[3 * j + 1], qx = qf[3 * j], qy = qf[3 * j + 1];
+          const bool m = (h >> jb) & 1u;
+          s0 = s0 + (m ? px : -0.0);
+          s1 = s1 + (m ? py : -0.0);
+          s2 = s2 + (m ? qx : -0.0);
+          s3 = s3 + (m ? qy : -0.0);
+        }
+      }
+    }
     const double oon = 1.0 / (double)k;
-    const double sm[2] = {sums[8 * v] * oon, sums[8 * v + 1] * oon};
-    const double dm[2] = {sums[8 * v + 2] * oon, sums[8 * v + 3] * oon};
-    const double S[4] = {sums[8 * v + 4], sums[8 * v + 6], sums[8 * v + 5], sums[8 * v + 7]};
+    const double sm[2] = {s0 * oon, s1 * oon};
+    const double dm[2] = {s2 * oon, s3 * oon};
+    const bool lazy = (k + 4) < 20;
+    // lazy: the first product is the sum's first term (start from -0.0, the
+    // exact additive identity); otherwise the sum starts at +0.0 (0 + the
+    // first product); a non-neighbour adds -0.0 (no change, bit for bit).
+    // c = 2 di + sj: (q_di - dm_di) (p_sj - sm_sj)
+    const double z0 = lazy ? -0.0 : 0.0;
+    double c0 = z0, c1 = z0, c2 = z0, c3 = z0;
+#pragma unroll
+    for (int w = 0; w < kWMaxW; ++w) {
+      if (w >= NW) break;
+      for (int hf = 0; hf < 2; ++hf) {
+        const unsigned h = (unsigned)(rowb[w] >> (32 * hf));
+#pragma unroll 4
+        for (int jb = 0; jb < 32; ++jb) {
+          int j = 64 * w + 32 * hf + jb;
+          j = j < n ? j : 0;
+          const double e0 = p[3 * j] - sm[0], e1 = p[3 * j + 1] - sm[1];
+          double d0 = qf[3 * j] - dm[0], d1 = qf[3 * j + 1] - dm[1];
+          if (lazy) {
+            d0 = oon * d0;
+            d1 = oon * d1;
+          }
+          const bool m = (h >> jb) & 1u;
+          c0 = c0 + (m ? d0 * e0 : -0.0);
+          c1 = c1 + (m ? d0 * e1 : -0.0);
+          c2 = c2 + (m ? d1 * e0 : -0.0);
+          c3 = c3 + (m ? d1 * e1 : -0.0);
+        }
+      }
+    }
+    if (!lazy) {
+      c0 = c0 * oon; c1 = c1 * oon; c2 = c2 * oon; c3 = c3 * oon;
+    }
+    const double S[4] = {c0, c2, c1, c3};
     double R[4], t[2], ga;
     umeyama_finish(S, sm, dm, R, t, &ga);
     galign = ga < galign ? ga : galign;
@@ -653,8 +652,25 @@ __global__ void __launch_bounds__(kWABlock, 1) align_wide_kernel(const SolvePara
 // FUSE: the control phase of a swarm whose vehicles all adopted one
 // assignment runs in this workgroup after its adoption (wide_control);
 // GM: it also reports the gate margin.
+// ACL_WIDE_KARG (default 1): the kernel reads its parameters through a
+// pointer to the kernarg segment, laundered so the compiler reloads a field
+// by a scalar load where it is used instead of holding every pointer and
+// layout offset in SGPRs for the whole kernel (it spilled ~130 of them to
+// VGPR lanes and read them back inside the CBAA rounds).
+#ifndef ACL_WIDE_KARG
+#define ACL_WIDE_KARG 1
+#endif
+typedef const __attribute__((address_space(4))) SolveParams KSolveParams;
+
 template <bool FUSE, bool GM>
-__global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParams P) {
+__global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParams P_) {
+#if ACL_WIDE_KARG
+  KSolveParams* Pk = (KSolveParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(Pk));
+  KSolveParams& P = *Pk;
+#else
+  const SolveParams& P = P_;
+#endif
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const int NW = (n + 63) >> 6;
@@ -803,11 +819,12 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         uint16_t* Tj = T + (((size_t)(j >> 3) * ((n + 7) >> 3)) << 6) + ((j & 7) << 3);
         const int tlo = ((lane >> 3) << 6) + (lane & 7);
         unsigned wu[kWMaxW], key[kWMaxW], nw[kWMaxW], k1[kWMaxW], k2[kWMaxW];
-        // per vehicle: st 0 = undecided, 1 = winner level found (k1), 2 =
-        // done (k2 = the next level its neighbourhood holds, 0 = none);
-        // need = exact ordered scan (ties, NaN, levels exhausted)
-        int st[kWMaxW];
-        bool need[kWMaxW];
+        // per vehicle (bit c of a per-lane VGPR word, not an SGPR lane mask
+        // per c: eight of each would not fit the scalar file): s1m -- a
+        // winner level found (k1), s2m -- done (k2 = the next level its
+        // neighbourhood holds, 0 = none; also the lanes past n), needm --
+        // exact ordered scan (ties, NaN, levels exhausted)
+        unsigned s1m = 0u, s2m = 0u, needm = 0u;
 #pragma unroll
         for (int c = 0; c < kWMaxW; ++c) {
           const int u = lane + 64 * c;
@@ -816,35 +833,34 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           key[c] = ok ? 1u : 0u;  // + the holder's price bits below (1: none)
           nw[c] = (unsigned)n;
           k1[c] = k2[c] = 0u;
-          st[c] = ok ? 0 : 2;
-          need[c] = false;
+          s2m |= (ok ? 0u : 1u) << c;
         }
         {
           // entries of one holder share its price: one (lane-uniform) price
           // per distinct holder, the first few holders; any further ones per
           // entry
-          bool pend[kWMaxW];
+          unsigned pendm = 0u;
 #pragma unroll
-          for (int c = 0; c < kWMaxW; ++c) pend[c] = wu[c] < (unsigned)n;
+          for (int c = 0; c < kWMaxW; ++c) pendm |= (wu[c] < (unsigned)n ? 1u : 0u) << c;
           for (int it = 0; it < 4; ++it) {
             int lw = -1;
 #pragma unroll
             for (int c = 0; c < kWMaxW; ++c) {
-              const unsigned long long bl = __ballot(pend[c]);
+              const unsigned long long bl = __ballot((pendm >> c) & 1u);
               if (lw < 0 && bl) lw = __builtin_amdgcn_readlane((int)wu[c], __ffsll((long long)bl) - 1);
             }
             if (lw < 0) break;
             const unsigned kk = __float_as_uint(price(lw, j)) + 1u;
 #pragma unroll
             for (int c = 0; c < kWMaxW; ++c)
-              if (pend[c] && wu[c] == (unsigned)lw) {
+              if (((pendm >> c) & 1u) && wu[c] == (unsigned)lw) {
                 key[c] = kk;
-                pend[c] = false;
+                pendm &= ~(1u << c);
               }
           }
 #pragma unroll
           for (int c = 0; c < kWMaxW; ++c)
-            if (pend[c]) key[c] = __float_as_uint(price((int)wu[c], j)) + 1u;
+            if ((pendm >> c) & 1u) key[c] = __float_as_uint(price((int)wu[c], j)) + 1u;
         }
         WPROF_T(pk);
         WPROF_ADD(pf_cload, pk - pc0);
@@ -878,66 +894,60 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           // hit: the vehicle's closed neighbourhood holds a vehicle of this
           // level; holder-word outer loop, so the vehicle words' LDS loads
           // issue together, stopping once every active vehicle is hit
-          bool act[kWMaxW], hit[kWMaxW];
-#pragma unroll
-          for (int c = 0; c < kWMaxW; ++c) {
-            act[c] = st[c] < 2 && !need[c];
-            hit[c] = false;
-          }
+          const unsigned actm = ~(s2m | needm) & ((1u << kWMaxW) - 1u);
+          unsigned hitm = 0u;
 #pragma unroll
           for (int w2 = 0; w2 < kWMaxW; ++w2) {
             if (!h[w2]) continue;
-            bool pendw = false;
-#pragma unroll
-            for (int c = 0; c < kWMaxW; ++c) pendw |= act[c] && !hit[c];
-            if (__ballot(pendw) == 0ull) break;
+            if (__ballot((actm & ~hitm) != 0u) == 0ull) break;
 #pragma unroll
             for (int c = 0; c < kWMaxW; ++c)
-              if (act[c] && !hit[c]) hit[c] = (vadj[w2 * n + lane + 64 * c] & h[w2]) != 0ull;
+              if (((actm & ~hitm) >> c) & 1u)
+                hitm |= ((vadj[w2 * n + lane + 64 * c] & h[w2]) != 0ull ? 1u : 0u) << c;
           }
           if (k == 0 && wk >= 0 && wk < n) {
             wk0 = wk;
             Mk0 = Mk;
           }
-          bool open = false;
+          const unsigned took = actm & hitm;   // st 0 -> 1 or 1 -> 2
 #pragma unroll
           for (int c = 0; c < kWMaxW; ++c) {
-            if (act[c] && hit[c]) {
-              if (st[c] == 0) {
+            if ((took >> c) & 1u) {
+              if (!((s1m >> c) & 1u)) {
                 nw[c] = (unsigned)wk;
                 k1[c] = Mk;
-                st[c] = 1;
-                need[c] = tk;
               } else {
                 k2[c] = Mk;
-                st[c] = 2;
               }
             }
-            open |= st[c] < 2 && !need[c];
           }
+          const unsigned first = took & ~s1m, second = took & s1m;
+          s1m |= first;
+          s2m |= second;
+          if (tk) needm |= first;
+          const bool open = (~(s2m | needm) & ((1u << kWMaxW) - 1u)) != 0u;
           if (__ballot(open) == 0ull) break;
           cap = Mk;
         }
         WPROF_T(pl);
         WPROF_ADD(pf_clvl, pl - pk);
-        bool anyneed = false;
+        // undecided, or the runner-up level not found before the level cap
+        needm |= ~(s1m | s2m) & ((1u << kWMaxW) - 1u);
+        if (!exhausted) needm |= s1m & ~s2m;
+        const unsigned donem = s2m & ~needm;
 #pragma unroll
-        for (int c = 0; c < kWMaxW; ++c) {
-          // undecided, or the runner-up level not found before the level cap
-          need[c] |= st[c] == 0 || (st[c] == 1 && !exhausted);
-          anyneed |= need[c];
-          if (!need[c] && st[c] == 2 && k2[c] != 0u)
+        for (int c = 0; c < kWMaxW; ++c)
+          if (((donem >> c) & 1u) && k2[c] != 0u)
             margin_track(mp, __uint_as_float(k1[c] - 1u), __uint_as_float(k2[c] - 1u));
-        }
         WPROF_T(ps0);
-        if (__ballot(anyneed) != 0ull) {
+        if (__ballot(needm != 0u) != 0ull) {
           WPROF_ADD(pf_cnt, 1ull << 21);
           // exact ordered scan (ascending vehid, strict >): ties, NaN prices,
           // vehicles no tracked level decides; the runner-up is the best
           // price of another `who` (entries of one `who` share its price)
 #pragma unroll
           for (int c = 0; c < kWMaxW; ++c) {
-            if (need[c]) {
+            if ((needm >> c) & 1u) {
               const int u = lane + 64 * c;
               float bp = 0.0f, p2 = 0.0f;
               unsigned bw = (unsigned)n;

@@ -79,9 +79,15 @@ def run(C, nb):
     return st
 
 
-def main(B=8, n=100, seed=0):
+def main(B=8, n=100, seed=0, crowd_pct=100):
+    """crowd_pct < 100: positions scaled by crowd_pct/100 about each swarm's
+    centre (bench.py's ca_probe uses 30)."""
     gen = torch.Generator().manual_seed(seed)
     w = workload.simform_workload(B, n, gen, "cpu", formations="philox")
+    if crowd_pct != 100:
+        q = w["q"]
+        cen = q[:, :, :2].mean(dim=1, keepdim=True)
+        q[:, :, :2] = cen + (crowd_pct / 100.0) * (q[:, :, :2] - cen)
     tot = dict(rounds=0, dirty=0, full=0, uni=0, sel=0, lv=[])
     for b in range(B):
         q = w["q"][b].numpy(); p = w["p"][b].numpy(); adj = w["adj"][b].numpy().astype(np.uint8)
