@@ -28,6 +28,8 @@
 //                  them by a prefix count and picks the closest safe edge
 //                  exactly as the reference.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -318,21 +320,15 @@ __device__ void gain_swarm(const CtlParams& P, int b) {
   gain_epilogue(P, b, n, q, uo, &caw, tid, kB);
 }
 
-// One workgroup per swarm; with only_nonuniform (the swarms holding
-// per-vehicle assignments, after the pair kernel or the fused auction took
-// the others) a small grid strides over the launch's swarms, so a launch
-// that finds none costs a few hundred workgroups, not one per swarm.
+// One workgroup per swarm. (A small grid striding over the swarms for the
+// per-vehicle pass measured no faster -- 8.4 vs 8.1 us per empty launch of
+// 4 096 swarms -- and a loop around the walk made the compiler hold the
+// kernel arguments in registers across it: 40-60 VGPR spills.)
 template <int NP, bool GM, int kB>
 __global__ void __launch_bounds__(kB, kB == 256 ? (NP == 5 ? ACL_GAIN_WAVES : 4) : 1) gain_kernel(const CtlParams P) {
-  if (P.only_nonuniform) {
-    for (int b = P.b0 + blockIdx.x; b < P.b0 + P.nb; b += gridDim.x) {
-      if (P.wsMode[b] == 0) continue;  // workgroup-uniform
-      gain_swarm<NP, GM, kB>(P, b);
-      __syncthreads();  // the LDS image is rewritten for the next swarm
-    }
-    return;
-  }
-  gain_swarm<NP, GM, kB>(P, P.b0 + blockIdx.x);
+  const int b = P.b0 + blockIdx.x;
+  if (P.only_nonuniform && P.wsMode[b] == 0) return;  // gain_pair_kernel's swarms
+  gain_swarm<NP, GM, kB>(P, b);
 }
 
 
@@ -343,15 +339,20 @@ __global__ void __launch_bounds__(kB, kB == 256 ? (NP == 5 ? ACL_GAIN_WAVES : 4)
 #define ACL_GAIN_PAIR_WAVES 5
 #endif
 
-// kPB threads per swarm: 256, or 64 for n <= 32 (a 20-vehicle swarm has
-// six 8 x 8 tiles: one wave, a quarter of the waves to launch per call)
+// kPB threads per swarm (256; 64-thread workgroups for n <= 32 measured
+// slower in the n = 20 episode step: 64 vs 46 us per 4 096 swarms)
 template <bool kTiled, bool GM, int kPB>
 __global__ void __launch_bounds__(kPB, kPB == kCtlBlock ? ACL_GAIN_PAIR_WAVES : 8)
     gain_pair_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = P.b0 + blockIdx.x;
   if (P.status[b].flags & ACL_SWARM_BAD_INPUT) return;
-  if (P.wsMode[b] != 0) return;  // per-vehicle assignments: gain_kernel
+  if (P.wsMode[b] != 0) {
+    // per-vehicle assignments: the directed walk on the row-major records,
+    // in this launch (no second launch over every swarm for the few)
+    gain_swarm<5, GM, kPB>(P, b);
+    return;
+  }
   pair_gain_swarm<kPB / 64, kTiled, GM, 1>(P, b, P.fidx[b], smem, threadIdx.x, kPB,
                                            P.wsPt + (size_t)b * P.n);
 }
@@ -1346,9 +1347,6 @@ hipError_t launch_control_prep(const CtlParams& P, const uint16_t* Pgiven, int n
 #define ACL_WIDE_DIRECTED 1
 #endif
 
-// the strided grid of a gain launch over per-vehicle swarms only
-constexpr int kNonuniformGrid = 256;
-
 hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t stream) {
   // the control kernels' dynamic-LDS limit, once per device (not per launch)
   static PerDeviceOnce once;
@@ -1381,31 +1379,27 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
       // uniform swarms: one evaluation per undirected edge; then gain_kernel
       // for the swarms whose vehicles hold different assignments
       const bool tiled = P.gains_tiled != nullptr && P.n <= kMaxN;
-      const bool small = P.n <= 32;
-      const PairLayout PL = make_pair_layout(P.n, small ? 1 : kCtlWaves, tiled);
+      const PairLayout PL = make_pair_layout(P.n, kCtlWaves, tiled);
+      const int lds = std::max(PL.total, make_gain_layout(P.n, kCtlWaves).total);
       const bool gm = P.gate_margin != nullptr;
 #define ACL_PAIR(T_, G_)                                                                     \
   do {                                                                                       \
-    if (small)                                                                               \
-      hipLaunchKernelGGL((gain_pair_kernel<T_, G_, 64>), dim3(nb), dim3(64), PL.total, stream, Q); \
-    else                                                                                     \
-      hipLaunchKernelGGL((gain_pair_kernel<T_, G_, kCtlBlock>), dim3(nb), dim3(kCtlBlock), PL.total, \
-                         stream, Q);                                                         \
+    hipLaunchKernelGGL((gain_pair_kernel<T_, G_, kCtlBlock>), dim3(nb), dim3(kCtlBlock), lds,   \
+                       stream, Q);                                                           \
   } while (0)
       if (tiled && gm) ACL_PAIR(true, true);
       else if (tiled) ACL_PAIR(true, false);
       else if (gm) ACL_PAIR(false, true);
       else ACL_PAIR(false, false);
 #undef ACL_PAIR
-      if (P.all_uniform) return hipGetLastError();
-      Q.only_nonuniform = 1;
+      return hipGetLastError();  // the pair kernel also took the per-vehicle swarms
     }
     // n > 128: 16 waves per swarm (the directed walk keeps per-lane sums;
     // the pair kernel's per-wave accumulators would not fit the LDS)
     const bool big = P.n > kMaxN;
     const GainLayout L = make_gain_layout(P.n, big ? 16 : kCtlWaves);
     const bool gm = P.gate_margin != nullptr;
-    const int gb = Q.only_nonuniform ? (nb < kNonuniformGrid ? nb : kNonuniformGrid) : nb;
+    const int gb = nb;
 #define ACL_GAIN(NP_, G_)                                                                    \
   do {                                                                                       \
     if (big) {                                                                               \

@@ -23,6 +23,9 @@ ap.add_argument("--formations", type=int, default=0)
 ap.add_argument("--L", type=float, default=None)
 ap.add_argument("--crowd", type=float, default=None,
                 help="scale positions about each swarm's centre (collision avoidance active)")
+ap.add_argument("--no-control", action="store_true",
+                help="auction only (the PROF build's CBAA section counters are not overwritten "
+                     "by the collision-avoidance kernel's)")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 gen = torch.Generator(device=dev)
@@ -38,10 +41,11 @@ if args.crowd:
 lib = L.lib()
 lib.acl_internal_set_stamps.argtypes = [ct.c_void_p]
 st = torch.zeros((args.B, 16), dtype=torch.int64, device=dev)
-engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"])  # warm
+ctl = not args.no_control
+engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=ctl)  # warm
 torch.cuda.synchronize()
 lib.acl_internal_set_stamps(ct.c_void_p(st.data_ptr()))
-engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"])
+engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=ctl)
 torch.cuda.synchronize()
 lib.acl_internal_set_stamps(ct.c_void_p(0))
 s = st.cpu().numpy().astype(np.float64)
