@@ -10,7 +10,7 @@ mkdir -p gpurun_out/$OUT
 for C in FETCH_SIZE WRITE_SIZE; do
   rm -rf /tmp/pmc_$C
   timeout -k 10 600 rocprofv3 --pmc $C -d /tmp/pmc_$C -o run --output-format csv -- \
-      python3 bench.py --steps 2 --warmup 1 --no-cpu ${BENCH_ARGS} \
+      python3 bench.py --steps 2 --warmup 1 --no-cpu --no-ca-probe ${BENCH_ARGS} \
       > gpurun_out/$OUT/bench_$C.json 2> gpurun_out/$OUT/rocprof_$C.err || { echo "pmc $C failed"; tail -20 gpurun_out/$OUT/rocprof_$C.err; exit 1; }
   f=$(find /tmp/pmc_$C -name "*counter_collection.csv" | head -1)
   head -1 "$f" > gpurun_out/$OUT/$C.csv

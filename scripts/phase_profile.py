@@ -65,7 +65,7 @@ if (s[:, 7] > 0).all():
 # CBAA column-step sections (a -DACL_AUCTION_PROF=1 build): cycles summed
 # over a swarm's waves, and the counts of evaluated columns, walks and scans
 sec = st.cpu().numpy()[:, 7:16].astype(np.uint64)
-if args.n <= 128 and not args.crowd and sec[:, :8].any():
+if args.n <= 128 and (not args.crowd or args.no_control) and sec[:, :8].any():
     SN = ["level 0", "levels", "margin bound", "runner-up walk", "exact scan", "write-back",
           "selects+barrier", "column barrier"]
     tot8 = sec[:, :8].astype(np.float64).sum()
@@ -97,7 +97,7 @@ if args.n > 128 and sec[:, :4].any():
     for k, nm in enumerate(["T load + keys", "levels", "write-back"]):
         print(f"    column {nm:14s} wave-cycles/swarm {sec[:, 6 + k].astype(np.float64).mean():12.0f}")
 # collision avoidance (a -DACL_CA_PROF=1 build, --crowd): ca_kernel wave-cycles
-if args.crowd:
+if args.crowd and not args.no_control:
     x = st.cpu().numpy()[:, 8:12].astype(np.float64)
     cnt = x[:, 3].sum()
     print(f"  ca close vehicles {cnt:.0f} ({cnt / args.B:.1f} per swarm)")
