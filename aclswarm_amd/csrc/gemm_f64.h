@@ -37,6 +37,13 @@ struct GemmJob {
   double alpha, beta;
   const int* skip;  // job skipped when non-NULL and *skip != 0
   double* err2;     // non-NULL (default kernel only): += |D - I|_F^2 of the stored D
+  // operand transform (default kernel only): operands in tmask (bit 0 A,
+  // bit 1 B, bit 2 C) are read as (x - [diagonal] tdiag) * (1 / *tnrm) --
+  // the Newton-Schulz start Z0 = (W - eps I) / nrm formed while staging
+  // instead of a pass that writes it
+  const double* tnrm = nullptr;
+  double tdiag = 0.0;
+  int tmask = 0;
 };
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -359,21 +366,23 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
     if (TB) { j = e % TILE; kb = e / TILE; }
     else    { kb = e & 15; j = e >> 4; }
   };
+  const int tmask = J.tmask;
+  const double tinv = tmask ? 1.0 / *J.tnrm : 1.0, tdiag = J.tdiag;
   auto load = [&](int k0) {
 #pragma unroll
     for (int r = 0; r < EPT; ++r) {
       int i, kk;
       a_idx(r, i, kk);
       const int gi = m0 + i, gk = k0 + kk;
-      ra[r] = (gi < J.m && gk < J.k)
-                  ? (TA ? J.A[gk + (size_t)gi * J.lda] : J.A[gi + (size_t)gk * J.lda])
-                  : 0.0;
+      const bool ina = gi < J.m && gk < J.k;
+      ra[r] = ina ? (TA ? J.A[gk + (size_t)gi * J.lda] : J.A[gi + (size_t)gk * J.lda]) : 0.0;
+      if ((tmask & 1) && ina) ra[r] = (ra[r] - (gi == gk ? tdiag : 0.0)) * tinv;
       int j, kb;
       b_idx(r, j, kb);
       const int gj = n0 + j, gkb = k0 + kb;
-      rb[r] = (gj < J.n && gkb < J.k)
-                  ? (TB ? J.B[gj + (size_t)gkb * J.ldb] : J.B[gkb + (size_t)gj * J.ldb])
-                  : 0.0;
+      const bool inb = gj < J.n && gkb < J.k;
+      rb[r] = inb ? (TB ? J.B[gj + (size_t)gkb * J.ldb] : J.B[gkb + (size_t)gj * J.ldb]) : 0.0;
+      if ((tmask & 2) && inb) rb[r] = (rb[r] - (gj == gkb ? tdiag : 0.0)) * tinv;
     }
   };
   auto store = [&](int buf) {
@@ -435,7 +444,11 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
     const int gj = n0 + cb * 16 + (lane >> 4) + 4 * r;
     if (gi < J.m && gj < J.n) {
       double v = alpha * a;
-      if (beta != 0.0) v += beta * J.C[gi + (size_t)gj * J.ldc];
+      if (beta != 0.0) {
+        double c = J.C[gi + (size_t)gj * J.ldc];
+        if (tmask & 4) c = (c - (gi == gj ? tdiag : 0.0)) * tinv;
+        v += beta * c;
+      }
       J.D[gi + (size_t)gj * J.ldd] = v;
       if (SYM && bi != bj) J.D[gj + (size_t)gi * J.ldd] = v;
       const double d = v - (gi == gj ? 1.0 : 0.0);
