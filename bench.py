@@ -54,6 +54,9 @@ CONFIGS = {
 }
 METRIC_C5 = "batched ADMM formation-gain designs/sec (N=100, F=1024); % fp64 MFMA roofline"
 FP64_MATRIX_PEAK_TF = 78.6  # MI355X fp64 matrix, AMD spec (the microarch guide has no fp64 row)
+# the instruction's ceiling measured on the box: v_mfma_f64_16x16x4f64 chains
+# without memory traffic (scripts/mfma_f64_peak.hip, profiles/r4_mfma_f64_peak.txt)
+FP64_MFMA_MEASURED_TF = 41.0
 
 
 def _free_port():
@@ -301,6 +304,9 @@ def bench_c5(args, world, rank, local):
                              "symmetric products as upper-triangle tiles) / batch time",
                      "achieved": ach, "peak": FP64_MATRIX_PEAK_TF, "unit": "TFLOP/s",
                      "frac": ach / FP64_MATRIX_PEAK_TF, "traffic": None,
+                     "measured_instruction_peak": FP64_MFMA_MEASURED_TF,
+                     "frac_of_measured_peak": ach / FP64_MFMA_MEASURED_TF,
+                     "measured_peak_source": "profiles/r4_mfma_f64_peak.txt (scripts/mfma_f64_peak.hip)",
                      "gemm_flops_per_batch": flops, "batch_ms_events": batch_ms},
         "iters_xy": {int(k): int(v) for k, v in zip(*torch.unique(itn[:, 0], return_counts=True))},
         "iters_z": {int(k): int(v) for k, v in zip(*torch.unique(itn[:, 1], return_counts=True))},
