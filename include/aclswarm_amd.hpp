@@ -717,6 +717,30 @@ class Solver {
 
 }  // namespace admm
 
+// ============================================================================
+// ADMM (aclswarm/include/aclswarm/admm.h:27-40, src/admm.cpp:12-55): the
+// wrapper of the MATLAB-Coder ADMMGainDesign3D -- codegen semantics (the
+// LINPACK complement basis, acl_admm_params_t defaults) and the wrapper's
+// |a| <= 1e-10 zeroing (admm.cpp:50, applied by acl_admm_solve_batch).
+// ============================================================================
+class ADMM {
+ public:
+  explicit ADMM(const size_t n) : solver_(params_for_codegen()) { (void)n; }
+
+  /* admm.cpp:34-55: p is n x 3 (PtsMat), adjmat n x n (AdjMat) */
+  GainMat calculateFormationGains(const PtsMat& p, const AdjMat& adjmat) {
+    return solver_.solve(p.transpose(), adjmat.template cast<double>());
+  }
+
+ private:
+  static admm::Solver::Params params_for_codegen() {
+    admm::Solver::Params prm;
+    prm.basis = ACL_ADMM_BASIS_LINPACK;
+    return prm;
+  }
+  admm::Solver solver_;
+};
+
 }  // namespace amd
 }  // namespace aclswarm
 }  // namespace acl

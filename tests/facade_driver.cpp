@@ -15,6 +15,7 @@
 //         f64 u[n][3]; i32 iters[2]; f64 A[9m^2] (column-major)
 #include <stdio.h>
 
+#include <algorithm>
 #include <functional>
 #include <memory>
 #include <vector>
@@ -195,6 +196,26 @@ extern "C" int facade_run(const char* in_path, const char* out_path) {
     fclose(out);
   } catch (const std::exception& e) {
     fprintf(stderr, "facade_driver: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}
+
+// The reference's ADMM wrapper class (aclswarm/src/admm.cpp:34-55):
+// pts n x 3 (PtsMat, column-major), adj n x n u8 (AdjMat), gains out 3n x 3n
+// column-major. Codegen semantics.
+extern "C" int facade_admm_codegen(int n, const double* pts_nx3, const uint8_t* adj_nxn,
+                                   double* gains_out) {
+  try {
+    amd::PtsMat p(n, 3);
+    amd::AdjMat adj(n, n);
+    std::copy(pts_nx3, pts_nx3 + (size_t)3 * n, p.data());
+    std::copy(adj_nxn, adj_nxn + (size_t)n * n, adj.data());
+    amd::ADMM admm((size_t)n);
+    const amd::GainMat A = admm.calculateFormationGains(p, adj);
+    std::copy(A.data(), A.data() + (size_t)9 * n * n, gains_out);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "facade_admm_codegen: %s\n", e.what());
     return 1;
   }
   return 0;

@@ -137,3 +137,29 @@ def test_facade_admm_solver_nine_agent(tmp_path):
     zs, worst = nine_agent_violations(got["A"], adj9)
     assert abs(zs) < d["tol"] and worst < d["tol"], (zs, worst)
     assert (got["iters"] > 0).all()
+
+
+def test_facade_admm_wrapper_class_codegen():
+    """The reference's ADMM wrapper (aclswarm/src/admm.cpp:34-55,
+    include/aclswarm/admm.h:27-40) through the facade's ADMM class: codegen
+    semantics, so the reference's own codegen outputs (tests/golden,
+    admm_golden.npz) within 1e-5 relative and the MATLAB 12 x 12 matrices of
+    test_admm.cpp:10-80 within 1e-8."""
+    import admm_cases as AC
+    lib = ct.CDLL(LIB)
+    lib.facade_admm_codegen.argtypes = [ct.c_int, ct.c_void_p, ct.c_void_p, ct.c_void_p]
+
+    def run(p, adj):
+        n = p.shape[0]
+        P = np.asfortranarray(p, np.float64)
+        A8 = np.asfortranarray(np.asarray(adj) != 0, np.uint8)
+        out = np.zeros((3 * n, 3 * n), np.float64, order="F")
+        assert lib.facade_admm_codegen(n, P.ctypes.data, A8.ctypes.data, out.ctypes.data) == 0
+        return out
+    d = H.load_json("admm_test_admm.json")
+    for c in d["cases"]:
+        A = run(np.array(c["p"]), np.array(c["adj"]))
+        assert np.linalg.norm(A - np.array(c["A"])) < d["tol"]
+    for c in [c for c in AC.load() if c["p"].shape[0] <= 20][:4]:
+        A = run(c["p"], c["adj"])
+        assert AC.rel_err(A, AC.assemble(c["Axy"], c["Az"])) < 1e-5, c["name"]
