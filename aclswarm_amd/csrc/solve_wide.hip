@@ -111,7 +111,7 @@ __host__ __device__ inline WLayout make_wlayout(int n) {
   L.ccw = o;   o = wal(o + n * 2);    // column price cache: a holder of task j
   L.ccp = o;   o = wal(o + n * 4);    // and its price for j
   L.valid = o; o = wal(o + n);
-  L.masks = o; o = wal(o + 4 * NW * 8);                // dmask[2][NW], obm[2][NW]
+  L.masks = o; o = wal(o + 5 * NW * 8);                // dmask[2][NW], obm[2][NW], unif[NW]
   L.seen = o;  o = wal(o + kWWaves * NW * 8);         // per-wave validity checks
   L.misc = o;  o = wal(o + 64);
   L.total = o;
@@ -690,6 +690,10 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   unsigned char* validv = smem + L.valid;
   unsigned long long* dmask = reinterpret_cast<unsigned long long*>(smem + L.masks);
   unsigned long long* obm = dmask + 2 * NW;
+  // unif bit j: column j holds one `who` for every vehicle (as of its last
+  // update; a bid written into it clears the bit and dirties the column), so
+  // at the fixed point all tables agree <=> every bit is set
+  unsigned long long* unif = dmask + 4 * NW;
   unsigned long long* seen = reinterpret_cast<unsigned long long*>(smem + L.seen);
   int* misc = reinterpret_cast<int*>(smem + L.misc);
 
@@ -744,6 +748,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       Ptin[pv] = (uint16_t)v;
     }
     for (int k = tid; k < 4 * NW; k += kWBlock) dmask[k] = 0ull;
+    for (int k = tid; k < NW; k += kWBlock) unif[k] = ~0ull;  // every column all `none`
     for (int k = tid; k < n; k += kWBlock) ccw[k] = (uint16_t)n;
     if (tid < 16) misc[tid] = 0;
   }
@@ -794,6 +799,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     if (task >= 0 && lane == 0) {
       T[tix(n, task, v)] = (uint16_t)v;
       atomicOr(&dmask[NW + (task >> 6)], 1ull << (task & 63));
+      atomicAnd(&unif[task >> 6], ~(1ull << (task & 63)));
     }
   }
   __syncthreads();
@@ -1002,6 +1008,10 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           misc[W_RCH + par] = 1;
           if (anymx || nonfinite) atomicOr(&dmask[npar * NW + (j >> 6)], 1ull << (j & 63));
         }
+        if (lane == 0) {
+          if (anymx) atomicAnd(&unif[j >> 6], ~(1ull << (j & 63)));
+          else atomicOr(&unif[j >> 6], 1ull << (j & 63));
+        }
         WPROF_T(pc1);
         WPROF_ADD(pf_col, pc1 - pc0 - (ps1 - ps0));
         WPROF_ADD(pf_cwb, pc1 - ps1);
@@ -1037,6 +1047,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           if (task >= 0 && lane == 0) {
             T[tix(n, task, v)] = (uint16_t)v;
             atomicOr(&dmask[npar * NW + (task >> 6)], 1ull << (task & 63));
+            atomicAnd(&unif[task >> 6], ~(1ull << (task & 63)));
           }
           WPROF_T(pr1);
           WPROF_ADD(pf_sel, pr1 - pr0);
@@ -1079,13 +1090,16 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   // Do all vehicles hold vehicle 0's table? T is column-major, so compare
   // each column with its row-0 entry (coalesced). Then one table decides
   // every vehicle's validity (isValidAssignment of row 0, as auction.hip).
-  {
-    bool diff = false;
-    for (int j = wave; j < n; j += kWWaves) {
-      const uint16_t t0 = T[tix(n, j, 0)];
-      for (int u = lane; u < n; u += 64) diff |= T[tix(n, j, u)] != t0;
+  // Do all vehicles hold vehicle 0's table? <=> every column is uniform
+  // (the unif bits; no pass over the n^2 table)
+  if (tid == 0) {
+    bool agree = true;
+    for (int w = 0; w < NW; ++w) {
+      const unsigned long long need =
+          (w == NW - 1 && (n & 63)) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+      agree &= (unif[w] & need) == need;
     }
-    if (__any(diff) && lane == 0) misc[M_AGREE] = 0;
+    if (!agree) misc[M_AGREE] = 0;
   }
   __syncthreads();
   const bool allagree = misc[M_AGREE] != 0;
