@@ -739,7 +739,7 @@ __device__ __forceinline__ bool ca_resolve_serial(int nslot, double* caA, signed
 }
 
 #ifndef ACL_CA_GRID
-#define ACL_CA_GRID 1024
+#define ACL_CA_GRID 2048
 #endif
 // diagnostic build (-DACL_CA_PROF=1, scripts/phase_profile.py --crowd): wave
 // cycles of the sector build, the resolution and the rest into
