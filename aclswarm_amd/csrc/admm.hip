@@ -45,6 +45,9 @@ namespace admm {
 constexpr int kT = 256;         // threads per workgroup of the per-part kernels
 constexpr int kMaxN = 1024;     // points per formation
 constexpr int kMaxRows = 2047;  // graph rows (K) per part: the Gram system is (K+1)^2
+#ifndef ACL_ADMM_CHUNK
+#define ACL_ADMM_CHUNK 1024  // formations per pass (~16 GB of workspace at N = 100; 512: 4 728 vs 4 846 formations/s at C5)
+#endif
 constexpr int kNsMax = 64;      // Newton-Schulz iterations before a part is declared failed
 constexpr double kNsScale = 1.5;  // Z0 scaling: |W - eps I|_inf / kNsScale (norm_kernel)
 // A part's sign iteration has converged when |Z^2 - I|_F^2 < kNsTol * dim;
@@ -1199,7 +1202,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     if (e_ != hipSuccess) return hipfail(e_, what); \
   } while (0)
 
-  const int chunk = std::min(F, 512);
+  const int chunk = std::min(F, ACL_ADMM_CHUNK);
   const int np_max = 2 * n;
   const size_t qstride = (size_t)np_max * np_max;
   const size_t kcap = (size_t)n * (n - 1);  // xy graph rows at most
