@@ -339,10 +339,11 @@ __global__ void __launch_bounds__(kB, kB == 256 ? (NP == 5 ? ACL_GAIN_WAVES : 4)
 #define ACL_GAIN_PAIR_WAVES 5
 #endif
 
-// kPB threads per swarm (256; 64-thread workgroups for n <= 32 measured
-// slower in the n = 20 episode step: 64 vs 46 us per 4 096 swarms)
+// kPB threads per swarm: 256, or one wave for n <= 32 (launch_control). The
+// occupancy bound is the same for every size (a bound of 8 waves per SIMD
+// for the small block capped it at 64 VGPRs: spills, slower)
 template <bool kTiled, bool GM, int kPB>
-__global__ void __launch_bounds__(kPB, kPB == kCtlBlock ? ACL_GAIN_PAIR_WAVES : 8)
+__global__ void __launch_bounds__(kPB, ACL_GAIN_PAIR_WAVES)
     gain_pair_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = P.b0 + blockIdx.x;
@@ -1379,13 +1380,22 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
       // uniform swarms: one evaluation per undirected edge; then gain_kernel
       // for the swarms whose vehicles hold different assignments
       const bool tiled = P.gains_tiled != nullptr && P.n <= kMaxN;
-      const PairLayout PL = make_pair_layout(P.n, kCtlWaves, tiled);
-      const int lds = std::max(PL.total, make_gain_layout(P.n, kCtlWaves).total);
+#ifndef ACL_PAIR_SMALL_BLOCK
+#define ACL_PAIR_SMALL_BLOCK 64  // threads per swarm for n <= 32 (one wave; episode n = 20: 81 -> 70 us per step)
+#endif
+      constexpr int kSB = ACL_PAIR_SMALL_BLOCK > 0 ? ACL_PAIR_SMALL_BLOCK : kCtlBlock;
+      const bool small = ACL_PAIR_SMALL_BLOCK > 0 && P.n <= 32;
+      const int pw = small ? kSB / 64 : kCtlWaves;
+      const PairLayout PL = make_pair_layout(P.n, pw, tiled);
+      const int lds = std::max(PL.total, make_gain_layout(P.n, pw).total);
       const bool gm = P.gate_margin != nullptr;
 #define ACL_PAIR(T_, G_)                                                                     \
   do {                                                                                       \
-    hipLaunchKernelGGL((gain_pair_kernel<T_, G_, kCtlBlock>), dim3(nb), dim3(kCtlBlock), lds,   \
-                       stream, Q);                                                           \
+    if (small)                                                                               \
+      hipLaunchKernelGGL((gain_pair_kernel<T_, G_, kSB>), dim3(nb), dim3(kSB), lds, stream, Q); \
+    else                                                                                     \
+      hipLaunchKernelGGL((gain_pair_kernel<T_, G_, kCtlBlock>), dim3(nb), dim3(kCtlBlock), lds, \
+                         stream, Q);                                                         \
   } while (0)
       if (tiled && gm) ACL_PAIR(true, true);
       else if (tiled) ACL_PAIR(true, false);
@@ -1416,7 +1426,10 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
 #undef ACL_GAIN
   } else {
     // a fixed grid striding over the device-side count of listed swarms
-    if (P.n <= kMaxN) {
+#ifndef ACL_CA_PAIR_MIN_N
+#define ACL_CA_PAIR_MIN_N 33  // smaller swarms: the per-vehicle ca_kernel (episode n = 20: 81 -> 77 us per step)
+#endif
+    if (P.n <= kMaxN && P.n >= ACL_CA_PAIR_MIN_N) {
       const int lp = ca_pair_layout(P.n).total;
       hipLaunchKernelGGL(ca_pair_kernel, dim3(nb < ACL_CA_GRID ? nb : ACL_CA_GRID), dim3(kCaPT), lp,
                          stream, P);
