@@ -96,7 +96,7 @@ __host__ __device__ inline WALayout make_walayout(int n) {
 
 // solve_wide_kernel's LDS
 struct WLayout {
-  int p, qv, vadj, Pin, Ptin, ccw, ccp, valid, masks, seen, misc, total;
+  int p, qv, vadj, Pin, Ptin, ccw, ccp, cuw, valid, masks, seen, misc, total;
 };
 
 __host__ __device__ inline WLayout make_wlayout(int n) {
@@ -110,6 +110,7 @@ __host__ __device__ inline WLayout make_wlayout(int n) {
   L.Ptin = o;  o = wal(o + n * 2);
   L.ccw = o;   o = wal(o + n * 2);    // column price cache: a holder of task j
   L.ccp = o;   o = wal(o + n * 4);    // and its price for j
+  L.cuw = o;   o = wal(o + n * 2);    // column j's one `who` while its unif bit is set
   L.valid = o; o = wal(o + n);
   L.masks = o; o = wal(o + 5 * NW * 8);                // dmask[2][NW], obm[2][NW], unif[NW]
   L.seen = o;  o = wal(o + kWWaves * NW * 8);         // per-wave validity checks
@@ -153,21 +154,30 @@ struct WPrice {
 // `fresh`: the row is all `none` (the START bid). Tracks the margin of the
 // decisive comparisons (include/aclswarm_amd.h) in m.
 __device__ int wide_select(int n, int NW, int v, int lane, const WPrice& price,
-                           const uint16_t* T, const uint16_t* ccw, const float* ccp, bool fresh,
+                           const uint16_t* T, const uint16_t* ccw, const float* ccp,
+                           const uint16_t* cuw, const unsigned long long* unif, bool fresh,
                            MarginPair& m) {
   unsigned key[kWMaxW];
   float cvs[kWMaxW], prs[kWMaxW];
   bool other[kWMaxW];
   unsigned lm = 0u;
   int wv[kWMaxW];
-  // row v of the tiled table: task j = lane + 64 c at Tv[lo + c * 512 n8]
+  // row v of the tiled table: task j = lane + 64 c at Tv[lo + c * 512 n8];
+  // a column whose unif bit is set holds cuw[j] in every row (a bid that
+  // breaks that clears the bit, and changes only its own row), so only the
+  // other columns' entries are read from the table
   const int n8 = (n + 7) >> 3;
   const uint16_t* Tv = T + (((v >> 3) << 6) + (v & 7));
   const int lo = (((lane >> 3) * n8) << 6) + ((lane & 7) << 3);
 #pragma unroll
   for (int c = 0; c < kWMaxW; ++c) {
     const int j = lane + 64 * c;
-    wv[c] = (fresh || c >= NW || j >= n) ? n : Tv[lo + c * (n8 << 9)];
+    if (fresh || c >= NW || j >= n) {
+      wv[c] = n;
+    } else {
+      const bool uni = (unif[c] >> lane) & 1ull;
+      wv[c] = uni ? cuw[j] : Tv[lo + c * (n8 << 9)];
+    }
   }
 #pragma unroll
   for (int c = 0; c < kWMaxW; ++c) {
@@ -687,6 +697,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   uint16_t* Ptin = reinterpret_cast<uint16_t*>(smem + L.Ptin);
   uint16_t* ccw = reinterpret_cast<uint16_t*>(smem + L.ccw);
   float* ccp = reinterpret_cast<float*>(smem + L.ccp);
+  uint16_t* cuw = reinterpret_cast<uint16_t*>(smem + L.cuw);
   unsigned char* validv = smem + L.valid;
   unsigned long long* dmask = reinterpret_cast<unsigned long long*>(smem + L.masks);
   unsigned long long* obm = dmask + 2 * NW;
@@ -749,7 +760,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     }
     for (int k = tid; k < 4 * NW; k += kWBlock) dmask[k] = 0ull;
     for (int k = tid; k < NW; k += kWBlock) unif[k] = ~0ull;  // every column all `none`
-    for (int k = tid; k < n; k += kWBlock) ccw[k] = (uint16_t)n;
+    for (int k = tid; k < n; k += kWBlock) ccw[k] = cuw[k] = (uint16_t)n;
     if (tid < 16) misc[tid] = 0;
   }
   __syncthreads();
@@ -795,7 +806,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
 
   // ---------------- phase 3: CBAA ------------------------------------------
   for (int v = wave; v < n; v += kWWaves) {
-    const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, true, mp);
+    const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, cuw, unif, true, mp);
     if (task >= 0 && lane == 0) {
       T[tix(n, task, v)] = (uint16_t)v;
       atomicOr(&dmask[NW + (task >> 6)], 1ull << (task & 63));
@@ -990,7 +1001,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         for (int c = 0; c < kWMaxW; ++c) {
           const int u = lane + 64 * c;
           const bool ok = c < NW && u < n;
-          if (ok) Tj[tlo + (c << 9)] = (uint16_t)nw[c];
+          if (ok && nw[c] != wu[c]) Tj[tlo + (c << 9)] = (uint16_t)nw[c];  // changed entries only
           // outbid (:502): a per-lane bit, published once per wave and round
           obf |= (vflag(ok) & vflag(wu[c] == (unsigned)u) & vflag(nw[c] != (unsigned)u)) << c;
           ch |= nw[c] != wu[c];
@@ -1009,8 +1020,12 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           if (anymx || nonfinite) atomicOr(&dmask[npar * NW + (j >> 6)], 1ull << (j & 63));
         }
         if (lane == 0) {
-          if (anymx) atomicAnd(&unif[j >> 6], ~(1ull << (j & 63)));
-          else atomicOr(&unif[j >> 6], 1ull << (j & 63));
+          if (anymx) {
+            atomicAnd(&unif[j >> 6], ~(1ull << (j & 63)));
+          } else {
+            cuw[j] = (uint16_t)nw0;
+            atomicOr(&unif[j >> 6], 1ull << (j & 63));
+          }
         }
         WPROF_T(pc1);
         WPROF_ADD(pf_col, pc1 - pc0 - (ps1 - ps0));
@@ -1043,7 +1058,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           if ((idx2++ % kWWaves) != wave) continue;
           WPROF_T(pr0);
           WPROF_ADD(pf_cnt, 1ull << 42);
-          const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, false, mp);
+          const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, cuw, unif, false, mp);
           if (task >= 0 && lane == 0) {
             T[tix(n, task, v)] = (uint16_t)v;
             atomicOr(&dmask[npar * NW + (task >> 6)], 1ull << (task & 63));
