@@ -44,6 +44,18 @@ struct GemmJob {
   const double* tnrm = nullptr;
   double tdiag = 0.0;
   int tmask = 0;
+  // trace partials (default kernel only): a diagonal tile (bi == bj) stores
+  // the sum of its diagonal at trp[bi] (fixed-order sums: deterministic)
+  double* trp = nullptr;
+  // scaled Newton-Schulz update (default kernel only): with nsp set, the
+  // product D = alpha Z Y + beta Z (Y = Z^2) is taken for a Z -- alpha *= a^3,
+  // beta *= a -- with a = sqrt(m / tr Y) capped at nscap, tr Y = the nsn
+  // partials at nsp summed in order; a = 1 when *nserr < nstol (the part's
+  // last update) or the ratio is not a number
+  const double* nsp = nullptr;
+  const double* nserr = nullptr;
+  int nsn = 0;
+  double nscap = 0.0, nstol = 0.0;
 };
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -437,8 +449,19 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[(wave * 4 + r) * 64 + lane] = acc44[r];
   __syncthreads();
-  const double alpha = J.alpha, beta = J.beta;
+  double alpha = J.alpha, beta = J.beta;
+  if (J.nsp && !(*J.nserr < J.nstol)) {
+    double tr = 0.0;
+    for (int b = 0; b < J.nsn; ++b) tr += J.nsp[b];
+    const double a = sqrt((double)J.m / tr);
+    if (a == a) {
+      const double ac = a < J.nscap ? a : J.nscap;
+      alpha *= ac * ac * ac;
+      beta *= ac;
+    }
+  }
   double e2 = 0.0;  // |D - I|_F^2 of this wave's stored elements (J.err2)
+  double tr = 0.0;  // this lane's diagonal elements (J.trp), in put order
   auto put = [&](int si, int cb, int r, double a) {
     const int gi = m0 + si * 16 + (lane & 15);
     const int gj = n0 + cb * 16 + (lane >> 4) + 4 * r;
@@ -453,6 +476,7 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
       if (SYM && bi != bj) J.D[gj + (size_t)gi * J.ldd] = v;
       const double d = v - (gi == gj ? 1.0 : 0.0);
       e2 += (SYM && bi != bj) ? 2.0 * (d * d) : d * d;
+      if (gi == gj) tr += v;
     }
   };
 #pragma unroll
@@ -474,6 +498,13 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
   if (J.err2) {  // the Newton-Schulz error of Y = Z^2, fused (no pass over Y)
     for (int o = 32; o > 0; o >>= 1) e2 += __shfl_xor(e2, o, 64);
     if (lane == 0) atomicAdd(J.err2, e2);
+  }
+  if (J.trp && bi == bj) {  // workgroup-uniform; the B buffer is free after the K loop
+    for (int o = 32; o > 0; o >>= 1) tr += __shfl_xor(tr, o, 64);
+    double* tw = &Bsh[0][0];
+    if (lane == 0) tw[wave] = tr;
+    __syncthreads();
+    if (tid == 0) J.trp[bi] = ((tw[0] + tw[1]) + tw[2]) + tw[3];
   }
 }
 
