@@ -494,13 +494,23 @@ __global__ void __launch_bounds__(kT) chol_kernel(const Part* parts) {
 // rows j..K1-1, at pk(j) - j + i), for systems whose triangle fits
 // (chol_lds_bytes <= 160 KiB: K1 <= 198). Every element takes the same
 // operations in the same order as in chol_kernel (pivot test, scale, the
-// trailing updates in k order, the column-per-thread substitution), so L^-1
-// is bit-identical; only the factor's home moves from global memory, where
-// the trailing update was a chain of dependent round trips, to LDS. The
-// trailing update runs one column per wave, lanes over its rows.
+// trailing updates in k order, each row's substitution sum in m order), so
+// L^-1 is bit-identical. One barrier per column step: every wave takes the
+// pivot and the scaled column k itself (lanes over rows, in registers) and
+// wave 0 stores column k one step late (no later step reads it). The
+// substitution: a wave per column of L^-1, lanes over its rows, the running
+// sums in registers (no round trips through the global column).
 constexpr int kCholT = 512;
+constexpr int kCholRows = 4;  // rows per lane: K1 <= 256
 inline size_t chol_lds_bytes(int K1) {
   return ((size_t)K1 * (K1 + 1) / 2 + (size_t)K1) * sizeof(double) + (size_t)K1 + 16;
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 __global__ void __launch_bounds__(kCholT) chol_lds_kernel(const Part* parts) {
@@ -512,7 +522,6 @@ __global__ void __launch_bounds__(kCholT) chol_lds_kernel(const Part* parts) {
   double* Lp = lsm;
   double* d0 = Lp + (size_t)K1 * (K1 + 1) / 2;
   unsigned char* keep = reinterpret_cast<unsigned char*>(d0 + K1);
-  __shared__ int s_keep;
   // column j of L: col(j)[i] = L[i, j], i >= j
   auto col = [&](int j) { return Lp + ((size_t)j * K1 - (size_t)j * (j - 1) / 2) - j; };
   for (int j = wave; j < K1; j += kW) {
@@ -522,43 +531,80 @@ __global__ void __launch_bounds__(kCholT) chol_lds_kernel(const Part* parts) {
   }
   for (int k = tid; k < K1; k += kCholT) d0[k] = P.Gam[k + (size_t)k * K1];
   __syncthreads();
+  double lk[kCholRows];    // scaled column k, rows k + 1 + lane + 64 t
+  double piv = 0.0;
+  bool kp = false;
   for (int k = 0; k < K1; ++k) {
-    double* ck = col(k);
-    if (tid == 0) {
-      const double d = ck[k];
-      s_keep = d > 1e-10 * d0[k];
-      keep[k] = (unsigned char)s_keep;
-      if (s_keep) ck[k] = sqrt(d);
+    if (wave == 0 && k > 0) {  // column k - 1, held since the last step
+      double* cp = col(k - 1);
+      if (lane == 0) cp[k - 1] = kp ? piv : 0.0;
+#pragma unroll
+      for (int t = 0; t < kCholRows; ++t) {
+        const int i = k + lane + 64 * t;
+        if (i < K1) cp[i] = lk[t];
+      }
     }
-    __syncthreads();
-    const bool kp = s_keep;
-    const double piv = ck[k];
-    for (int i = k + 1 + tid; i < K1; i += kCholT) {
-      double& x = ck[i];
-      x = kp ? x / piv : 0.0;
+    const double* ck = col(k);
+    const double d = ck[k];
+    kp = d > 1e-10 * d0[k];
+    piv = kp ? sqrt(d) : 0.0;
+    if (tid == 0) keep[k] = (unsigned char)kp;
+#pragma unroll
+    for (int t = 0; t < kCholRows; ++t) {
+      const int i = k + 1 + lane + 64 * t;
+      lk[t] = (i < K1 && kp) ? ck[i] / piv : 0.0;
     }
-    if (!kp && tid == 0) ck[k] = 0.0;
-    __syncthreads();
     if (kp) {
       for (int j = k + 1 + wave; j < K1; j += kW) {
-        const double ljk = ck[j];
+        const int r = j - k - 1;  // row j's lane and slot
+        double v = lk[0];
+#pragma unroll
+        for (int t = 1; t < kCholRows; ++t) v = (r >> 6) == t ? lk[t] : v;
+        const double ljk = readlane_f64(v, r & 63);
         if (ljk == 0.0) continue;
         double* cj = col(j);
-        for (int i = j + lane; i < K1; i += 64) cj[i] -= ck[i] * ljk;
+#pragma unroll
+        for (int t = 0; t < kCholRows; ++t) {
+          const int i = k + 1 + lane + 64 * t;
+          if (i >= j && i < K1) cj[i] -= lk[t] * ljk;
+        }
       }
     }
     __syncthreads();
   }
-  for (int c = tid; c < K1; c += kCholT) {
-    double* x = P.Gam + (size_t)c * K1;
-    for (int i = 0; i < K1; ++i) {
-      if (i < c || !keep[c] || !keep[i]) {
-        x[i] = 0.0;
-        continue;
+  if (wave == 0) {  // the last column
+    double* cp = col(K1 - 1);
+    if (lane == 0) cp[K1 - 1] = kp ? piv : 0.0;
+  }
+  __syncthreads();
+  // L^-1 column c: x_i = (delta_ic - sum_{m=c}^{i-1} L[i, m] x_m) / L[i, i]
+  // (0 above c, in dropped rows and for a dropped c), rows i = lane + 64 t
+  for (int c = wave; c < K1; c += kW) {
+    double x[kCholRows];
+#pragma unroll
+    for (int t = 0; t < kCholRows; ++t) x[t] = (lane + 64 * t == c) ? 1.0 : 0.0;
+    const bool kc = keep[c];
+    if (kc) {
+      for (int m = c; m < K1; ++m) {
+        const int tm = m >> 6, lm = m & 63;
+        double a = x[0];
+#pragma unroll
+        for (int t = 1; t < kCholRows; ++t) a = tm == t ? x[t] : a;
+        const double* cm = col(m);
+        const double xm = readlane_f64(keep[m] ? a / cm[m] : 0.0, lm);
+#pragma unroll
+        for (int t = 0; t < kCholRows; ++t) {
+          const int i = lane + 64 * t;
+          if (i == m) x[t] = xm;
+          else if (i > m && i < K1) x[t] -= cm[i] * xm;
+        }
       }
-      double acc = (i == c) ? 1.0 : 0.0;
-      for (int m = c; m < i; ++m) acc -= col(m)[i] * x[m];
-      x[i] = acc / col(i)[i];
+    }
+    double* g = P.Gam + (size_t)c * K1;
+#pragma unroll
+    for (int t = 0; t < kCholRows; ++t) {
+      const int i = lane + 64 * t;
+      if (i < K1) g[i] = (kc && i >= c) ? x[t] : 0.0;
     }
   }
 }
