@@ -227,29 +227,39 @@ __global__ void __launch_bounds__(kT) basis_kernel(int n, int Fc, int f0, const 
     }
     __syncthreads();
     const double b1 = sv[0], b2 = sv[1];
-    for (int k = 2 + tid; k < n; k += kT) {
+    // a wave per column pair, lanes over agents: w = H2 e_k, then
+    // w -= b1 v1 (v1^H w) with the dot product as a wave sum
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int k = 2 + wv; k < n; k += kT / 64) {
       double* u = Q + (size_t)(2 * (k - 2)) * np;       // emb(w)
       double* ui = u + np;                              // emb(i w)
       // H2 e_k = e_k - b2 v2 conj(v2_k)
       const double cr = v2[2 * k], ci = -v2[2 * k + 1];
-      for (int i = 0; i < n; ++i) {
+      auto h2 = [&](int i, double& wr, double& wi) {
         const double vr = v2[2 * i], vi = v2[2 * i + 1];
-        u[2 * i] = (i == k ? 1.0 : 0.0) - b2 * (vr * cr - vi * ci);
-        u[2 * i + 1] = -b2 * (vr * ci + vi * cr);
-      }
-      // H1: w -= b1 v1 (v1^H w)
+        wr = (i == k ? 1.0 : 0.0) - b2 * (vr * cr - vi * ci);
+        wi = -b2 * (vr * ci + vi * cr);
+      };
       double dr = 0.0, di = 0.0;
-      for (int i = 0; i < n; ++i) {
-        const double vr = v1[2 * i], vi = v1[2 * i + 1], wr = u[2 * i], wi = u[2 * i + 1];
+      for (int i = lane; i < n; i += 64) {
+        double wr, wi;
+        h2(i, wr, wi);
+        const double vr = v1[2 * i], vi = v1[2 * i + 1];
         dr += vr * wr + vi * wi;
         di += vr * wi - vi * wr;
       }
-      for (int i = 0; i < n; ++i) {
+      for (int o = 32; o > 0; o >>= 1) {
+        dr += __shfl_xor(dr, o, 64);
+        di += __shfl_xor(di, o, 64);
+      }
+      for (int i = lane; i < n; i += 64) {
+        double wr, wi;
+        h2(i, wr, wi);
         const double vr = v1[2 * i], vi = v1[2 * i + 1];
-        const double wr = u[2 * i] - b1 * (vr * dr - vi * di);
-        const double wi = u[2 * i + 1] - b1 * (vr * di + vi * dr);
-        u[2 * i] = wr; u[2 * i + 1] = wi;
-        ui[2 * i] = -wi; ui[2 * i + 1] = wr;
+        const double xr = wr - b1 * (vr * dr - vi * di);
+        const double xi = wi - b1 * (vr * di + vi * dr);
+        u[2 * i] = xr; u[2 * i + 1] = xi;
+        ui[2 * i] = -xi; ui[2 * i + 1] = xr;
       }
     }
   } else {
@@ -316,19 +326,28 @@ __global__ void __launch_bounds__(kT) basis_kernel(int n, int Fc, int f0, const 
     }
   }
   __syncthreads();
-  // U(:, p:np) = H_0 ... H_{nct-1} e_jj, one column per thread; U(q:, q) is
-  // A(q:, q) after step q (later steps never touch column q).
-  for (int jj = p + tid; jj < np; jj += kT) {
-    double* u = Q + (size_t)(jj - p) * np;
-    for (int i = 0; i < np; ++i) u[i] = (i == jj) ? 1.0 : 0.0;
-    for (int q = nct - 1; q >= 0; --q) {
-      if (sv[q] == 0.0) continue;
-      const double* h = A + (size_t)q * np;
-      double d = 0.0;
-      for (int i = q; i < np; ++i) d += h[i] * u[i];
-      const double t = -(d / h[q]);
-      if (t != 0.0)
-        for (int i = q; i < np; ++i) u[i] += t * h[i];
+  // U(:, p:np) = H_0 ... H_{nct-1} e_jj; U(q:, q) is A(q:, q) after step q
+  // (later steps never touch column q). A wave per column, each element on
+  // one lane throughout (i = lane + 64 m), the reflector dot products as wave
+  // sums (the factorisation above, whose rounding decides the reflectors'
+  // signs, keeps the codegen's serial order).
+  {
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int jj = p + wv; jj < np; jj += kT / 64) {
+      double* u = Q + (size_t)(jj - p) * np;
+      for (int i = lane; i < np; i += 64) u[i] = (i == jj) ? 1.0 : 0.0;
+      for (int q = nct - 1; q >= 0; --q) {
+        if (sv[q] == 0.0) continue;
+        const double* h = A + (size_t)q * np;
+        double d = 0.0;
+        for (int i = lane; i < np; i += 64)
+          if (i >= q) d += h[i] * u[i];
+        for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+        const double t = -(d / h[q]);
+        if (t != 0.0)
+          for (int i = lane; i < np; i += 64)
+            if (i >= q) u[i] += t * h[i];
+      }
     }
   }
   }

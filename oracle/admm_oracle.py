@@ -175,7 +175,8 @@ def complex_complement(p_xy):
     ~1e-1 on that test's formation. Any complex-structured orthonormal basis
     gives the same design up to rounding (the SDP and ADMM iterates are
     equivariant under complex-unitary changes of basis). Restates
-    admm.hip basis_kernel's basis == 1 branch, same operation order."""
+    admm.hip basis_kernel's basis == 1 branch (the same operations; the
+    kernel sums v1^H w as a wave tree, numpy's vdot pairwise)."""
     p_xy = np.asarray(p_xy, dtype=np.float64)
     n = p_xy.shape[0]
     z = p_xy[:, 0] + 1j * p_xy[:, 1]
