@@ -56,6 +56,14 @@ struct GemmJob {
   const double* nserr = nullptr;
   int nsn = 0;
   double nscap = 0.0, nstol = 0.0;
+  // gate (default kernel only): the job runs only while glo <= *gerr < ghi
+  const double* gerr = nullptr;
+  double glo = 0.0, ghi = 0.0;
+  // alternative operand (default kernel only, with nserr): while
+  // qlo <= *nserr < qhi the product reads B = qB (untransformed) and takes
+  // alpha = qalpha, beta = qbeta, unscaled (the quintic final update)
+  const double* qB = nullptr;
+  double qlo = 0.0, qhi = 0.0, qalpha = 0.0, qbeta = 0.0;
 };
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -347,8 +355,21 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
     bi = t % tm;
     bj = t / tm;
   }
-  const GemmJob J = jobs[job];
+  GemmJob J = jobs[job];
   if (J.skip && *J.skip) return;
+  if (J.gerr) {
+    const double ge = *J.gerr;
+    if (!(ge >= J.glo && ge < J.ghi)) return;
+  }
+  bool quint = false;
+  if (J.qB) {
+    const double qe = *J.nserr;
+    if (qe >= J.qlo && qe < J.qhi) {
+      quint = true;
+      J.B = J.qB;
+      J.tmask &= ~2;
+    }
+  }
   const int m0 = bi * TILE, n0 = bj * TILE;
   if (m0 >= J.m || n0 >= J.n) return;
   if (flops && threadIdx.x == 0)
@@ -450,7 +471,10 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
   for (int r = 0; r < 4; ++r) red[(wave * 4 + r) * 64 + lane] = acc44[r];
   __syncthreads();
   double alpha = J.alpha, beta = J.beta;
-  if (J.nsp && !(*J.nserr < J.nstol)) {
+  if (quint) {
+    alpha = J.qalpha;
+    beta = J.qbeta;
+  } else if (J.nsp && !(*J.nserr < J.nstol)) {
     double tr = 0.0;
     for (int b = 0; b < J.nsn; ++b) tr += J.nsp[b];
     const double a = sqrt((double)J.m / tr);

@@ -191,13 +191,14 @@ def test_psd_projection_near_eps(N):
 def test_admm_c5_full_batch():
     """Config C5 at its size: F = 1024 generator formations (n = 100,
     L = 40, noncomplete; the bench's formations, seeds 0..1023) in one
-    acl_admm_solve_batch call, which runs them as two 512-formation chunks
-    (csrc/admm.hip) with the workspace reused between them. Every formation:
-    finite, symmetric, the trace identity of the reference's design (trace
-    of the gain matrix = -(2 (n - 2) + n - 2) for a 3-D formation), both
-    designs converged (positive iteration counts). Formations from both
-    chunks (0, 511, 512, 1023 and four random ones) against the CPU
-    restatement: gains within 1e-5 relative, equal iteration counts."""
+    acl_admm_solve_batch call, which runs them as one pass of
+    ACL_ADMM_CHUNK = 1024 formations (csrc/admm.hip; smaller chunk builds
+    reuse the workspace between passes). Every formation: finite,
+    symmetric, the trace identity of the reference's design (trace of the
+    gain matrix = -(2 (n - 2) + n - 2) for a 3-D formation), both designs
+    converged (positive iteration counts). Formations across the batch (0,
+    511, 512, 1023 and four random ones) against the CPU restatement: gains
+    within 1e-5 relative, equal iteration counts."""
     import torch
     from aclswarm_amd import engine, workload
     dev = torch.device("cuda:0")
@@ -223,3 +224,24 @@ def test_admm_c5_full_batch():
         Ao, ito = O.design_3d(p[f], adj[f])
         assert AC.rel_err(A[f], Ao) < REL_TOL, (f, AC.rel_err(A[f], Ao))
         assert tuple(int(x) for x in its[f]) == tuple(ito), (f, its[f], ito)
+
+
+@pytest.mark.parametrize("basis", [O.BASIS_LINPACK, O.BASIS_COMPLEX])
+def test_admm_deterministic(basis):
+    """Two calls on the same 64 generator formations (n = 20, noncomplete)
+    give bit-identical gains and iteration counts: every sum the outputs
+    depend on runs in a fixed order (the wave sums of the basis, the
+    per-diagonal-tile trace partials that scale the Newton-Schulz updates,
+    summed in tile order); the atomically accumulated sums (|Z^2 - I|_F^2,
+    sum |dX|, tr X22) only feed stop decisions."""
+    import torch
+    from aclswarm_amd import engine, workload
+    dev = torch.device("cuda:0")
+    pts, adjb = workload.reference_formations(64, 20, 40.0, False, 4096, dev)
+    adj = adjb.to(torch.float64)
+    A1, i1 = engine.admm_design(pts, adj, basis=basis)
+    A2, i2 = engine.admm_design(pts, adj, basis=basis)
+    torch.cuda.synchronize()
+    assert torch.equal(i1, i2)
+    assert torch.equal(A1.view(torch.int64), A2.view(torch.int64))
+    assert torch.isfinite(A1).all()
