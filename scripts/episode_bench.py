@@ -80,9 +80,22 @@ def main():
                 g.replay()
         torch.cuda.synchronize()
         dg = (time.perf_counter() - t0) / args.reps
+        # eager launches over the same stretch of the episode as the timed
+        # replays (chunks 3 .. 2 + reps): the swarms are further along there
+        # (closer, more collision avoidance) than in the first chunk above
+        ee = engine.Episode(T, w["fidx"], w["q"], w["vel"], w["P_in"])
+        ee.run(2 * args.steps)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            ee.run(args.steps)
+        torch.cuda.synchronize()
+        de = (time.perf_counter() - t0) / args.reps
         graph = {"value": args.B * args.steps / dg, "unit": "swarm-steps/s",
                  "ms_per_step": dg / args.steps * 1e3, "replays": args.reps,
-                 "what": f"{args.steps} steps captured once as a HIP graph, replayed"}
+                 "eager_same_stretch_ms_per_step": de / args.steps * 1e3,
+                 "what": f"{args.steps} steps captured once as a HIP graph, replayed; "
+                         "eager_same_stretch: eager launches over the same chunks of the episode"}
     st = e.status()
     ep = e.ep
     line = {
