@@ -705,16 +705,35 @@ __global__ void __launch_bounds__(kT) rc_kernel(const Part* parts, int mode, dou
     rr[0] = (mode == 0) ? (double)s : T22;
     if (mode == 1) P.sc->trM11 = T11;
   }
+  // the row dot products and the Ginv product as kAcc interleaved partial
+  // sums (independent load chains; added in a fixed order: deterministic)
+  constexpr int kAcc = 8;
   for (int k = tid; k < K; k += kT) {
     double a = 0.0;
-    if (mode != 0)
-      for (int j = 0; j < s; ++j) a += P.Yk[k + (size_t)j * K] * P.Qb[k + (size_t)j * K];
+    if (mode != 0) {
+      double pa[kAcc] = {};
+      int j = 0;
+      for (; j + kAcc <= s; j += kAcc)
+#pragma unroll
+        for (int u = 0; u < kAcc; ++u)
+          pa[u] += P.Yk[k + (size_t)(j + u) * K] * P.Qb[k + (size_t)(j + u) * K];
+      for (; j < s; ++j) pa[0] += P.Yk[k + (size_t)j * K] * P.Qb[k + (size_t)j * K];
+#pragma unroll
+      for (int u = 0; u < kAcc; ++u) a += pa[u];
+    }
     rr[k + 1] = a;
   }
   __syncthreads();
   for (int i = tid; i < K1; i += kT) {
+    double pa[kAcc] = {};
+    int m = 0;
+    for (; m + kAcc <= K1; m += kAcc)
+#pragma unroll
+      for (int u = 0; u < kAcc; ++u) pa[u] += P.Ginv[i + (size_t)(m + u) * K1] * rr[m + u];
+    for (; m < K1; ++m) pa[0] += P.Ginv[i + (size_t)m * K1] * rr[m];
     double a = 0.0;
-    for (int m = 0; m < K1; ++m) a += P.Ginv[i + (size_t)m * K1] * rr[m];
+#pragma unroll
+    for (int u = 0; u < kAcc; ++u) a += pa[u];
     P.c[i] = a;
     cc[i] = a;
   }
