@@ -188,6 +188,32 @@ def test_psd_projection_near_eps(N):
         assert err <= (1e-9 if k == 1 else 1e-12), (k, err)
 
 
+@pytest.mark.parametrize("N", [40, 392])
+def test_psd_projection_tight_bound(N):
+    """Spectra where the Newton-Schulz start's eigenvalue bound is exact: a
+    diagonal W has spectral radius = |W - eps I|_inf, so the largest
+    |eigenvalue| of Z0 is the kNsScale bound and the first scaled update sits
+    at its cap (a |x| = 0.98 sqrt 3); with eigenvalues +-1, eps +- 1e-3 and a
+    cluster near 0 every sign still comes out right (the Newton-Schulz path,
+    no fallback), within 1e-9 |W| of the eigendecomposition projection; a
+    rotated copy of the same spectrum agrees too."""
+    rng = np.random.RandomState(77 + N)
+    eps = 1e-5
+    lam = rng.uniform(-1.0, 1.0, N)
+    lam[0], lam[1] = 1.0, -1.0
+    lam[2], lam[3] = eps + 1e-3, eps - 1e-3
+    lam[4:8] = rng.uniform(-0.05, 0.05, 4)
+    D = np.diag(lam)
+    Q, _ = np.linalg.qr(rng.normal(size=(N, N)))
+    R = (Q * lam) @ Q.T
+    Ws = [D, 0.5 * (R + R.T)]
+    S, used = _psd_gpu(Ws, eps, force=False)
+    assert used == [0, 0], used
+    for k, W in enumerate(Ws):
+        err = np.abs(S[k] - _psd_ref(W, eps)).max()
+        assert err <= 1e-9, (k, err)
+
+
 def test_admm_c5_full_batch():
     """Config C5 at its size: F = 1024 generator formations (n = 100,
     L = 40, noncomplete; the bench's formations, seeds 0..1023) in one
