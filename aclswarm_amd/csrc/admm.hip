@@ -1068,34 +1068,83 @@ __global__ void __launch_bounds__(kJT) psd_jacobi_kernel(const Part* parts, doub
   }
 }
 
-// S = sym(Sr), Sr = (W + W sign)/2 from the GEMM; X = (S - W)/mu;
-// sum |X_old - X|, tr X22.
-// Sr comes from the symmetric GEMM path: a tile off the diagonal (tile size
-// `tile`) is stored mirrored, so there Sr_ji == Sr_ij and sym(Sr) = Sr bit for
-// bit; only the diagonal tiles (both triangles computed) need the transposed
-// read.
-__global__ void __launch_bounds__(kT) post_kernel(const Part* parts, double mu, int tile) {
+// S = sym(Sr), Sr = (W + W sign)/2 from the S products (or the Jacobi
+// fallback); X = (S - W)/mu; sum |X_old - X|, tr X22. A tile of the S
+// products off the diagonal (tile size `tile`) is stored mirrored, so there
+// sym(Sr) = Sr bit for bit; a diagonal tile's element is 0.5 (Sr_ij + Sr_ji).
+// By 32 x 32 blocks of the upper triangle: Sr, W and X are symmetric element
+// for element (the S products and the fallback store mirrored, W by
+// construction, X = (S - W) / mu), so a block and its mirror share S, X and
+// X_old: the block is read (Sr's mirror block too, through LDS, where it
+// meets a diagonal tile) and S, X are written to both, the mirror through the
+// LDS tile (coalesced); sum |dX| counts an off-diagonal pair twice.
+constexpr int kPB = 32;
+__global__ void __launch_bounds__(256) post_ut_kernel(const Part* parts, double mu, int tile) {
   const Part& P = parts[blockIdx.y];
   if (!P.sc->active) return;
   const int s = P.s, n2 = 2 * s;
-  __shared__ double red[kT / 64];
-  double dsum = 0.0, tr = 0.0;
+  const int nb = (n2 + kPB - 1) / kPB;
+  int t = blockIdx.x;
+  if (t >= nb * (nb + 1) / 2) return;
+  int bj = 0;
+  while (t > bj) { t -= bj + 1; ++bj; }
+  const int bi = t;
+  const int i0 = bi * kPB, j0 = bj * kPB;
+  __shared__ double ts[kPB][kPB + 1];  // Sr mirror block, then S of the block
+  __shared__ double tx[kPB][kPB + 1];  // X of the block
+  __shared__ double red[4];
+  const int tid = threadIdx.x, li = tid & 31, lg = tid >> 5;
+  const bool dgb = bi == bj;
+  const int ie = min(i0 + kPB, n2) - 1, je = min(j0 + kPB, n2) - 1;
+  const bool meets = i0 / tile <= je / tile && j0 / tile <= ie / tile;
+  if (meets) {  // ts[r][c] = Sr(j0 + r, i0 + c)
+#pragma unroll
+    for (int m = 0; m < kPB / 8; ++m) {
+      const int c = lg + 8 * m, gr = j0 + li, gc = i0 + c;
+      ts[li][c] = (gr < n2 && gc < n2) ? P.Sr[gr + (size_t)gc * n2] : 0.0;
+    }
+  }
+  __syncthreads();
   const double imu = 1.0 / mu;
-  for (int e = blockIdx.x * kT + threadIdx.x; e < n2 * n2; e += gridDim.x * kT) {
-    const int i = e % n2, j = e / n2;
-    const double Sv = (i / tile != j / tile) ? P.Sr[e]
-                                             : 0.5 * (P.Sr[e] + P.Sr[j + (size_t)i * n2]);
-    const double Xn = (Sv - P.W[e]) * imu;
-    dsum += fabs(P.X[e] - Xn);
-    if (i == j && i >= s) tr += Xn;
-    P.S[e] = Sv;
-    P.X[e] = Xn;
+  double dsum = 0.0, tr = 0.0;
+#pragma unroll
+  for (int m = 0; m < kPB / 8; ++m) {
+    const int c = lg + 8 * m, i = i0 + li, j = j0 + c;
+    if (i < n2 && j < n2) {
+      const size_t e = i + (size_t)j * n2;
+      const double a = P.Sr[e];
+      const double Sv = (i / tile != j / tile) ? a : 0.5 * (a + ts[c][li]);
+      const double Xn = (Sv - P.W[e]) * imu;
+      const double d = fabs(P.X[e] - Xn);
+      if (dgb) {
+        dsum += d;
+        if (i == j && i >= s) tr += Xn;
+      } else {
+        dsum += 2.0 * d;
+      }
+      P.S[e] = Sv;
+      P.X[e] = Xn;
+      ts[c][li] = Sv;  // this thread's own slot (read above)
+      tx[c][li] = Xn;
+    }
+  }
+  if (!dgb) {  // workgroup-uniform: the mirror block, rows j coalesced
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < kPB / 8; ++m) {
+      const int c = lg + 8 * m, j = j0 + li, i = i0 + c;
+      if (j < n2 && i < n2) {
+        const size_t et = j + (size_t)i * n2;
+        P.S[et] = ts[li][c];
+        P.X[et] = tx[li][c];
+      }
+    }
   }
   const double D = block_sum(dsum, red);
   const double Tt = block_sum(tr, red);
   if (threadIdx.x == 0) {
     atomicAdd(&P.sc->diff, D);
-    atomicAdd(&P.sc->tr22, Tt);
+    if (Tt != 0.0) atomicAdd(&P.sc->tr22, Tt);
   }
 }
 
@@ -1537,9 +1586,11 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       hipLaunchKernelGGL(w_kernel, dim3(cdiv(n2max, kT / 64), NP), dim3(kT), 0, st, dp, mu, eps);
       ACL_HIP(hipGetLastError(), "iteration kernels");
       ACL_HIP(psd_project(JL, dp, NP, n2max, eps, fuse_err, false, X, st), "PSD projection");
-      hipLaunchKernelGGL(post_kernel, dim3(std::min(grid1((long long)n2max * n2max), 64), NP),
-                         dim3(kT), 0, st, dp, mu,
-                         JobLists::sym(J_S) ? gemm_tile_size() : (1 << 30));
+      {
+        const int nbp = (n2max + kPB - 1) / kPB;
+        hipLaunchKernelGGL(post_ut_kernel, dim3(nbp * (nbp + 1) / 2, NP), dim3(256), 0, st, dp, mu,
+                           JobLists::sym(J_S) ? gemm_tile_size() : (1 << 30));
+      }
       hipLaunchKernelGGL(check_kernel, dim3(1), dim3(1024), 0, st, dp, NP, prm.thresh,
                          prm.threshTr, X.d_cnt + 1);
       ACL_HIP(hipGetLastError(), "iteration kernels");
