@@ -100,7 +100,8 @@ struct Part {
   double *r, *c;
   double *hb, *Pm, *T;
   double *W, *S, *Sr, *X, *N0, *N1, *Y;
-  double* cs;  // [2s] column sums of |W - eps I| (w_kernel), or NULL: norm_kernel reads W
+  double* cs;  // [nb][2s] column-sum partials of |W - eps I| per 32-row block (w_ut_kernel, in
+               // Y), or NULL: norm_kernel reads W
   double *G, *Pre, *Pim;  // setup (alias W, Sr, Y)
   double *A1, *Ap;        // final (alias N0, N1)
   Scal* sc;
@@ -768,40 +769,80 @@ __global__ void __launch_bounds__(kT) init_kernel(const Part* parts) {
   }
 }
 
-// W = sym(S + (I-P)(C - S - mu X) - mu x_b) (admm_oracle.Part.run)
-__global__ void __launch_bounds__(kT) w_kernel(const Part* parts, double mu, double eps) {
+// W = sym(S + (I-P)(C - S - mu X) - mu x_b) (admm_oracle.Part.run), element
+// (i, j) before the sym. raw(j, i) == raw(i, j) bit for bit: S, Pm, hb and
+// combine are symmetric element for element (each is built from symmetric
+// operands by the same operations in the same order, or as 0.5 (a + b) of a
+// transposed pair), so sym(raw) = 0.5 (x + x) = x exactly.
+__device__ __forceinline__ double w_raw(const Part& P, double trs, double c0, double mu, int i,
+                                        int j) {
+  const int s = P.s, n2 = 2 * s;
+  double w = P.S[i + (size_t)j * n2];
+  if (i < s && j < s) {
+    if (i == j) w += trs;
+  } else if (i >= s && j >= s) {
+    const int a = i - s, b = j - s;
+    w += P.Pm[a + (size_t)b * s] - combine_at(P, c0, a, b) - mu * P.hb[a + (size_t)b * s];
+  } else if (i % s == j % s) {
+    w -= mu;
+  }
+  return w;
+}
+
+// W by 32 x 32 blocks of the upper triangle (W symmetric element for element,
+// above): the block's raw values, the mirror block through LDS (coalesced),
+// and the column sums of |W - eps I| for norm_kernel as per-block-row
+// partials cs[b n2 + j] (block row b = rows 32 b .. 32 b + 31; a block off
+// the diagonal also gives its mirror's, from its row sums), which
+// norm_kernel adds in block order (deterministic).
+constexpr int kWB = 32;
+__global__ void __launch_bounds__(256) w_ut_kernel(const Part* parts, double mu, double eps) {
   const Part& P = parts[blockIdx.y];
   if (!P.sc->active) return;
   const int s = P.s, n2 = 2 * s;
+  const int nb = (n2 + kWB - 1) / kWB;
+  int t = blockIdx.x;
+  if (t >= nb * (nb + 1) / 2) return;
+  int bj = 0;
+  while (t > bj) { t -= bj + 1; ++bj; }
+  const int bi = t;
+  const int i0 = bi * kWB, j0 = bj * kWB;
+  const bool dgb = bi == bj;
   const double trs = P.sc->trM11 / s, c0 = P.sc->c0;
-  auto raw = [&](int i, int j) {
-    double w = P.S[i + (size_t)j * n2];
-    if (i < s && j < s) {
-      if (i == j) w += trs;
-    } else if (i >= s && j >= s) {
-      const int a = i - s, b = j - s;
-      w += P.Pm[a + (size_t)b * s] - combine_at(P, c0, a, b) - mu * P.hb[a + (size_t)b * s];
-    } else if (i % s == j % s) {
-      w -= mu;
-    }
-    return w;
-  };
-  // raw(j, i) == raw(i, j) bit for bit: S, Pm, hb and combine are symmetric
-  // element for element (each is built from symmetric operands by the same
-  // operations in the same order, or as 0.5 (a + b) of a transposed pair),
-  // so sym(raw) = 0.5 (x + x) = x exactly -- no transposed (uncoalesced) reads
-  // a wave per column (coalesced), which also leaves the column's sum of
-  // |W - eps I| for norm_kernel (no second pass over W)
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int j = blockIdx.x * (kT / 64) + wv; j < n2; j += gridDim.x * (kT / 64)) {
-    double a = 0.0;
-    for (int i = lane; i < n2; i += 64) {
-      const double w = raw(i, j);
+  __shared__ double tw[kWB][kWB + 1];
+  __shared__ double rs[8][kWB];
+  const int tid = threadIdx.x, li = tid & 31, lg = tid >> 5;
+  double rsum = 0.0;  // this thread's part of row i0 + li (the mirror's column)
+#pragma unroll
+  for (int m = 0; m < kWB / 8; ++m) {
+    const int c = lg + 8 * m, i = i0 + li, j = j0 + c;
+    double av = 0.0;
+    if (i < n2 && j < n2) {
+      const double w = w_raw(P, trs, c0, mu, i, j);
       P.W[i + (size_t)j * n2] = w;
-      a += fabs(w - (i == j ? eps : 0.0));
+      tw[c][li] = w;
+      av = fabs(w - (i == j ? eps : 0.0));
     }
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
-    if (lane == 0) P.cs[j] = a;
+    rsum += av;
+    // column j0 + c over the block's 32 rows: the half-wave's lanes (li)
+    double cv = av;
+    for (int o = 16; o > 0; o >>= 1) cv += __shfl_xor(cv, o, 32);
+    if (li == 0 && j < n2) P.cs[(size_t)bi * n2 + j] = cv;
+  }
+  if (!dgb) {  // workgroup-uniform
+    rs[lg][li] = rsum;
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < kWB / 8; ++m) {
+      const int c = lg + 8 * m, j = j0 + li, i = i0 + c;
+      if (j < n2 && i < n2) P.W[j + (size_t)i * n2] = tw[li][c];
+    }
+    if (lg == 0 && i0 + li < n2) {
+      double a = 0.0;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) a += rs[g][li];
+      P.cs[(size_t)bj * n2 + i0 + li] = a;  // mirror: row block bj, column i0 + li
+    }
   }
 }
 
@@ -819,8 +860,9 @@ __global__ void __launch_bounds__(kT) norm_kernel(const Part* parts, double eps)
   double mx = 0.0;
   for (int j = threadIdx.x; j < n2; j += kT) {
     double a = 0.0;
-    if (P.cs) {  // left by w_kernel
-      a = P.cs[j];
+    if (P.cs) {  // per-block-row partials left by w_ut_kernel, in block order
+      const int nbw = (n2 + kWB - 1) / kWB;
+      for (int b = 0; b < nbw; ++b) a += P.cs[(size_t)b * n2 + j];
     } else {
       const double* col = P.W + (size_t)j * n2;
       for (int i = 0; i < n2; ++i) a += fabs(col[i] - (i == j ? eps : 0.0));
@@ -1499,7 +1541,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       P.hb = base + o[9]; P.Pm = base + o[10]; P.T = base + o[11];
       P.W = base + o[12]; P.S = base + o[13]; P.Sr = base + o[14]; P.X = base + o[15];
       P.N0 = base + o[16]; P.N1 = base + o[17]; P.Y = base + o[18];
-      P.cs = base + o[19];
+      P.cs = P.Y;  // w_ut_kernel's column-sum partials (nb x 2s; Y is free until the sign iteration)
       P.G = P.W; P.Pre = P.Sr; P.Pim = P.Y;
       P.A1 = P.N0; P.Ap = P.N1;
       P.sc = scal + p;
@@ -1583,7 +1625,10 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       ACL_HIP(gemm(J_YK, false, false), "gemm Yk");
       hipLaunchKernelGGL(rc_kernel, dim3(NP), dim3(kT), 0, st, dp, 1, mu);
       ACL_HIP(gemm(J_T, true, false), "gemm T");
-      hipLaunchKernelGGL(w_kernel, dim3(cdiv(n2max, kT / 64), NP), dim3(kT), 0, st, dp, mu, eps);
+      {
+        const int nbw = (n2max + kWB - 1) / kWB;
+        hipLaunchKernelGGL(w_ut_kernel, dim3(nbw * (nbw + 1) / 2, NP), dim3(256), 0, st, dp, mu, eps);
+      }
       ACL_HIP(hipGetLastError(), "iteration kernels");
       ACL_HIP(psd_project(JL, dp, NP, n2max, eps, fuse_err, false, X, st), "PSD projection");
       {
