@@ -56,7 +56,7 @@ METRIC_C5 = "batched ADMM formation-gain designs/sec (N=100, F=1024); % fp64 MFM
 FP64_MATRIX_PEAK_TF = 78.6  # MI355X fp64 matrix, AMD spec (the microarch guide has no fp64 row)
 # the instruction's ceiling measured on the box: v_mfma_f64_16x16x4f64 chains
 # without memory traffic (scripts/mfma_f64_peak.hip, profiles/r4_mfma_f64_peak.txt)
-FP64_MFMA_MEASURED_TF = 41.0
+FP64_MFMA_MEASURED_TF = 48.6
 
 
 def _free_port():

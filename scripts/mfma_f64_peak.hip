@@ -30,6 +30,10 @@ void run(int blocks, int iters) {
   hipFree(d);
 }
 int main() {
-  run<4>(256 * 3, 2000); run<8>(256 * 3, 1000); run<8>(256 * 1, 1000); run<16>(256 * 2, 500); run<8>(256*4, 1000);
+  // short runs (the round-4 first measurement) under-read: the clock settles
+  // over ~10 ms, and 3 waves per SIMD do not keep the pipe full
+  run<8>(256 * 3, 1000); run<8>(256 * 3, 10000); run<8>(256 * 3, 20000);
+  run<4>(256 * 6, 10000); run<8>(256 * 6, 10000); run<4>(256 * 8, 10000);
+  run<2>(256 * 8, 20000); run<8>(256 * 3, 10000);
   return 0;
 }
