@@ -271,3 +271,31 @@ def test_admm_deterministic(basis):
     assert torch.equal(i1, i2)
     assert torch.equal(A1.view(torch.int64), A2.view(torch.int64))
     assert torch.isfinite(A1).all()
+
+
+def test_admm_large_n_global_cholesky():
+    """Eight generator formations at n = 160 (seeds 7..14, L = 60,
+    noncomplete): three of them have more than 197 graph rows in the 2-D
+    design (Gram systems of 253, 309 and 215), past the LDS Cholesky, so the
+    batch factors in global memory (chol_kernel); the sign iteration's parts
+    have 8 diagonal tiles (the scaled and quintic updates' trace partials)
+    and the post and W passes 20 x 20 blocks. Gains within 1e-5 relative of
+    the CPU restatement, equal iteration counts."""
+    import torch
+    from aclswarm_amd import engine, workload
+    dev = torch.device("cuda:0")
+    F, n = 8, 160
+    pts, adjb = workload.reference_formations(F, n, 60.0, False, 7, dev)
+    A, its = engine.admm_design(pts, adjb.to(torch.float64))
+    torch.cuda.synchronize()
+    A = A.cpu().numpy()
+    its = its.cpu().numpy()
+    p = pts.cpu().numpy()
+    adj = adjb.cpu().numpy().astype(np.float64)
+    nonedges = ((adj == 0).sum(axis=(1, 2)) - n) // 2
+    assert (2 * nonedges + 1 > 198).sum() >= 3, nonedges
+    assert np.isfinite(A).all()
+    for f in range(F):
+        Ao, ito = O.design_3d(p[f], adj[f])
+        assert AC.rel_err(A[f], Ao) < REL_TOL, (f, AC.rel_err(A[f], Ao))
+        assert tuple(int(x) for x in its[f]) == tuple(ito), (f, its[f], ito)
