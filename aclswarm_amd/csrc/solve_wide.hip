@@ -42,7 +42,30 @@
 namespace acl_amd {
 
 enum { W_RCH = 3 /* misc[3..4]: a column changed in a round of that parity */,
-       W_BIG = 12 /* a coordinate or alignment entry is not below 1e100 */ };
+       W_BIG = 12 /* a coordinate or alignment entry is not below 1e100 */,
+       W_TCOL = 13 /* the round's next dirty column (ticket) */,
+       W_TSEL = 14 /* the round's next re-select (ticket) */ };
+
+// the k-th set bit (k < popcount) of the NW-word mask m (wave-uniform)
+__device__ __forceinline__ int kth_bit(const unsigned long long* m, int NW, int k) {
+  for (int w = 0; w < NW; ++w) {
+    unsigned long long x = m[w];
+    const int pc = __popcll(x);
+    if (k < pc) {
+      for (int q = 0; q < k; ++q) x &= x - 1;
+      return 64 * w + __ffsll((long long)x) - 1;
+    }
+    k -= pc;
+  }
+  return -1;
+}
+
+// a ticket from the workgroup's counter at misc[slot] (wave-uniform)
+__device__ __forceinline__ int wave_ticket(int* misc, int slot, int lane) {
+  int t = 0;
+  if (lane == 0) t = atomicAdd(&misc[slot], 1);
+  return __builtin_amdgcn_readfirstlane(t);
+}
 
 constexpr int kWBlock = 512;    // solve_wide_kernel: 8 waves per swarm, 2 swarms per CU
 constexpr int kWWaves = kWBlock / 64;
@@ -823,13 +846,16 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   const int max_rounds = 2 * n;
   for (int r = 1; r <= max_rounds; ++r) {
     const int par = r & 1, npar = par ^ 1;
-    int idx = 0;
-    for (int w = 0; w < NW; ++w) {
-      unsigned long long m = dmask[par * NW + w];
-      while (m) {
-        const int j = 64 * w + __ffsll((long long)m) - 1;
-        m &= m - 1;
-        if ((idx++ % kWWaves) != wave) continue;
+    // the round's dirty columns, a ticket at a time: a wave takes the next
+    // one when it finishes its last (column updates differ in cost; the
+    // updates of one round touch disjoint columns, so the order is free)
+    int ncol = 0;
+    for (int w = 0; w < NW; ++w) ncol += __popcll(dmask[par * NW + w]);
+    for (;;) {
+      const int tk = wave_ticket(misc, W_TCOL, lane);
+      if (tk >= ncol) break;
+      {
+        const int j = kth_bit(dmask + par * NW, NW, tk);
         WPROF_T(pc0);
         WPROF_ADD(pf_cnt, 1ull);
         // column j of the tiled table: vehicle u = lane + 64 c at Tj[tlo + 512 c]
@@ -1047,15 +1073,20 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       dmask[par * NW + tid] = 0ull;
       obm[npar * NW + tid] = 0ull;
     }
-    if (tid == 0) misc[W_RCH + npar] = 0;  // round r+1's change flag (round r-1's was read)
+    if (tid == 0) {
+      misc[W_RCH + npar] = 0;  // round r+1's change flag (round r-1's was read)
+      misc[W_TCOL] = 0;        // every wave has left this round's column loop
+    }
     {
-      int idx2 = 0;
-      for (int w = 0; w < NW; ++w) {
-        unsigned long long m = obm[par * NW + w];
-        while (m) {
-          const int v = 64 * w + __ffsll((long long)m) - 1;
-          m &= m - 1;
-          if ((idx2++ % kWWaves) != wave) continue;
+      // outbid vehicles, a ticket at a time (a re-select writes only its own
+      // row's entry: any order)
+      int nsel = 0;
+      for (int w = 0; w < NW; ++w) nsel += __popcll(obm[par * NW + w]);
+      for (;;) {
+        const int tk = wave_ticket(misc, W_TSEL, lane);
+        if (tk >= nsel) break;
+        {
+          const int v = kth_bit(obm + par * NW, NW, tk);
           WPROF_T(pr0);
           WPROF_ADD(pf_cnt, 1ull << 42);
           const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, cuw, unif, false, mp);
@@ -1073,6 +1104,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     __syncthreads();
     WPROF_T(pb3);
     WPROF_ADD(pf_bar, pb3 - pb2);
+    if (tid == 0) misc[W_TSEL] = 0;  // every wave has left this round's re-selects
     bool next = false;
     for (int w = 0; w < NW; ++w) next |= dmask[npar * NW + w] != 0ull;
     if (next || misc[W_RCH + par]) eff = r;
