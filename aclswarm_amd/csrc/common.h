@@ -393,6 +393,28 @@ __device__ __forceinline__ double wrap_to_pi(double a) {  // utils.h:275-280
 
 namespace acl_amd {
 
+// ---- round work by ticket (the auction kernels' column updates and re-selects)
+// the k-th set bit (k < popcount) of the NW-word mask m (wave-uniform)
+__device__ __forceinline__ int kth_bit(const unsigned long long* m, int NW, int k) {
+  for (int w = 0; w < NW; ++w) {
+    unsigned long long x = m[w];
+    const int pc = __popcll(x);
+    if (k < pc) {
+      for (int q = 0; q < k; ++q) x &= x - 1;
+      return 64 * w + __ffsll((long long)x) - 1;
+    }
+    k -= pc;
+  }
+  return -1;
+}
+
+// a ticket from the workgroup's counter at misc[slot] (wave-uniform)
+__device__ __forceinline__ int wave_ticket(int* misc, int slot, int lane) {
+  int t = 0;
+  if (lane == 0) t = atomicAdd(&misc[slot], 1);
+  return __builtin_amdgcn_readfirstlane(t);
+}
+
 // ---- decision margin (include/aclswarm_amd.h, acl_swarm_status_t::margin) --
 // A thread tracks the compared f32 pair (hi, lo), hi >= lo >= 0, with the
 // largest ratio lo / hi: products of two floats are exact in double, so the

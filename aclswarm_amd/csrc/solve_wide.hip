@@ -46,26 +46,6 @@ enum { W_RCH = 3 /* misc[3..4]: a column changed in a round of that parity */,
        W_TCOL = 13 /* the round's next dirty column (ticket) */,
        W_TSEL = 14 /* the round's next re-select (ticket) */ };
 
-// the k-th set bit (k < popcount) of the NW-word mask m (wave-uniform)
-__device__ __forceinline__ int kth_bit(const unsigned long long* m, int NW, int k) {
-  for (int w = 0; w < NW; ++w) {
-    unsigned long long x = m[w];
-    const int pc = __popcll(x);
-    if (k < pc) {
-      for (int q = 0; q < k; ++q) x &= x - 1;
-      return 64 * w + __ffsll((long long)x) - 1;
-    }
-    k -= pc;
-  }
-  return -1;
-}
-
-// a ticket from the workgroup's counter at misc[slot] (wave-uniform)
-__device__ __forceinline__ int wave_ticket(int* misc, int slot, int lane) {
-  int t = 0;
-  if (lane == 0) t = atomicAdd(&misc[slot], 1);
-  return __builtin_amdgcn_readfirstlane(t);
-}
 
 constexpr int kWBlock = 512;    // solve_wide_kernel: 8 waves per swarm, 2 swarms per CU
 constexpr int kWWaves = kWBlock / 64;
