@@ -217,6 +217,9 @@ def lib():
     L.acl_internal_kernel_times.restype = ct.c_int
     L.acl_internal_admm_flop_counter.argtypes = [VP]
     L.acl_internal_admm_flop_counter.restype = None
+    if hasattr(L, "acl_internal_admm_mem_cap"):  # (absent from older experiment builds)
+        L.acl_internal_admm_mem_cap.argtypes = [SZ]
+        L.acl_internal_admm_mem_cap.restype = None
     L.acl_internal_psd_project.argtypes = [ct.c_int, ct.c_int, VP, ct.c_double, VP, ct.c_int,
                                            ct.POINTER(ct.c_int)]
     L.acl_internal_psd_project.restype = ct.c_int

@@ -46,7 +46,7 @@ constexpr int kT = 256;         // threads per workgroup of the per-part kernels
 constexpr int kMaxN = 1024;     // points per formation
 constexpr int kMaxRows = 2047;  // graph rows (K) per part: the Gram system is (K+1)^2
 #ifndef ACL_ADMM_CHUNK
-#define ACL_ADMM_CHUNK 1024  // formations per pass (~16 GB of workspace at N = 100; 512: 4 728 vs 4 846 formations/s at C5)
+#define ACL_ADMM_CHUNK 1024  // formations per pass at most (~16 GB of workspace at N = 100; 512: 4 728 vs 4 846 formations/s at C5)
 #endif
 constexpr int kNsMax = 64;      // Newton-Schulz iterations before a part is declared failed
 constexpr double kNsScale = 1.5;  // Z0 scaling: |W - eps I|_inf / kNsScale (norm_kernel)
@@ -532,6 +532,15 @@ constexpr int kCholT = 512;
 constexpr int kCholRows = 4;  // rows per lane: K1 <= 256
 inline size_t chol_lds_bytes(int K1) {
   return ((size_t)K1 * (K1 + 1) / 2 + (size_t)K1) * sizeof(double) + (size_t)K1 + 16;
+}
+constexpr size_t kCholLdsMax = 160 * 1024;
+// the register columns hold 64 kCholRows rows: every K1 the LDS budget admits
+// must fit them (a larger budget needs more rows per lane, or rows past
+// 64 kCholRows would be skipped silently)
+static_assert(((size_t)64 * kCholRows + 1) * (64 * kCholRows + 2) / 2 * sizeof(double) > kCholLdsMax,
+              "chol_lds_kernel: the LDS budget admits K1 > 64 * kCholRows");
+inline bool chol_lds_fits(int K1) {
+  return K1 <= 64 * kCholRows && chol_lds_bytes(K1) <= kCholLdsMax;
 }
 
 __device__ __forceinline__ double readlane_f64(double v, int l) {
@@ -1250,6 +1259,10 @@ __global__ void __launch_bounds__(kT) assemble_kernel(const Part* parts, int n, 
 // ---------------------------------------------------------------------------
 // host side
 
+// test hook (acl_internal_admm_mem_cap): workspace allocations above this many
+// bytes fail as out of memory (0 = no cap), to exercise the halving retry
+size_t g_mem_cap = 0;
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -1258,6 +1271,7 @@ struct DevBuf {
     if (p) (void)hipFree(p);
     p = nullptr;
     bytes = 0;
+    if (g_mem_cap && b > g_mem_cap) return hipErrorOutOfMemory;
     hipError_t e = hipMalloc(&p, b);
     if (e == hipSuccess) bytes = b;
     return e;
@@ -1453,18 +1467,31 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     if (e_ != hipSuccess) return hipfail(e_, what); \
   } while (0)
 
-  const int chunk = std::min(F, ACL_ADMM_CHUNK);
+  // Formations per pass: at most ACL_ADMM_CHUNK; a pass whose workspace does
+  // not fit the device (the per-part arena grows with the graph rows K and
+  // the complement dimension s) is retried with half as many formations.
+  int chunk = std::min(F, ACL_ADMM_CHUNK);
+  auto oom_retry = [&](hipError_t e, int Fc) {
+    if (e != hipErrorOutOfMemory || Fc <= 1) return false;
+    (void)hipGetLastError();  // clear the failed allocation's error
+    chunk = Fc / 2;
+    return true;
+  };
   const int np_max = 2 * n;
   const size_t qstride = (size_t)np_max * np_max;
   const size_t kcap = (size_t)n * (n - 1);  // xy graph rows at most
   const size_t pstride = 2 * std::min(kcap, (size_t)kMaxRows);
-  for (int f0 = 0; f0 < F; f0 += chunk) {
+  for (int f0 = 0; f0 < F;) {
     const int Fc = std::min(chunk, F - f0);
     const int NP = 2 * Fc;
     // ---- phase 0: basis and graph rows
     const size_t a0 = NP * qstride * sizeof(double) + NP * pstride * sizeof(unsigned short) +
                       NP * sizeof(Info) + 256;
-    ACL_HIP(X.arena0.ensure(a0), "hipMalloc");
+    {
+      const hipError_t e0 = X.arena0.ensure(a0);
+      if (oom_retry(e0, Fc)) continue;
+      ACL_HIP(e0, "hipMalloc");
+    }
     double* Qbuf = (double*)X.arena0.p;
     unsigned short* pairbuf = (unsigned short*)(Qbuf + NP * qstride);
     Info* d_info = (Info*)(((uintptr_t)(pairbuf + NP * pstride) + 15) & ~(uintptr_t)15);
@@ -1524,7 +1551,11 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     const size_t nd_parts = off;
     const size_t scal_off = nd_parts * sizeof(double);
     const size_t a1 = scal_off + NP * sizeof(Scal) + 256;
-    ACL_HIP(X.arena1.ensure(a1), "hipMalloc (ADMM workspace)");
+    {
+      const hipError_t e1 = X.arena1.ensure(a1);
+      if (oom_retry(e1, Fc)) continue;
+      ACL_HIP(e1, "hipMalloc (ADMM workspace)");
+    }
     double* base = (double*)X.arena1.p;
     Scal* scal = (Scal*)((char*)X.arena1.p + scal_off);
     for (int p = 0; p < NP; ++p) {
@@ -1603,7 +1634,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     ACL_HIP(gemm(J_PIM1, false, true), "gemm Pim");
     ACL_HIP(gemm(J_PIM2, false, true), "gemm Pim");
     hipLaunchKernelGGL(gamma_kernel, dim3(grid1((long long)maxK1 * maxK1), NP), dim3(kT), 0, st, dp);
-    if (chol_lds_bytes(maxK1) <= 160 * 1024) {
+    if (chol_lds_fits(maxK1)) {
       const size_t cb = chol_lds_bytes(maxK1);
       if (cb > 64 * 1024)
         ACL_HIP(hipFuncSetAttribute((const void*)chol_lds_kernel,
@@ -1655,11 +1686,17 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
                        f0, gains, iters);
     ACL_HIP(hipGetLastError(), "final kernels");
     // the next chunk reuses the workspace
-    if (f0 + chunk < F) ACL_HIP(hipStreamSynchronize(st), "sync");
+    f0 += Fc;
+    if (f0 < F) ACL_HIP(hipStreamSynchronize(st), "sync");
   }
 #undef ACL_HIP
   return ACL_OK;
 }
+
+// Test hook (not part of the public ABI; tests/test_gpu_admm.py): ADMM
+// workspace allocations above `bytes` fail as out of memory (0 = off), so a
+// batch runs in passes of fewer formations, as it does when the device is full.
+extern "C" void acl_internal_admm_mem_cap(size_t bytes) { acl_amd::admm::g_mem_cap = bytes; }
 
 // Diagnostic (not part of the public ABI): counts the algorithmic flops of
 // every ADMM GEMM tile into *counter (a device pointer; NULL turns it off).

@@ -167,11 +167,16 @@ __device__ __forceinline__ void masked_add4(unsigned long long mask, double& a0,
 
 // diagnostic: s_memtime at phase ends (scripts/phase_profile.py)
 __device__ __forceinline__ void stamp_phase(const SolveParams& P, int b, int tid, int k) {
-  if (P.stamps && tid == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
+  if (P.stamps && tid == 0) P.stamps[(size_t)b * kStampStride + k] = __builtin_amdgcn_s_memtime();
+}
+// diagnostic: the shared 100 MHz clock into slot k (kStampRt0 / kStampRt1)
+__device__ __forceinline__ void stamp_rt(const SolveParams& P, int b, int tid, int k) {
+  if (P.stamps && tid == 0) P.stamps[(size_t)b * kStampStride + k] = __builtin_amdgcn_s_memrealtime();
 }
 
 // diagnostic builds (-DACL_AUCTION_PROF=1): s_memtime cycles of the CBAA
-// column step's sections, summed over a swarm's waves into stamps[b][7..15]
+// column step's sections, summed over a swarm's waves into
+// stamps[b][kStampSec + 0..8]
 // (scripts/phase_profile.py; each mark waits for the wave's LDS operations,
 // so the split is indicative)
 #ifndef ACL_AUCTION_PROF
@@ -197,7 +202,7 @@ struct SecProf {
   }
   __device__ void flush(const SolveParams& P, int b, int lane) {
     if (ACL_AUCTION_PROF && P.stamps && lane == 0) {
-      unsigned long long* s = P.stamps + (size_t)b * 16 + 7;
+      unsigned long long* s = P.stamps + (size_t)b * kStampStride + kStampSec;
       for (int k = 0; k < PS_N; ++k) atomicAdd(s + k, acc[k]);
       atomicAdd(s + PS_N, (unsigned long long)cols | ((unsigned long long)walks << 12) |
                               ((unsigned long long)scans << 24) |
@@ -649,6 +654,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   MarginPair mp;
   margin_init(mp);
   stamp_phase(P, b, tid, 0);
+  stamp_rt(P, b, tid, kStampRt0);
 
   // ---------------- phase 0: load ------------------------------------------
   // Every global read of the phase is issued up front (one HBM round trip,
@@ -1333,8 +1339,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
                                    offsetof(SolveParams, ctl));
     asm volatile("" : "+s"(pc));
     pair_gain_fused<kAW, GM>(pc, b, f, smem, tid, kAB);
-    if (!ACL_AUCTION_PROF) stamp_phase(P, b, tid, 7);  // diagnostic: end of the control phase
+    stamp_phase(P, b, tid, 7);  // diagnostic: end of the control phase
   }
+  stamp_rt(P, b, tid, kStampRt1);
 }
 
 // test hook: acl_price (fast path) and the IEEE expression for m squared

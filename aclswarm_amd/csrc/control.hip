@@ -744,7 +744,7 @@ __device__ __forceinline__ bool ca_resolve_serial(int nslot, double* caA, signed
 #endif
 // diagnostic build (-DACL_CA_PROF=1, scripts/phase_profile.py --crowd): wave
 // cycles of the sector build, the resolution and the rest into
-// P.stamps[b][8..10], close vehicles into [11]
+// P.stamps[b][kStampSec + 8..10], close vehicles into [kStampSec + 11]
 #ifndef ACL_CA_PROF
 #define ACL_CA_PROF 0
 #endif
@@ -878,7 +878,7 @@ __global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
 #if ACL_CA_PROF
     CPROF_T(cw1);
     if (P.stamps && lane == 0) {
-      unsigned long long* ps = P.stamps + (size_t)b * 16;
+      unsigned long long* ps = P.stamps + (size_t)b * kStampStride + kStampSec;
       atomicAdd(ps + 8, cp_build);
       atomicAdd(ps + 9, cp_res);
       atomicAdd(ps + 10, (cw1 - cw0) - cp_build - cp_res);

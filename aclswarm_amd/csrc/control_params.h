@@ -129,6 +129,16 @@ struct CtlParams {
   uint16_t* seed_out = nullptr;
 };
 
+// Diagnostic stamps (acl_internal_set_stamps; scripts/phase_profile.py):
+// [B][kStampStride] u64 per swarm. Slots 0..7: s_memtime (the XCD's shader
+// clock: only differences within one workgroup mean anything) at the end of
+// each phase, slot 7 = the end of the fused control phase; slots 8/9:
+// s_memrealtime (the 100 MHz clock every XCD shares) at the swarm's start and
+// end, for the kernel span and the resident-swarm count; slots 16..31: the
+// section counters of the -DACL_*_PROF builds (auction, wide, collision).
+constexpr int kStampStride = 32;
+constexpr int kStampRt0 = 8, kStampRt1 = 9, kStampSec = 16;
+
 struct SolveParams {
   int n, B, F, b0;
   const double* p;
@@ -152,7 +162,7 @@ struct SolveParams {
   int do_control;
   unsigned char* ws;  // workspace base (WsLayout)
   WsLayout W;
-  unsigned long long* stamps;  // diagnostic: [B][16] s_memtime at phase ends (NULL = off)
+  unsigned long long* stamps;  // diagnostic: [B][kStampStride] (above; NULL = off)
   double* gate_margin;         // acl_solve_args_t::gate_margin (+inf for BAD_INPUT swarms)
   CtlParams ctl;               // the fused control phase's parameters (auction.hip, FUSE)
 };

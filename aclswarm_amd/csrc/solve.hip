@@ -39,7 +39,7 @@ extern "C" acl_status_t acl__set_error(const char* msg);
 extern "C" int32_t acl_max_vehicles(void) { return acl_amd::kMaxNWide; }
 
 // Diagnostic hook (not part of the public ABI): when set, the next solves
-// record s_memtime at the end of each phase into stamps[B][8].
+// record phase stamps into stamps[B][kStampStride] (control_params.h).
 static unsigned long long* g_stamps = nullptr;
 extern "C" void acl_internal_set_stamps(unsigned long long* stamps) { g_stamps = stamps; }
 

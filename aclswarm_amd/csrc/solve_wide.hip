@@ -463,12 +463,14 @@ __device__ __forceinline__ void wide_control(KCtlParams* Pp, int b, int f, unsig
 // diagnostic: s_memtime at phase ends into P.stamps[b][k] (scripts/phase_profile.py)
 template <class SP>
 __device__ __forceinline__ void wstamp(SP& P, int b, int k) {
-  if (P.stamps && threadIdx.x == 0) P.stamps[(size_t)b * 16 + k] = __builtin_amdgcn_s_memtime();
+  if (P.stamps && threadIdx.x == 0)
+    P.stamps[(size_t)b * kStampStride + k] =
+        k >= kStampRt0 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
 }
 
 // diagnostic build (-DACL_WIDE_PROF=1, scripts/phase_profile.py): CBAA
-// section cycles summed over the swarm's waves into P.stamps[b][7..10] and
-// counts into [11] (columns | exact scans << 21 | re-selects << 42), [12]
+// section cycles summed over the swarm's waves into P.stamps[b][kStampSec +
+// 0..3] and counts into [kStampSec + 4] (columns | exact scans << 21 | re-selects << 42), [12]
 // rounds
 #ifndef ACL_WIDE_PROF
 #define ACL_WIDE_PROF 0
@@ -723,6 +725,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   MarginPair mp;
   margin_init(mp);
   wstamp(P, b, 0);
+  wstamp(P, b, kStampRt0);
 
   // ---------------- phase 0: load (align_wide_kernel's results) -------------
   if (wflags & 1u) {
@@ -1095,16 +1098,17 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   }
 #if ACL_WIDE_PROF
   if (P.stamps && lane == 0) {
-    unsigned long long* ps = reinterpret_cast<unsigned long long*>(P.stamps) + (size_t)b * 16;
-    atomicAdd(ps + 7, pf_col);
-    atomicAdd(ps + 8, pf_scan);
-    atomicAdd(ps + 9, pf_sel);
-    atomicAdd(ps + 10, pf_bar);
-    atomicAdd(ps + 11, pf_cnt);
-    if (wave == 0) ps[12] = pf_rounds;
-    atomicAdd(ps + 13, pf_cload);
-    atomicAdd(ps + 14, pf_clvl);
-    atomicAdd(ps + 15, pf_cwb);
+    unsigned long long* ps =
+        reinterpret_cast<unsigned long long*>(P.stamps) + (size_t)b * kStampStride + kStampSec;
+    atomicAdd(ps + 0, pf_col);
+    atomicAdd(ps + 1, pf_scan);
+    atomicAdd(ps + 2, pf_sel);
+    atomicAdd(ps + 3, pf_bar);
+    atomicAdd(ps + 4, pf_cnt);
+    if (wave == 0) ps[5] = pf_rounds;
+    atomicAdd(ps + 6, pf_cload);
+    atomicAdd(ps + 7, pf_clvl);
+    atomicAdd(ps + 8, pf_cwb);
   }
 #endif
 
@@ -1248,6 +1252,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
                      reinterpret_cast<const uint16_t*>(P.ws + P.W.pt) + (size_t)b * n);
     wstamp(P, b, 7);
   }
+  wstamp(P, b, kStampRt1);
 }
 
 hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream, bool fuse) {

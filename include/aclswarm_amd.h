@@ -431,8 +431,15 @@ acl_status_t acl_hungarian_batch(const acl_formations_t* formations,
  *      one sets `flush`; on disagreement each vehicle whose own final table
  *      is valid adopts it and the others keep theirs -- the swarm then flies
  *      per-vehicle tables (est.per_vehicle) until an agreed valid auction
- *      (model limit: the next auction aligns every vehicle with the last
- *      agreed assignment, where the reference's vehicles each use their own);
+ *      (model limits: the next auction aligns every vehicle with the last
+ *      agreed assignment, where the reference's vehicles each use their own;
+ *      and a vehicle whose own table is invalid after a disagreeing auction
+ *      only keeps its old table, where the reference's vehicle also sets
+ *      invalid_assignment_ (auctioneer.cpp:291) and flushes and skips its
+ *      next auto-auction alone (coordination_ros.cpp:339-345) -- a per-vehicle
+ *      skip the lockstep auction does not model, so episodes in which a
+ *      vehicle ends a disagreeing auction on an invalid table have parity
+ *      unpinned from that auction on);
  *   2. DistCntrl::compute with each vehicle's table and vel (controlCb,
  *      coordination_ros.cpp:365-378), Safety::cmdinCb saturation and collisionAvoidance
  *      (safety.cpp:172-197,412-541) -> the velocity goal;

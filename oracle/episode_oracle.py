@@ -179,7 +179,15 @@ def adopt(state, flush, res):
     theirs; the swarm then flies per-vehicle tables until an agreed valid
     auction (seed unchanged: the model seeds every vehicle's next alignment
     with the last agreed assignment, where the reference aligns each vehicle
-    with its own P_)."""
+    with its own P_).
+
+    Model limit: a vehicle whose own table is invalid after a disagreeing
+    auction keeps its old table here; the reference's vehicle also sets
+    invalid_assignment_ (auctioneer.cpp:291) and flushes and skips its next
+    auto-auction on its own (coordination_ros.cpp:339-345), a per-vehicle
+    skip the lockstep auction does not model. Parity is unpinned for the
+    auctions after such an event (the swarm-level skip is modelled only for
+    an agreed invalid result)."""
     if flush:
         return 0, "skipped"
     fl = res["status"]["flags"]

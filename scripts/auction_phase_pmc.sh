@@ -11,7 +11,7 @@ C="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY 
 for k in ${STOPS:-1 2 3 4 5 0}; do
   rm -rf /tmp/pp_$k
   ACLSWARM_AMD_LIB=$PWD/aclswarm_amd/lib/exp/stop$k.so timeout -k 10 -s KILL 120 rocprofv3 --pmc $C -d /tmp/pp_$k -o run --output-format csv -- \
-      python3 scripts/auction_only.py --reps 2 > gpurun_out/$OUT/out_$k.txt 2> gpurun_out/$OUT/err_$k.txt || { echo "pass $k failed"; tail -20 gpurun_out/$OUT/err_$k.txt; exit 1; }
+      python3 scripts/auction_only.py --reps 2 ${AO_ARGS} > gpurun_out/$OUT/out_$k.txt 2> gpurun_out/$OUT/err_$k.txt || { echo "pass $k failed"; tail -20 gpurun_out/$OUT/err_$k.txt; exit 1; }
   f=$(find /tmp/pp_$k -name "*counter_collection.csv" | head -1)
   head -1 "$f" > gpurun_out/$OUT/pass_$k.csv
   grep -E "auction_kernel" "$f" >> gpurun_out/$OUT/pass_$k.csv

@@ -1,7 +1,16 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase cycle shares of the auction kernel (s_memtime stamps
-written by thread 0 of each workgroup at the end of every phase), on the
-bench workload. Uses the library's internal hook acl_internal_set_stamps."""
+"""Diagnostic: per-phase cycle shares of the auction kernel, on the bench
+workload, through the library's internal hook acl_internal_set_stamps.
+
+Stamp layout per swarm (csrc/control_params.h, kStampStride = 32 u64):
+  0..6   s_memtime at the end of each auction phase (the XCD's shader clock:
+         only differences within one workgroup are used)
+  7      s_memtime at the end of the fused control phase (0 if the swarm had
+         per-vehicle rows and left its control to gain_kernel)
+  8, 9   s_memrealtime (the 100 MHz clock every XCD shares) at the swarm's
+         start and end: the kernel span and the mean resident swarms
+  16..   section counters of the -DACL_AUCTION_PROF / ACL_WIDE_PROF /
+         ACL_CA_PROF builds"""
 import argparse
 import ctypes as ct
 import os
@@ -40,7 +49,8 @@ if args.crowd:
     w["q"][:, :, :2] = c + args.crowd * (w["q"][:, :, :2] - c)
 lib = L.lib()
 lib.acl_internal_set_stamps.argtypes = [ct.c_void_p]
-st = torch.zeros((args.B, 16), dtype=torch.int64, device=dev)
+SS, RT0, RT1, SEC = 32, 8, 9, 16  # csrc/control_params.h kStamp*
+st = torch.zeros((args.B, SS), dtype=torch.int64, device=dev)
 ctl = not args.no_control
 engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=ctl)  # warm
 torch.cuda.synchronize()
@@ -54,17 +64,27 @@ tot = d.sum(1)
 print(f"per-swarm cycles: mean {tot.mean():.0f}  median {np.median(tot):.0f}")
 for k, nm in enumerate(NAMES):
     print(f"  {nm:16s} mean {d[:, k].mean():10.0f}  share {d[:, k].sum() / tot.sum() * 100:5.1f}%")
-# fused control phase (stamp 7, non-PROF builds): its cycles, and how the
-# swarms' phases overlap on the chip (busy workgroups over the kernel span)
-g = s[:, 7] - s[:, 6]
-if (s[:, 7] > 0).all():
+# fused control phase (slot 7): its cycles and its share of the life of the
+# swarms that ran it (same-workgroup s_memtime differences only)
+fz = s[:, 7] > 0
+if fz.any():
+    g = s[fz, 7] - s[fz, 6]
+    life = s[fz, 7] - s[fz, 0]
     print(f"  control (fused)  mean {g.mean():10.0f}  share of swarm life "
-          f"{g.sum() / (g.sum() + tot.sum()) * 100:5.1f}%")
-    span = s[:, 7].max() - s[:, 0].min()
-    print(f"  span {span:.0f} cycles; mean resident swarms {(s[:, 7] - s[:, 0]).sum() / span:.1f}")
+          f"{g.sum() / life.sum() * 100:5.1f}%  ({int(fz.sum())} of {args.B} swarms fused)")
+# kernel span and residency from the shared 100 MHz clock (slots 8, 9)
+ok = (s[:, RT0] > 0) & (s[:, RT1] > 0)
+if ok.any():
+    r0, r1 = s[ok, RT0], s[ok, RT1]
+    span = r1.max() - r0.min()
+    print(f"  span {span / 100:.1f} us (100 MHz clock); mean resident swarms "
+          f"{(r1 - r0).sum() / span:.1f}; swarm life mean {(r1 - r0).mean() / 100:.2f} us")
+    e = s[ok, 7] if fz[ok].all() else s[ok, 6]
+    c = s[ok, 0]
+    print(f"  shader clock over the swarm lives: {((e - c) / (r1 - r0)).mean() * 100:.0f} MHz")
 # CBAA column-step sections (a -DACL_AUCTION_PROF=1 build): cycles summed
 # over a swarm's waves, and the counts of evaluated columns, walks and scans
-sec = st.cpu().numpy()[:, 7:16].astype(np.uint64)
+sec = st.cpu().numpy()[:, SEC:SEC + 9].astype(np.uint64)
 if args.n <= 128 and (not args.crowd or args.no_control) and sec[:, :8].any():
     SN = ["level 0", "levels", "margin bound", "runner-up walk", "exact scan", "write-back",
           "selects+barrier", "column barrier"]
@@ -98,7 +118,7 @@ if args.n > 128 and sec[:, :4].any():
         print(f"    column {nm:14s} wave-cycles/swarm {sec[:, 6 + k].astype(np.float64).mean():12.0f}")
 # collision avoidance (a -DACL_CA_PROF=1 build, --crowd): ca_kernel wave-cycles
 if args.crowd and not args.no_control:
-    x = st.cpu().numpy()[:, 8:12].astype(np.float64)
+    x = st.cpu().numpy()[:, SEC + 8:SEC + 12].astype(np.float64)
     cnt = x[:, 3].sum()
     print(f"  ca close vehicles {cnt:.0f} ({cnt / args.B:.1f} per swarm)")
     for k, nm in enumerate(["sector build", "resolve", "other (q, loop)"]):

@@ -273,6 +273,39 @@ def test_admm_deterministic(basis):
     assert torch.isfinite(A1).all()
 
 
+def test_admm_passes_halve_when_workspace_does_not_fit():
+    """A batch whose workspace does not fit the device runs in passes of
+    fewer formations (halved until a pass fits) instead of failing: with the
+    test hook capping workspace allocations, 24 formations at n = 40 run in
+    passes of 3 and give the gains and iteration counts of one pass,
+    bit for bit."""
+    import torch
+    from aclswarm_amd import _lib, engine, workload
+    dev = torch.device("cuda:0")
+    pts, adjb = workload.reference_formations(24, 40, 40.0, False, 11, dev)
+    adj = adjb.to(torch.float64)
+    A1, i1 = engine.admm_design(pts, adj)
+    torch.cuda.synchronize()
+    L = _lib.lib()
+    # the one-pass workspace (arena0 + arena1) of 24 formations is tens of
+    # MB here; 8 MB forces several halvings
+    L.acl_internal_admm_mem_cap(8 << 20)
+    try:
+        A2, i2 = engine.admm_design(pts, adj)
+        torch.cuda.synchronize()
+    finally:
+        L.acl_internal_admm_mem_cap(0)
+    assert torch.equal(i1, i2)
+    assert torch.equal(A1.view(torch.int64), A2.view(torch.int64))
+    # a cap no single formation fits still fails loudly
+    L.acl_internal_admm_mem_cap(1 << 10)
+    try:
+        with pytest.raises(RuntimeError):
+            engine.admm_design(pts[:2], adj[:2])
+    finally:
+        L.acl_internal_admm_mem_cap(0)
+
+
 def test_admm_large_n_global_cholesky():
     """Eight generator formations at n = 160 (seeds 7..14, L = 60,
     noncomplete): three of them have more than 197 graph rows in the 2-D

@@ -45,21 +45,37 @@ def _cases():
     return [a, b_, _chain_case()]
 
 
-def _chain_case():
+def _chain_case(n=10, B=6, seed=21, tail=None):
     """Chain (path-graph) formations, n = 10: lockstep CBAA needs more than
     the reference's 2n rounds to reach consensus along a chain for many
     starts, so auctions end with vehicles on different tables, some of them
-    valid (found with the CPU oracle; the GPU auction is bit-exact with it)."""
-    rng = np.random.RandomState(21)
-    n, B = 10, 6
+    valid (found with the CPU oracle; the GPU auction is bit-exact with it).
+
+    tail: a lollipop instead -- a clique of n - tail vehicles with a chain of
+    `tail` vehicles hanging off it; at n = 100 / 136 a plain chain almost
+    never leaves a valid table, a long enough tail often does. These reach the
+    per-vehicle control paths of the larger workgroups (33 <= n <= 128: the
+    256-thread pair/gain kernels; n > 128: the 1 024-thread directed walk)."""
+    rng = np.random.RandomState(seed)
     pts, adjs, gains, qs = [], [], [], []
+    L = 5.0 if tail is None else n / 4.0
+    tries = 0
     while len(qs) < B:
+        tries += 1
+        assert tries < 400, "no disagreeing case found"
         adj = np.zeros((n, n), np.uint8)
         perm = rng.permutation(n)
-        for x, y in zip(perm[:-1], perm[1:]):
+        if tail is None:
+            chain = perm
+        else:
+            core = perm[:n - tail]
+            adj[np.ix_(core, core)] = 1
+            np.fill_diagonal(adj, 0)
+            chain = perm[n - tail - 1:]
+        for x, y in zip(chain[:-1], chain[1:]):
             adj[x, y] = adj[y, x] = 1
-        p = np.c_[rng.uniform(-5, 5, (n, 2)), rng.uniform(0, 2, n)]
-        q = np.c_[rng.uniform(-5, 5, (n, 2)), np.ones(n)]
+        p = np.c_[rng.uniform(-L, L, (n, 2)), rng.uniform(0, 2, n)]
+        q = np.c_[rng.uniform(-L, L, (n, 2)), np.ones(n)]
         P0 = np.arange(n, dtype=np.uint16)
         r = O.solve(q, np.zeros((n, 3)), p, adj, np.zeros((3 * n, 3 * n)), P0)
         who = r["who"]
@@ -67,10 +83,19 @@ def _chain_case():
         if r["status"]["flags"] & 0x02 or nvalid == 0:
             continue
         pts.append(p); adjs.append(adj); gains.append(H.synth_gains(rng, adj)); qs.append(q)
-    return dict(name="chain10_disagree", pts=pts, adj=adjs, gains=gains, fidx=np.arange(B),
+    name = f"chain{n}_disagree" if tail is None else f"lollipop{n}_{tail}_disagree"
+    return dict(name=name, pts=pts, adj=adjs, gains=gains, fidx=np.arange(B),
                 q=np.stack(qs), vel=np.zeros((B, n, 3)),
                 P=np.stack([np.arange(n, dtype=np.uint16)] * B), steps=90,
                 ep=dict(auction_every=30, bufflen=10), disagree=True)
+
+
+def _case(ci):
+    if ci < 3:
+        return _cases()[ci]
+    return {3: lambda: _chain_case(40, 4, 31),
+            4: lambda: _chain_case(100, 3, 23, tail=40),
+            5: lambda: _chain_case(136, 3, 25, tail=60)}[ci]()
 
 
 def _episode(case, dev):
@@ -88,13 +113,15 @@ def _episode(case, dev):
     return e, ep
 
 
-@pytest.mark.parametrize("ci", [0, 1, 2])
+@pytest.mark.parametrize("ci", [0, 1, 2, 3, 4, 5])
 def test_episode_teacher_forced_parity(cuda, ci):
-    """ci 2: chain formations whose 2n-round auctions end with vehicles on
-    different tables -- each vehicle adopts its own valid table
-    (auctioneer.cpp:250-295) and flies it until an agreed auction."""
+    """ci 2-5: chain (n = 10, 40) and lollipop (n = 100, 136) formations whose
+    2n-round auctions end with vehicles on different tables -- each vehicle
+    adopts its own valid table (auctioneer.cpp:250-295) and flies it until an
+    agreed auction (per-vehicle control on the 64-, 256- and 1 024-thread
+    paths)."""
     import torch
-    case = _cases()[ci]
+    case = _case(ci)
     e, eps = _episode(case, cuda)
     hist = e.run(case["steps"], history=True)
     torch.cuda.synchronize()

@@ -45,8 +45,11 @@ def _case(rng, n, F, disconnected):
     return pts, adjs, gains
 
 
-@pytest.mark.parametrize("n", [2, 7, 20, 33, 64, 65, 100, 128])
+@pytest.mark.parametrize("n", [2, 7, 20, 33, 64, 65, 100, 128, 129, 200])
 def test_fused_solve_vs_oracle_and_control(cuda, n):
+    """n > 128: the wide solve's fused control phase (wide_control, 5-plane
+    records) for the uniform swarms, the directed gain kernel for the
+    disconnected formation's per-vehicle swarms, gate margins on."""
     import torch
     from aclswarm_amd import engine
     rng = np.random.RandomState(4000 + n)
