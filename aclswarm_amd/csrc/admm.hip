@@ -1267,11 +1267,11 @@ struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
   hipError_t ensure(size_t b) {
+    if (g_mem_cap && b > g_mem_cap) return hipErrorOutOfMemory;
     if (b <= bytes) return hipSuccess;
     if (p) (void)hipFree(p);
     p = nullptr;
     bytes = 0;
-    if (g_mem_cap && b > g_mem_cap) return hipErrorOutOfMemory;
     hipError_t e = hipMalloc(&p, b);
     if (e == hipSuccess) bytes = b;
     return e;

@@ -67,7 +67,7 @@ struct ALayout {
   int C, pq, adjF, items;
   int A, p, qf, out;
   int T, TS;
-  int vadj, Pin, Ptin, itm, valid, H, misc, dummy, total;
+  int vadj, Pin, Ptin, itm, valid, H, misc, dummy, W1, total;
 };
 
 __host__ __device__ inline ALayout make_alayout(int n) {
@@ -97,6 +97,7 @@ __host__ __device__ inline ALayout make_alayout(int n) {
   L.H = o;     o = a16(o + 16 * 8);  // dmask[2][2], obm[2][2], seen[2]
   L.misc = o;  o = a16(o + 16 * 4);
   L.dummy = o; o = a16(o + 64);      // write-back target of the lanes past n
+  L.W1 = o;    o = a16(o + n * 8);   // [n] u64 START argmax words (phase 2)
   L.total = o;
   return L;
 }
@@ -224,6 +225,29 @@ struct SecProf {
 #endif
 #ifndef ACL_AUCTION_NO_PUBLISH
 #define ACL_AUCTION_NO_PUBLISH 0
+#endif
+
+// Column maxima (ACL_CBAA_COLMAX, default on): an entry's price never falls
+// (updateTaskAssignment keeps the best of a closed neighbourhood that holds
+// the vehicle itself; a select raises it), so a column's highest key is the
+// highest bid ever placed in it -- kept per column in LDS by one atomic max per
+// bid, it is the column's level 0 without a wave reduction.
+#ifndef ACL_CBAA_COLMAX
+#define ACL_CBAA_COLMAX 1
+#endif
+// Lazy per-round margin work (ACL_CBAA_LAZY, default on): a wave with no
+// dirty column skips the walk bound, and a wave publishes its gap bound only
+// after a round in which it evaluated something.
+#ifndef ACL_CBAA_LAZY
+#define ACL_CBAA_LAZY 1
+#endif
+
+// Waves that take CBAA round work (ACL_CBAA_WAVES, a power of two <= the
+// workgroup's waves): the others only pass the round barriers, so the
+// per-round bookkeeping (work distribution, margin publication) is paid by
+// fewer waves while the CU's other swarms keep its SIMDs busy.
+#ifndef ACL_CBAA_WAVES
+#define ACL_CBAA_WAVES 8
 #endif
 
 // An upper bound of margin_gap(hi, lo) in f32 for the mid-auction
@@ -616,6 +640,8 @@ __global__ void __launch_bounds__(64) align_kernel(const SolveParams P) {
 template <int NC, int kAB, bool FUSE, bool GM>
 __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   constexpr int kAW = kAB / 64;  // waves per swarm
+  constexpr int kCW = kAW < ACL_CBAA_WAVES ? kAW : ACL_CBAA_WAVES;  // CBAA round waves
+  static_assert((kCW & (kCW - 1)) == 0, "ACL_CBAA_WAVES: a power of two");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const ALayout L = make_alayout(n);
@@ -644,6 +670,10 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   unsigned long long* H = reinterpret_cast<unsigned long long*>(smem + L.H);
   int* misc = reinterpret_cast<int*>(smem + L.misc);
   unsigned long long* margw = reinterpret_cast<unsigned long long*>(misc + M_MARG);
+  unsigned long long* W1 = reinterpret_cast<unsigned long long*>(smem + L.W1);
+  // [n] u32 column maxima (ACL_CBAA_COLMAX): overlays vadj, dead once every
+  // thread has its neighbourhood masks in registers (the price-phase barrier)
+  unsigned* cmax = reinterpret_cast<unsigned*>(smem + L.vadj);
 
   // a formation index out of range is a bad input like a bad P_in (nothing
   // of the formation table is read for it)
@@ -692,6 +722,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       misc[tid] = 0;
       H[tid] = 0ull;
     }
+    if (tid < n) W1[tid] = 0ull;
   }
   __syncthreads();
   if (tid == 0) {
@@ -798,12 +829,25 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       P.align_Rt[(size_t)b * n * 6 + k] = out[6 * itm[Pin[v]] + (k - 6 * v)];
     }
 
-  // ---------------- phase 2: prices -----------------------------------------
+  // ---------------- phase 2: prices and the START bids ---------------------
+  // A thread per (vehicle v, task class j0): v = tid % n, tasks j = j0, j0 +
+  // per, ... ascending. The thread keeps v's alignment and q in registers and
+  // tracks, over its tasks, the START select (start, auctioneer.cpp:105 ->
+  // selectTaskAssignment :517-542 on the all-`none` table: the first task of
+  // the largest price > 0) and the runner-up price, so the START bids need no
+  // pass over the price matrix: the per-vehicle winner is one LDS atomic max
+  // over the `per` threads' (price, task) words (ties to the lowest task),
+  // the runner-up a second one over what each thread saw besides the winner.
+  // (The select's decision margin is its closest eligible loser: the
+  // runner-up -- a tie is a runner-up equal to the winner.)
+  unsigned* W2 = reinterpret_cast<unsigned*>(C + n * n);  // the `none` row, borrowed
+  const int per = kAB / n;
+  const int pv = tid % n, j0 = tid / n;
+  const bool pact = j0 < per;
+  float pbest = 0.0f, psec = 0.0f;
+  int pbj = -1;
   {
     int nonfin = 0;
-    const int per = kAB / n;
-    const int j = tid % n, v0 = tid / n;
-    const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
     // The aligned point is Eigen's 3x3 [R 0; 0 1] times p plus [t; 0]. With
     // every coordinate of p finite, the terms 0 * p are signed zeros: they
     // can change only the sign of a zero component of the aligned point, and
@@ -811,27 +855,39 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     // price bit-identical (a non-finite p keeps the full expression: 0 * inf
     // is NaN).
     const bool pfin = misc[M_PINF] == 0;  // workgroup-uniform
-    for (int v = v0; v0 < per && v < n; v += per) {
-      const int ip = Pin[v];
-      const double* o = out + 6 * itm[ip];
-      const double* qv = qf + 3 * ip;
+    const int ip = Pin[pv];
+    const double* o = out + 6 * itm[ip];
+    const double* qv = qf + 3 * ip;
+    const double o0 = o[0], o1 = o[1], o2 = o[2], o3 = o[3], o4 = o[4], o5 = o[5];
+    const double q0 = qv[0], q1 = qv[1], q2 = qv[2];
+    float* Crow = C + pv * n;
+    for (int j = j0; pact && j < n; j += per) {
+      const double px = p[3 * j], py = p[3 * j + 1], pz = p[3 * j + 2];
       double dx, dy, dz;
       if (pfin) {
-        dx = qv[0] - ((o[0] * px + o[1] * py) + o[4]);
-        dy = qv[1] - ((o[2] * px + o[3] * py) + o[5]);
-        dz = qv[2] - pz;
+        dx = q0 - ((o0 * px + o1 * py) + o4);
+        dy = q1 - ((o2 * px + o3 * py) + o5);
+        dz = q2 - pz;
       } else {
-        const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
-        const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
+        const double ax = ((o0 * px + o1 * py) + 0.0 * pz) + o4;
+        const double ay = ((o2 * px + o3 * py) + 0.0 * pz) + o5;
         const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
-        dx = qv[0] - ax; dy = qv[1] - ay; dz = qv[2] - az;
+        dx = q0 - ax; dy = q1 - ay; dz = q2 - az;
       }
       const float c = acl_price((dx * dx + dy * dy) + dz * dz);  // bit-exact, see common.h
-      C[v * n + j] = c;
+      Crow[j] = c;
       nonfin |= (c != c);
+      // strict > from max = 0 (NaN never wins, never becomes the runner-up)
+      const bool gt = c > pbest;
+      psec = gt ? pbest : (c > psec ? c : psec);
+      pbj = gt ? j : pbj;
+      pbest = gt ? c : pbest;
     }
+    if (pact && pbj >= 0)
+      atomicMax(&W1[pv], ((unsigned long long)__float_as_uint(pbest) << 8) |
+                             (unsigned long long)(255 - pbj));
     if (__any(nonfin) && lane == 0) misc[M_NONFIN] = 1;
-    for (int jj = tid; jj < n; jj += kAB) C[n * n + jj] = 0.0f;  // the `none` row
+    for (int jj = tid; jj < n; jj += kAB) W2[jj] = 0u;  // (the `none` row: zeros again below)
   }
   // per-lane neighbourhood masks of this lane's vehicles (lane + 64 c)
   unsigned long long vm[NC][NC];
@@ -846,22 +902,38 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   stamp_phase(P, b, tid, 3);
   ACL_AUCTION_STOP_AT(3);
 
-  // ---------------- phase 3: CBAA -------------------------------------------
+  // ---------------- START bids ----------------------------------------------
   unsigned long long* dmask = H;      // [2 parities][2 words]
   unsigned long long* obm = H + 4;    // [2][2]
-  // round 0: the START bid, select from the zero table (start, auctioneer.cpp:105)
-  // Each row is reset (auctioneer.cpp:448-465: every entry `none`) by the
-  // wave that then places that vehicle's START bid in it: one wave's LDS
-  // operations complete in order, so no reset store of another wave can land
-  // on a bid (a reset by all threads before the bids, without a barrier
-  // between, could: a latent race that surfaced as lost bids).
-  const unsigned fill = (unsigned)n * 0x01010101u;
-  for (int v = wave; v < n; v += kAW) {
-    if (lane < TS / 4) reinterpret_cast<unsigned*>(T + v * TS)[lane] = fill;
-    const int task = wave_select<NC>(n, TS, v, lane, C, T, true, mp);
-    if (task >= 0 && lane == 0) {
-      T[v * TS + task] = (unsigned char)v;
-      atomicOr(&dmask[2 + (task >> 6)], 1ull << (task & 63));
+  {
+    // every table row `none` (reset, auctioneer.cpp:448-465); each thread's
+    // runner-up candidate: its best unless that is the winner, else its second
+    const unsigned fill = (unsigned)n * 0x01010101u;
+    unsigned* T32 = reinterpret_cast<unsigned*>(T);
+    for (int k = tid; k < n * (TS / 4); k += kAB) T32[k] = fill;
+    if (ACL_CBAA_COLMAX)
+      for (int jj = tid; jj < n; jj += kAB) cmax[jj] = 1u;  // the `none` key
+    if (pact && pbj >= 0) {
+      const int js = 255 - (int)(W1[pv] & 255ull);
+      const float cand = pbj == js ? psec : pbest;
+      if (cand > 0.0f) atomicMax(&W2[pv], __float_as_uint(cand));
+    }
+  }
+  __syncthreads();
+  if (tid < n) {
+    const int v = tid;
+    const unsigned long long w = W1[v];
+    const unsigned sec = W2[v];
+    W2[v] = 0u;  // the `none` row's price 0 again
+    if (w) {
+      const int js = 255 - (int)(w & 255ull);
+      T[v * TS + js] = (unsigned char)v;
+      atomicOr(&dmask[2 + (js >> 6)], 1ull << (js & 63));
+      if (ACL_CBAA_COLMAX) atomicMax(&cmax[js], (unsigned)(w >> 8) + 1u);
+      // the select's decision gaps (wave_select's terms on a fresh row): the
+      // winner against its price 0 (gap 1), every eligible loser against the
+      // winner -- the closest is the runner-up
+      if (sec) margin_track(mp, __uint_as_float((unsigned)(w >> 8)), __uint_as_float(sec));
     }
   }
   // the START selects' gaps, published for round 1's walk bound
@@ -869,6 +941,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   __syncthreads();
   ACL_AUCTION_STOP_AT(4);
 
+  // ---------------- phase 3: CBAA -------------------------------------------
   bool okv[NC];
   unsigned long long okm[NC];
   unsigned okk[NC];  // key mask: all ones for real vehicles, 0 past n
@@ -887,7 +960,11 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   // atomics per column and per re-select: FL_OB << c = vehicle lane + 64 c
   // outbid, FL_DIRTY << w = column 64 w + lane dirty next round, FL_CH = a
   // column changed this round
+  // (wave-uniform 64-bit masks instead, with the outbid and dirty terms on
+  // the scalar unit, spilled ~60 scalar registers to VGPR lanes: 360 more
+  // vector instructions in the loop)
   unsigned fl = 0u;
+  bool evald = false;  // the wave evaluated a column or a select since it last published
   SecProf sp;
   sp.start();
   const int max_rounds = 2 * n;  // cbaa_max_iter_ = n * diameter (:50-51)
@@ -897,6 +974,27 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     // wave's evaluations up to the last round): an evaluation whose gap is
     // bounded below by it cannot lower the margin, so its runner-up walk is
     // skipped (margin_gap is monotone in the pair's ratio)
+    // this wave's dirty columns: every 8th set bit in rank order
+    const bool cw = wave < kCW;  // this wave takes round work (wave-uniform)
+    unsigned long long mine[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) mine[c] = 0ull;
+    if (cw) {
+      int base = 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const unsigned long long D = uni_u64(dmask[2 * par + c]);
+        const int rk = base + (int)__builtin_amdgcn_mbcnt_hi(
+                                  (unsigned)(D >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)D, 0u));
+        mine[c] = __ballot(((D >> lane) & 1ull) && (rk & (kCW - 1)) == wave);
+        base += __popcll(D);
+      }
+    }
+    unsigned long long anymine = 0ull;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) anymine |= mine[c];
+    if (anymine) evald = true;
+    if (!ACL_CBAA_LAZY || anymine) {
     const double Gpub = __longlong_as_double((long long)*margw);
     // the walk bound: a column's exact runner-up walk can lower the margin
     // only if some resolving level's successor is within Gw of it, Gw = min
@@ -904,19 +1002,6 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     // for the conservative f32 tests (at least Gw (1 + 2^-20)), refreshed after walks
     double Gw = fmin(Gpub, margin_gap_pair(uhi, ulo));
     float Gwf = (float)(Gw * (1.0 + 0x1p-20));
-    // this wave's dirty columns: every 8th set bit in rank order
-    unsigned long long mine[NC];
-    {
-      int base = 0;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const unsigned long long D = uni_u64(dmask[2 * par + c]);
-        const int rk = base + (int)__builtin_amdgcn_mbcnt_hi(
-                                  (unsigned)(D >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)D, 0u));
-        mine[c] = __ballot(((D >> lane) & 1ull) && (rk & (kAW - 1)) == wave);
-        base += __popcll(D);
-      }
-    }
     {
       // one loop over both words (the column body is emitted once)
       unsigned long long mm = mine[0], m1 = NC > 1 ? mine[NC - 1] : 0ull;
@@ -941,7 +1026,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           nw[c] = wu[c];
         }
         // level 0: the column's highest price key, its holders and `who`
-        unsigned M0 = level_key<NC>(key, 0xFFFFFFFFu);
+        const unsigned M0 = ACL_CBAA_COLMAX
+                                ? (unsigned)__builtin_amdgcn_readfirstlane((int)cmax[j])
+                                : level_key<NC>(key, 0xFFFFFFFFu);
         unsigned long long h[NC];
         int cum = 0;
 #pragma unroll
@@ -1126,16 +1213,20 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         sp.mark(PS_WB);
       }
     }
+    }  // (a wave with no dirty column)
 #pragma unroll
     for (int c = 0; c < NC; ++c) {  // publish the outbid vehicles
+      if (!cw) break;
       const unsigned long long ob = __ballot((fl >> c) & 1u);
       if (ob && lane == 0) atomicOr(&obm[2 * par + c], ob);
     }
-    if (!ACL_AUCTION_NO_PUBLISH) {
+    if (!ACL_AUCTION_NO_PUBLISH && (!ACL_CBAA_LAZY || evald)) {
       // publish this wave's smallest gap so far (its lanes' select and scan
       // evaluations, its walks' pair) for the next round's pruning: an upper
-      // bound is enough there (gap_ub)
+      // bound is enough there (gap_ub); only after a round in which the wave
+      // evaluated something (its pairs are unchanged otherwise)
       publish_gap_ub(margw, mp, uhi, ulo);
+      evald = false;
     }
     sp.mark(PS_WB);
     __syncthreads();
@@ -1152,27 +1243,33 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       int base = 0;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
+        if (!cw) break;
         const unsigned long long O = uni_u64(obm[2 * par + c]);
         const int rk = base + (int)__builtin_amdgcn_mbcnt_hi(
                                   (unsigned)(O >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)O, 0u));
-        unsigned long long mv = __ballot(((O >> lane) & 1ull) && (rk & (kAW - 1)) == wave);
+        unsigned long long mv = __ballot(((O >> lane) & 1ull) && (rk & (kCW - 1)) == wave);
         base += __popcll(O);
         while (mv) {
           const int v = 64 * c + __ffsll((long long)mv) - 1;
           mv &= mv - 1;
           const int task = wave_select<NC>(n, TS, v, lane, C, T, false, mp, &sp.selx);
           if (ACL_AUCTION_PROF) sp.sels++;
+          evald = true;
           smem[(task >= 0 && lane == 0) ? L.T + v * TS + task : L.dummy + lane] = (unsigned char)v;
+          if (ACL_CBAA_COLMAX && task >= 0 && lane == 0)
+            atomicMax(&cmax[task], __float_as_uint(C[v * n + task]) + 1u);
           fl |= (vflag(task >= 0) & vflag(lane == (task & 63))) << (FL_DIRTY + (task >> 6));
         }
       }
     }
+    if (cw) {
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {  // publish next round's dirty columns
-      const unsigned long long dm = __ballot((fl >> (FL_DIRTY + c)) & 1u);
-      if (dm && lane == 0) atomicOr(&dmask[2 * npar + c], dm);
+      for (int c = 0; c < NC; ++c) {  // publish next round's dirty columns
+        const unsigned long long dm = __ballot((fl >> (FL_DIRTY + c)) & 1u);
+        if (dm && lane == 0) atomicOr(&dmask[2 * npar + c], dm);
+      }
+      if (__any((fl >> FL_CH) & 1u) && lane == 0) misc[A_RCH + par] = 1;
     }
-    if (__any((fl >> FL_CH) & 1u) && lane == 0) misc[A_RCH + par] = 1;
     fl = 0u;
     __syncthreads();
     sp.mark(PS_SEL);

@@ -374,10 +374,35 @@ __device__ __forceinline__ double acl_atan_b(double x, const double* tab) {
 // of them) -- and every x outside [1e-200, 1e60] (zero, subnormal results,
 // float underflow, inf, NaN) -- take the IEEE expression. `tests/
 // test_gpu_prices.py` sweeps it against the IEEE expression on the GPU.
+//
+// y = 1 / (s + 1e-8) = r / (1 + d) with r = 1/sqrt(x), d = 1e-8 r: r from the
+// hardware reciprocal square root and two Newton steps (each squares the
+// relative error, then a few ulp of rounding), y = r (1 - d + d^2) -- the
+// truncated d^3 is below 1e-15 relative for x > 1e-6 (distances above 1 mm;
+// smaller x take the IEEE expression): one transcendental and eleven
+// arithmetic instructions instead of a square root and a quotient by Newton
+// steps (two transcendentals, seventeen).
+#ifndef ACL_PRICE_RSQ
+#define ACL_PRICE_RSQ 1
+#endif
 __device__ __forceinline__ float acl_price(double x) {
+#if ACL_PRICE_RSQ
+  double r = __builtin_amdgcn_rsq(x);
+  double t = x * r;
+  double e = __builtin_fma(-t, r, 1.0);
+  r = __builtin_fma(0.5 * r, e, r);
+  t = x * r;
+  e = __builtin_fma(-t, r, 1.0);
+  r = __builtin_fma(0.5 * r, e, r);
+  const double d = 1e-8 * r;
+  const double y = __builtin_fma(r, __builtin_fma(d, d, -d), r);
+  const double lo = 1e-6;
+#else
   const double y = div_nr(1.0, sqrt_nr(x) + 1e-8);
-  const unsigned r = (unsigned)((unsigned long long)__double_as_longlong(y) & ((1ull << 29) - 1ull));
-  const bool fast = x > 1e-200 && x < 1e60 && (r - (1u << 28) + 1024u) > 2048u;
+  const double lo = 1e-200;
+#endif
+  const unsigned r29 = (unsigned)((unsigned long long)__double_as_longlong(y) & ((1ull << 29) - 1ull));
+  const bool fast = x > lo && x < 1e60 && (r29 - (1u << 28) + 1024u) > 2048u;
   float c = (float)y;
   if (!fast) c = (float)(1.0 / (sqrt(x) + 1e-8));
   return c;

@@ -12,6 +12,18 @@
 //                   vehicles), a re-select reads its vehicle's row (8 lines
 //                   per 64 tasks instead of 64 with a column-major table)
 //
+// Sparse columns (round 5). A column whose update leaves at most kWSparseK
+// vehicles holding something other than one base `who` is kept in LDS
+// instead: the base (cuw[j]) and the exceptions (vehicle, who) -- the table
+// T is not written for it and is stale there. A bid on a sparse column is
+// appended to the select phase's bid list (LDS) and applied by the column's
+// next update; a column with more exceptions is written to T in full and
+// read from it (dense) until an update makes it sparse again. At N = 500
+// nearly every column update leaves 0-2 exceptions (a vehicle misses ~1 of
+// 499 neighbours), so the column reads and write-backs that moved most of
+// the table's HBM traffic (one 128-byte line per 8 vehicles, 16 bytes of it
+// used) leave the memory system; START needs no table reset.
+//
 // The price matrix (1 MB per swarm at n = 500) is not stored: a price is
 // recomputed from LDS where it is needed (wprice: vehicle v's alignment
 // applied to formation point j, the same f64 operations as the n <= 128
@@ -44,7 +56,11 @@ namespace acl_amd {
 enum { W_RCH = 3 /* misc[3..4]: a column changed in a round of that parity */,
        W_BIG = 12 /* a coordinate or alignment entry is not below 1e100 */,
        W_TCOL = 13 /* the round's next dirty column (ticket) */,
-       W_TSEL = 14 /* the round's next re-select (ticket) */ };
+       W_TSEL = 14 /* the round's next re-select (ticket) */,
+       W_NBID = 16 /* misc[16..17]: bids in the bid list of that parity */ };
+
+// exceptions a sparse column holds (LDS: 4 bytes each per column)
+constexpr int kWSparseK = 4;
 
 
 constexpr int kWBlock = 512;    // solve_wide_kernel: 8 waves per swarm, 2 swarms per CU
@@ -99,7 +115,7 @@ __host__ __device__ inline WALayout make_walayout(int n) {
 
 // solve_wide_kernel's LDS
 struct WLayout {
-  int p, qv, vadj, Pin, Ptin, ccw, ccp, cuw, valid, masks, seen, misc, total;
+  int p, qv, vadj, Pin, Ptin, ccw, ccp, cuw, valid, masks, seen, misc, ecnt, elist, bids, total;
 };
 
 __host__ __device__ inline WLayout make_wlayout(int n) {
@@ -113,11 +129,14 @@ __host__ __device__ inline WLayout make_wlayout(int n) {
   L.Ptin = o;  o = wal(o + n * 2);
   L.ccw = o;   o = wal(o + n * 2);    // column price cache: a holder of task j
   L.ccp = o;   o = wal(o + n * 4);    // and its price for j
-  L.cuw = o;   o = wal(o + n * 2);    // column j's one `who` while its unif bit is set
+  L.cuw = o;   o = wal(o + n * 2);    // a sparse column's base `who` (unif: every vehicle's)
   L.valid = o; o = wal(o + n);
-  L.masks = o; o = wal(o + 5 * NW * 8);                // dmask[2][NW], obm[2][NW], unif[NW]
+  L.masks = o; o = wal(o + 6 * NW * 8);  // dmask[2][NW], obm[2][NW], unif[NW], spm[NW]
   L.seen = o;  o = wal(o + kWWaves * NW * 8);         // per-wave validity checks
-  L.misc = o;  o = wal(o + 64);
+  L.misc = o;  o = wal(o + 128);
+  L.ecnt = o;  o = wal(o + n);                         // exceptions of a sparse column
+  L.elist = o; o = wal(o + n * kWSparseK * 4);         // [j][K] vehicle << 16 | who
+  L.bids = o;  o = wal(o + 2 * n * 4);                 // [2][n] bid lists: vehicle << 16 | task
   L.total = o;
   return L;
 }
@@ -156,19 +175,43 @@ struct WPrice {
 // (price_j = C[w][j] of the task's holder w in v's table).
 // `fresh`: the row is all `none` (the START bid). Tracks the margin of the
 // decisive comparisons (include/aclswarm_amd.h) in m.
+// Entry (task j, vehicle u) of the table: a sparse column's exception or its
+// base, else T (see the header).
+struct WTable {
+  const uint16_t* T;
+  const uint16_t* cuw;
+  const unsigned char* ecnt;
+  const unsigned* elist;
+  const unsigned long long* spm;
+  int n;
+  __device__ __forceinline__ bool sparse(int j) const { return (spm[j >> 6] >> (j & 63)) & 1ull; }
+  __device__ __forceinline__ unsigned sparse_entry(int j, int u) const {
+    unsigned w = cuw[j];
+    const int ne = ecnt[j];
+    const uint4 e4 = *reinterpret_cast<const uint4*>(elist + j * kWSparseK);
+    const unsigned e[4] = {e4.x, e4.y, e4.z, e4.w};
+    static_assert(kWSparseK == 4, "one 16-byte read per column");
+#pragma unroll
+    for (int k = 0; k < kWSparseK; ++k)
+      if (k < ne && (e[k] >> 16) == (unsigned)u) w = e[k] & 0xFFFFu;
+    return w;
+  }
+  __device__ __forceinline__ unsigned operator()(int j, int u) const {
+    return sparse(j) ? sparse_entry(j, u) : (unsigned)T[tix(n, j, u)];
+  }
+};
+
 __device__ int wide_select(int n, int NW, int v, int lane, const WPrice& price,
                            const uint16_t* T, const uint16_t* ccw, const float* ccp,
-                           const uint16_t* cuw, const unsigned long long* unif, bool fresh,
-                           MarginPair& m) {
+                           const WTable& tab, bool fresh, MarginPair& m) {
   unsigned key[kWMaxW];
   float cvs[kWMaxW], prs[kWMaxW];
   bool other[kWMaxW];
   unsigned lm = 0u;
   int wv[kWMaxW];
   // row v of the tiled table: task j = lane + 64 c at Tv[lo + c * 512 n8];
-  // a column whose unif bit is set holds cuw[j] in every row (a bid that
-  // breaks that clears the bit, and changes only its own row), so only the
-  // other columns' entries are read from the table
+  // a sparse column's entry comes from LDS (its base or v's exception), so
+  // only the dense columns' entries are read from the table
   const int n8 = (n + 7) >> 3;
   const uint16_t* Tv = T + (((v >> 3) << 6) + (v & 7));
   const int lo = (((lane >> 3) * n8) << 6) + ((lane & 7) << 3);
@@ -178,8 +221,8 @@ __device__ int wide_select(int n, int NW, int v, int lane, const WPrice& price,
     if (fresh || c >= NW || j >= n) {
       wv[c] = n;
     } else {
-      const bool uni = (unif[c] >> lane) & 1ull;
-      wv[c] = uni ? cuw[j] : Tv[lo + c * (n8 << 9)];
+      const bool spl = (tab.spm[c] >> lane) & 1ull;
+      wv[c] = spl ? (int)tab.sparse_entry(j, v) : (int)Tv[lo + c * (n8 << 9)];
     }
   }
 #pragma unroll
@@ -710,8 +753,12 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   // update; a bid written into it clears the bit and dirties the column), so
   // at the fixed point all tables agree <=> every bit is set
   unsigned long long* unif = dmask + 4 * NW;
+  unsigned long long* spm = dmask + 5 * NW;  // sparse columns (see the header)
   unsigned long long* seen = reinterpret_cast<unsigned long long*>(smem + L.seen);
   int* misc = reinterpret_cast<int*>(smem + L.misc);
+  unsigned char* ecnt = smem + L.ecnt;
+  unsigned* elist = reinterpret_cast<unsigned*>(smem + L.elist);
+  unsigned* bids = reinterpret_cast<unsigned*>(smem + L.bids);  // [2][n]
 
   unsigned char* wsb = P.ws + P.W.wide + (size_t)b * P.W.wide_stride;
   uint16_t* T = reinterpret_cast<uint16_t*>(wsb);
@@ -765,9 +812,14 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       Ptin[pv] = (uint16_t)v;
     }
     for (int k = tid; k < 4 * NW; k += kWBlock) dmask[k] = 0ull;
-    for (int k = tid; k < NW; k += kWBlock) unif[k] = ~0ull;  // every column all `none`
-    for (int k = tid; k < n; k += kWBlock) ccw[k] = cuw[k] = (uint16_t)n;
-    if (tid < 16) misc[tid] = 0;
+    // every column all `none`: sparse, base `none`, no exceptions (T is not
+    // reset: no column reads it before an update writes it in full)
+    for (int k = tid; k < NW; k += kWBlock) unif[k] = spm[k] = ~0ull;
+    for (int k = tid; k < n; k += kWBlock) {
+      ccw[k] = cuw[k] = (uint16_t)n;
+      ecnt[k] = 0;
+    }
+    if (tid < 32) misc[tid] = 0;
   }
   __syncthreads();
   if (tid == 0) {
@@ -805,19 +857,27 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       if (__any(nonfin) && lane == 0) misc[M_NONFIN] = 1;
     }
   }
-  for (int k = tid; k < tix_size(n); k += kWBlock) T[k] = (uint16_t)n;  // reset: all `none`
   __syncthreads();
   const bool nonfinite = misc[M_NONFIN] != 0;
+  const WTable tab{T, cuw, ecnt, elist, spm, n};
   wstamp(P, b, 3);
 
   // ---------------- phase 3: CBAA ------------------------------------------
-  for (int v = wave; v < n; v += kWWaves) {
-    const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, cuw, unif, true, mp);
-    if (task >= 0 && lane == 0) {
+  // a bid: into T for a dense column, else into the bid list of this
+  // select phase's parity (the column's next update applies it)
+  auto place_bid = [&](int v, int task, int bpar) {
+    if (tab.sparse(task)) {
+      const int k = atomicAdd(&misc[W_NBID + bpar], 1);
+      bids[bpar * n + k] = ((unsigned)v << 16) | (unsigned)task;
+    } else {
       T[tix(n, task, v)] = (uint16_t)v;
-      atomicOr(&dmask[NW + (task >> 6)], 1ull << (task & 63));
-      atomicAnd(&unif[task >> 6], ~(1ull << (task & 63)));
     }
+    atomicOr(&dmask[(bpar ^ 1) * NW + (task >> 6)], 1ull << (task & 63));
+    atomicAnd(&unif[task >> 6], ~(1ull << (task & 63)));
+  };
+  for (int v = wave; v < n; v += kWWaves) {
+    const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, tab, true, mp);
+    if (task >= 0 && lane == 0) place_bid(v, task, 0);  // round 1 (parity 1) reads list 0
   }
   __syncthreads();
   int eff = 0;
@@ -827,8 +887,10 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
 #endif
   unsigned obf = 0u;  // per-lane outbid bits (bit c: vehicle lane + 64 c), one round
   const int max_rounds = 2 * n;
+  int lastpar = 0;  // the parity of the last select phase's bid list
   for (int r = 1; r <= max_rounds; ++r) {
     const int par = r & 1, npar = par ^ 1;
+    lastpar = par;
     // the round's dirty columns, a ticket at a time: a wave takes the next
     // one when it finishes its last (column updates differ in cost; the
     // updates of one round touch disjoint columns, so the order is free)
@@ -851,15 +913,46 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         // neighbourhood holds, 0 = none; also the lanes past n), needm --
         // exact ordered scan (ties, NaN, levels exhausted)
         unsigned s1m = 0u, s2m = 0u, needm = 0u;
+        // the column's entries: a sparse column from its base, exceptions
+        // and the last select phase's bids on it (LDS); a dense one from T
+        const bool spj = tab.sparse(j);  // wave-uniform
+        const unsigned base = spj ? (unsigned)cuw[j] : 0u;
 #pragma unroll
         for (int c = 0; c < kWMaxW; ++c) {
           const int u = lane + 64 * c;
           const bool ok = c < NW && u < n;
-          wu[c] = ok ? Tj[tlo + (c << 9)] : (unsigned)n;
+          wu[c] = ok ? (spj ? base : (unsigned)Tj[tlo + (c << 9)]) : (unsigned)n;
           key[c] = ok ? 1u : 0u;  // + the holder's price bits below (1: none)
           nw[c] = (unsigned)n;
           k1[c] = k2[c] = 0u;
           s2m |= (ok ? 0u : 1u) << c;
+        }
+        if (spj) {
+          // vehicle u's entry is `who` (u wave-uniform): one lane of one chunk
+          auto set_entry = [&](unsigned u, unsigned who) {
+            const int cu = (int)(u >> 6);
+            const bool me = lane == (int)(u & 63u);
+#pragma unroll
+            for (int c = 0; c < kWMaxW; ++c)
+              if (c == cu) wu[c] = me ? who : wu[c];
+          };
+          const int ne = ecnt[j];
+          for (int k = 0; k < ne; ++k) {
+            const unsigned e = elist[j * kWSparseK + k];
+            set_entry(e >> 16, e & 0xFFFFu);
+          }
+          const int nb = misc[W_NBID + npar];
+          const unsigned* bl = bids + npar * n;
+          for (int k0 = 0; k0 < nb; k0 += 64) {
+            const unsigned e = k0 + lane < nb ? bl[k0 + lane] : 0xFFFFFFFFu;
+            unsigned long long m = __ballot((e & 0xFFFFu) == (unsigned)j);
+            while (m) {
+              const int k = __ffsll((long long)m) - 1;
+              m &= m - 1;
+              const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)e, k) >> 16;
+              set_entry(v, v);  // the bid: v holds its own bid
+            }
+          }
         }
         {
           // entries of one holder share its price: one (lane-uniform) price
@@ -966,8 +1059,18 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           if (((donem >> c) & 1u) && k2[c] != 0u)
             margin_track(mp, __uint_as_float(k1[c] - 1u), __uint_as_float(k2[c] - 1u));
         WPROF_T(ps0);
+        bool tvalid = !spj;  // T holds the column's entries (before this update)
         if (__ballot(needm != 0u) != 0ull) {
           WPROF_ADD(pf_cnt, 1ull << 21);
+          if (!tvalid) {  // (rare) the exact scan reads T: write the column in full
+#pragma unroll
+            for (int c = 0; c < kWMaxW; ++c)
+              if (c < NW && lane + 64 * c < n) Tj[tlo + (c << 9)] = (uint16_t)wu[c];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            tvalid = true;
+          }
           // exact ordered scan (ascending vehid, strict >): ties, NaN prices,
           // vehicles no tracked level decides; the runner-up is the best
           // price of another `who` (entries of one `who` share its price)
@@ -1006,15 +1109,51 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         __builtin_amdgcn_wave_barrier();
         bool ch = false, mx = false;
         const unsigned nw0 = (unsigned)__builtin_amdgcn_readfirstlane((int)nw[0]);  // vehicle 0
+        // the new state: sparse around the top level's `who` (the entry most
+        // vehicles take) when at most kWSparseK vehicles hold another, else
+        // dense in T (all entries written if T was stale, else the changed ones)
+        bool same = true;
+#pragma unroll
+        for (int c = 0; c < kWMaxW; ++c) same &= !(c < NW && lane + 64 * c < n) || nw[c] == nw0;
+        const unsigned nbase = (__ballot(!same) == 0ull || wk0 < 0 || wk0 >= n) ? nw0 : (unsigned)wk0;
+        unsigned long long em[kWMaxW];
+        int nexc = 0;
+#pragma unroll
+        for (int c = 0; c < kWMaxW; ++c) {
+          const bool ok = c < NW && lane + 64 * c < n;
+          em[c] = __ballot(ok && nw[c] != nbase);
+          nexc += __popcll(em[c]);
+        }
+        const bool nsparse = nexc <= kWSparseK;
+        int erank = 0;
 #pragma unroll
         for (int c = 0; c < kWMaxW; ++c) {
           const int u = lane + 64 * c;
           const bool ok = c < NW && u < n;
-          if (ok && nw[c] != wu[c]) Tj[tlo + (c << 9)] = (uint16_t)nw[c];  // changed entries only
+          if (nsparse) {
+            if ((em[c] >> lane) & 1ull) {
+              const int k = erank + (int)__builtin_amdgcn_mbcnt_hi(
+                                        (unsigned)(em[c] >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((unsigned)em[c], 0u));
+              elist[j * kWSparseK + k] = ((unsigned)u << 16) | nw[c];
+            }
+            erank += __popcll(em[c]);
+          } else if (ok && (!tvalid || nw[c] != wu[c])) {
+            Tj[tlo + (c << 9)] = (uint16_t)nw[c];
+          }
           // outbid (:502): a per-lane bit, published once per wave and round
           obf |= (vflag(ok) & vflag(wu[c] == (unsigned)u) & vflag(nw[c] != (unsigned)u)) << c;
           ch |= nw[c] != wu[c];
           mx |= ok && nw[c] != nw0;
+        }
+        if (lane == 0) {
+          if (nsparse) {
+            cuw[j] = (uint16_t)nbase;
+            ecnt[j] = (unsigned char)nexc;
+            if (!spj) atomicOr(&spm[j >> 6], 1ull << (j & 63));
+          } else if (spj) {
+            atomicAnd(&spm[j >> 6], ~(1ull << (j & 63)));
+          }
         }
         // a column left holding one `who` everywhere is a fixed point with no
         // runner-up: not dirty next round unless a re-select writes it (as in
@@ -1028,13 +1167,9 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           misc[W_RCH + par] = 1;
           if (anymx || nonfinite) atomicOr(&dmask[npar * NW + (j >> 6)], 1ull << (j & 63));
         }
-        if (lane == 0) {
-          if (anymx) {
-            atomicAnd(&unif[j >> 6], ~(1ull << (j & 63)));
-          } else {
-            cuw[j] = (uint16_t)nw0;
-            atomicOr(&unif[j >> 6], 1ull << (j & 63));
-          }
+        if (lane == 0) {  // (a column without exceptions: cuw[j] = nw0, set above)
+          if (anymx) atomicAnd(&unif[j >> 6], ~(1ull << (j & 63)));
+          else atomicOr(&unif[j >> 6], 1ull << (j & 63));
         }
         WPROF_T(pc1);
         WPROF_ADD(pf_col, pc1 - pc0 - (ps1 - ps0));
@@ -1059,6 +1194,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     if (tid == 0) {
       misc[W_RCH + npar] = 0;  // round r+1's change flag (round r-1's was read)
       misc[W_TCOL] = 0;        // every wave has left this round's column loop
+      misc[W_NBID + npar] = 0; // the bid list this round's updates read: round r+1's selects refill it
     }
     {
       // outbid vehicles, a ticket at a time (a re-select writes only its own
@@ -1072,12 +1208,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           const int v = kth_bit(obm + par * NW, NW, tk);
           WPROF_T(pr0);
           WPROF_ADD(pf_cnt, 1ull << 42);
-          const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, cuw, unif, false, mp);
-          if (task >= 0 && lane == 0) {
-            T[tix(n, task, v)] = (uint16_t)v;
-            atomicOr(&dmask[npar * NW + (task >> 6)], 1ull << (task & 63));
-            atomicAnd(&unif[task >> 6], ~(1ull << (task & 63)));
-          }
+          const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, tab, false, mp);
+          if (task >= 0 && lane == 0) place_bid(v, task, par);
           WPROF_T(pr1);
           WPROF_ADD(pf_sel, pr1 - pr0);
         }
@@ -1112,6 +1244,41 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   }
 #endif
 
+  // Bids of the last select phase that no column update applied (the rounds
+  // ran to the 2n limit with re-selects in the last one): fold them into
+  // their columns -- an exception entry while there is room, else the
+  // column is written to T in full (dense). One wave, bid by bid.
+  if (wave == 0) {
+    const int nb = misc[W_NBID + lastpar];
+    const unsigned* bl = bids + lastpar * n;
+    for (int k = 0; k < nb; ++k) {
+      const unsigned e = bl[k];
+      const int v = (int)(e >> 16), task = (int)(e & 0xFFFFu);
+      if (!tab.sparse(task)) {
+        if (lane == 0) T[tix(n, task, v)] = (uint16_t)v;  // (dense bids went to T already)
+        continue;
+      }
+      const int ne = ecnt[task];
+      int slot = -1;
+      for (int q = 0; q < ne; ++q)
+        if ((elist[task * kWSparseK + q] >> 16) == (unsigned)v) slot = q;
+      if (slot < 0 && ne < kWSparseK) slot = ne;
+      if (slot >= 0) {
+        if (lane == 0) {
+          elist[task * kWSparseK + slot] = ((unsigned)v << 16) | (unsigned)v;
+          if (slot == ne) ecnt[task] = (unsigned char)(ne + 1);
+        }
+      } else {
+        for (int u = lane; u < n; u += 64)
+          T[tix(n, task, u)] = (uint16_t)(u == v ? (unsigned)v : tab.sparse_entry(task, u));
+        if (lane == 0) atomicAnd(&spm[task >> 6], ~(1ull << (task & 63)));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+  }
+  __syncthreads();
   wstamp(P, b, 4);
   // swarm margin: min over every thread's CBAA pair (the alignment gaps are
   // in the word already)
@@ -1141,7 +1308,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     if (tid < NW) sw[tid] = 0ull;
     __syncthreads();
     for (int j = tid; j < n; j += kWBlock) {
-      const int w = T[tix(n, j, 0)];
+      const int w = cuw[j];  // every column uniform: its one `who`
       if (w >= n) misc[M_NINV] = n;
       else atomicOr(&sw[w >> 6], 1ull << (w & 63));
     }
@@ -1154,7 +1321,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     __syncthreads();
     const bool valid0 = misc[M_NINV] == 0;
     for (int j = tid; j < n; j += kWBlock) {
-      const int v = valid0 ? T[tix(n, j, 0)] : Ptin[j];
+      const int v = valid0 ? (int)cuw[j] : Ptin[j];
       validv[v] = valid0;
       if (j != Pin[v]) misc[M_CHANGED] = 1;
       P.P_out[(size_t)b * n + v] = (uint16_t)j;
@@ -1171,10 +1338,10 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       const int jj = lane + 64 * c;
       bool ismine = false;
       if (jj < n) {
-        const int w = T[tix(n, jj, v)];
+        const int w = (int)tab(jj, v);
         if (w >= n) bad = true;
         else atomicOr(&sw[w >> 6], 1ull << (w & 63));
-        diff |= w != T[tix(n, jj, 0)];
+        diff |= w != (int)tab(jj, 0);
         ismine = w == v;
       }
       const unsigned long long mm = __ballot(ismine);
@@ -1200,7 +1367,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   if (P.who) {
     for (int k = tid; k < n * n; k += kWBlock) {
       const int v = k / n, jj = k - v * n;
-      const int w = T[tix(n, jj, v)];
+      const int w = (int)tab(jj, v);
       P.who[(size_t)b * n * n + k] = (w >= n) ? (uint16_t)0xFFFF : (uint16_t)w;
     }
   }
@@ -1212,12 +1379,12 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     uint16_t* wsPt = reinterpret_cast<uint16_t*>(P.ws + P.W.pt) + (size_t)b * n;
     if (tid == 0) P.ws[P.W.mode + b] = uniform ? 0 : 1;
     if (uniform) {
-      for (int jj = tid; jj < n; jj += kWBlock) wsPt[jj] = allvalid ? T[tix(n, jj, 0)] : Ptin[jj];
+      for (int jj = tid; jj < n; jj += kWBlock) wsPt[jj] = allvalid ? (uint16_t)tab(jj, 0) : Ptin[jj];
     } else {
       uint16_t* rows = reinterpret_cast<uint16_t*>(P.ws + P.W.rows) + (size_t)b * n * n;
       for (int k = tid; k < n * n; k += kWBlock) {
         const int v = k / n, jj = k - v * n;
-        rows[k] = validv[v] ? T[tix(n, jj, v)] : Ptin[jj];
+        rows[k] = validv[v] ? (uint16_t)tab(jj, v) : Ptin[jj];
       }
       for (int v = tid; v < n; v += kWBlock) P.ws[P.W.vvalid + (size_t)b * n + v] = validv[v];
     }

@@ -33,12 +33,21 @@
  *    the new-assignment handler, didConvergeOnInvalidAssignment). The
  *    result equals the reference's when all vehicles start from the same
  *    snapshot q (the synchronous case the parity tests pin). The send-bid
- *    handler is stored but never invoked, enqueueBid/tick accept and drop
- *    bids (no bids cross the network), and isIdle() is true whenever start()
- *    is not running.
- *  - Errors. The reference has none (asserts only); failures of the GPU
- *    layer (no device, out of memory, bad sizes) throw std::runtime_error
- *    with acl_last_error().
+ *    handler is called once per auction, after the consensus, with this
+ *    vehicle's final bid (the table the reference's vehicle holds after its
+ *    last round: who, and each task's price rebuilt from the holder's
+ *    alignment as getPrice computes it, auctioneer.cpp:546-549) and
+ *    iter = 2n (cbaa_max_iter_), so a ROS-side wrapper can still publish a
+ *    CBAA.msg per auction (coordination_ros.cpp:308-318); the per-round bids
+ *    never leave the GPU. enqueueBid/tick accept and drop bids, and isIdle()
+ *    is true whenever start() is not running.
+ *  - Errors. The reference has none (asserts only). Auctioneer::start keeps
+ *    that shape: a call it cannot run (no formation, q not n x 3, a GPU-layer
+ *    failure) runs no auction, calls no handler and leaves the assignment as
+ *    it was; lastStatus() returns the acl_status_t (ACL_OK after a good
+ *    auction) and lastError() the message. The other facade calls
+ *    throw std::runtime_error with acl_last_error() on GPU-layer failures
+ *    (no device, out of memory, bad sizes).
  *  - Each call is synchronous on the default HIP stream. For throughput use
  *    the batched C entry points (one call for B swarms); this facade is for
  *    drop-in use, one swarm at a time.
@@ -355,7 +364,7 @@ class Auctioneer {
       f(user, P.indices().data(), (int32_t)P.indices().size());
     };
   }
-  /* Stored, never invoked: bids do not leave the GPU (see file header). */
+  /* Called once per auction with the final bid (see file header). */
   void setSendBidHandler(std::function<void(uint32_t, uint32_t, const BidConstPtr&)> f) {
     send_bid_ = std::move(f);
   }
@@ -370,6 +379,7 @@ class Auctioneer {
   /* p column-major n x 3, adjmat column-major n x n */
   void setFormationColMajor(const double* p_colmajor, const uint8_t* adj_colmajor) {
     form_.upload(n_, p_colmajor, adj_colmajor, nullptr);
+    form_p_ = detail::rows_xyz(n_, p_colmajor);
     auction_open_ = false;
     formation_just_received_ = true;
     for (int i = 0; i < n_; ++i) P_[i] = Pt_[i] = (vehidx_t)i;
@@ -378,14 +388,38 @@ class Auctioneer {
   /* auctioneer.cpp:78-125 + 245-306: run the auction on snapshot q to
    * consensus and adopt this vehicle's result. */
   void start(const PtsMat& q) {
-    if (q.rows() != n_ || q.cols() != 3)
-      throw std::runtime_error("Auctioneer::start: q is not n x 3");
+    if (q.rows() != n_ || q.cols() != 3) {
+      last_status_ = ACL_ERR_INVALID_ARG;
+      last_error_ = "Auctioneer::start: q is not n x 3";
+      return;
+    }
     startColMajor(q.data());
   }
   /* q column-major n x 3 */
   void startColMajor(const double* q_colmajor) {
     std::lock_guard<std::mutex> lock(auction_mtx_);
-    if (form_.n != n_) throw std::runtime_error("Auctioneer::start before setFormation");
+    if (form_.n != n_) {
+      last_status_ = ACL_ERR_INVALID_ARG;
+      last_error_ = "Auctioneer::start before setFormation";
+      return;
+    }
+    try {
+      run_auction(q_colmajor);
+      last_status_ = ACL_OK;
+      last_error_.clear();
+    } catch (const std::exception& e) {
+      last_status_ = ACL_ERR_HIP;
+      last_error_ = e.what();
+    }
+    auction_open_ = false;
+  }
+  /* the outcome of the last start(): ACL_OK, or why no auction ran
+   * (lastError() says what) */
+  acl_status_t lastStatus() const { return last_status_; }
+  const std::string& lastError() const { return last_error_; }
+
+ private:
+  void run_auction(const double* q_colmajor) {
     auction_open_ = true;
     auctionid_++;
     if (verbose_)  // auctioneer.cpp:110-115
@@ -402,6 +436,7 @@ class Auctioneer {
     d_pout_.reserve((size_t)n * 2);
     d_status_.reserve(sizeof(acl_swarm_status_t));
     d_who_.reserve((size_t)n * n * 2);
+    d_rt_.reserve((size_t)n * 6 * 8);
     d_ws_.reserve(acl_solve_workspace_bytes(n, 1));
 
     const acl_formations_t F = form_.table();
@@ -414,6 +449,7 @@ class Auctioneer {
     a.P_out = d_pout_.as<uint16_t>();
     a.status = d_status_.as<acl_swarm_status_t>();
     a.who = d_who_.as<uint16_t>();
+    a.align_Rt = d_rt_.as<double>();
     a.workspace = d_ws_.get();
     acl_default_cntrl_gains(&a.cntrl);
     acl_default_safety_params(&a.safety);
@@ -421,12 +457,44 @@ class Auctioneer {
     a.do_control = 0;
     detail::check(acl_solve_batch(&F, &a, nullptr));
     std::vector<uint16_t> who(n);  // this vehicle's final table: task -> vehicle
+    std::vector<double> Rt((size_t)n * 6);
     detail::check(acl_memcpy_d2h(who.data(), d_who_.as<uint16_t>() + (size_t)vehid_ * n,
                                  (size_t)n * 2, nullptr));
+    detail::check(acl_memcpy_d2h(Rt.data(), d_rt_.get(), Rt.size() * 8, nullptr));
     detail::check(acl_stream_synchronize(nullptr));
+    if (send_bid_) send_bid_((uint32_t)auctionid_, (uint32_t)(2 * n), finalBid(q, who, Rt));
     finish(who);
-    auction_open_ = false;
   }
+
+  /* The final bid of this vehicle: who[j] (-1 = none) and price[j] = the
+   * holder's getPrice for task j (auctioneer.cpp:546-549), from the holder's
+   * alignment (R, t) applied to formation point j as alignFormation does
+   * (R p + t, z row identity, auctioneer.cpp:400-414): the same f64
+   * operations, so the float equals the holder's bid bit for bit. */
+  BidConstPtr finalBid(const std::vector<double>& q, const std::vector<uint16_t>& who,
+                       const std::vector<double>& Rt) const {
+    const int n = n_;
+    auto bid = std::make_shared<Bid>();
+    bid->price.assign(n, 0.0f);
+    bid->who.assign(n, -1);
+    for (int j = 0; j < n; ++j) {
+      const unsigned w = who[j];
+      if (w >= (unsigned)n) continue;
+      const double* o = &Rt[(size_t)6 * w];
+      const double px = form_p_[(size_t)3 * j], py = form_p_[(size_t)3 * j + 1],
+                   pz = form_p_[(size_t)3 * j + 2];
+      const double ax = ((o[0] * px + o[1] * py) + 0.0 * pz) + o[4];
+      const double ay = ((o[2] * px + o[3] * py) + 0.0 * pz) + o[5];
+      const double az = ((0.0 * px + 0.0 * py) + 1.0 * pz) + 0.0;
+      const double dx = q[(size_t)3 * w] - ax, dy = q[(size_t)3 * w + 1] - ay,
+                   dz = q[(size_t)3 * w + 2] - az;
+      bid->price[j] = (float)(1.0 / (std::sqrt((dx * dx + dy * dy) + dz * dz) + 1e-8));
+      bid->who[j] = (int)w;
+    }
+    return bid;
+  }
+
+ public:
 
   /* Accepted and dropped: the consensus ran inside start(). */
   void enqueueBid(vehidx_t, uint32_t, uint32_t, const Bid&) {
@@ -507,8 +575,11 @@ class Auctioneer {
   std::mutex queue_mtx_, auction_mtx_;
   std::function<void(const AssignmentPerm&)> handler_;
   std::function<void(uint32_t, uint32_t, const BidConstPtr&)> send_bid_;
+  acl_status_t last_status_ = ACL_OK;
+  std::string last_error_;
+  std::vector<double> form_p_;  // formation points, xyz rows (final bids)
   detail::DeviceFormation form_;
-  detail::DeviceBuffer d_q_, d_pin_, d_fidx_, d_pout_, d_status_, d_who_, d_ws_;
+  detail::DeviceBuffer d_q_, d_pin_, d_fidx_, d_pout_, d_status_, d_who_, d_rt_, d_ws_;
 };
 
 // ============================================================================

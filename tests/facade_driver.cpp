@@ -12,6 +12,8 @@
 //        column-major); f64 q[n*3] (column-major); f64 vel[n][3];
 //        u8 P_in[n]; i32 m; f64 pts[3*m] (3 x m column-major); f64 adjf[m*m]
 // output: per vehicle v: u8 P[n], u8 invalid, u8 handler_calls;
+//         per vehicle v: u8 send_bid_calls, u32 iter, i32 who[n], f32 price[n]
+//         (the last bid its send-bid handler got); u8 start_errors_ok;
 //         f64 u[n][3]; i32 iters[2]; f64 A[9m^2] (column-major)
 #include <stdio.h>
 
@@ -47,6 +49,12 @@ struct Coordination {
   amd::AssignmentPerm Pcentral_;
   int handler_calls = 0;
   std::vector<amd::vehidx_t> neighbours;  // vehicles connectToNeighbors found
+  // what sendBidCb published last (coordination_ros.cpp:308-318 copies the
+  // bid into a CBAA.msg: auctionid, iter, price[], who[])
+  int bid_calls = 0;
+  uint32_t bid_auction = 0, bid_iter = 0;
+  std::vector<float> bid_price;
+  std::vector<int32_t> bid_who;
 
   Coordination(amd::vehidx_t vehid, uint8_t n) : vehid_(vehid), n_(n) {
     // coordination_ros.cpp:176-178
@@ -57,8 +65,16 @@ struct Coordination {
     namespace ph = std::placeholders;
     auctioneer_->setNewAssignmentHandler(
         std::bind(&Coordination::newAssignmentCb, this, ph::_1));
-    auctioneer_->setSendBidHandler(
-        [](uint32_t, uint32_t, const amd::Auctioneer::BidConstPtr&) {});
+    auctioneer_->setSendBidHandler(std::bind(&Coordination::sendBidCb, this, ph::_1, ph::_2, ph::_3));
+  }
+
+  // coordination_ros.cpp:308-318 (sendBidCb): the message copies the bid
+  void sendBidCb(uint32_t auctionid, uint32_t iter, const amd::Auctioneer::BidConstPtr& bid) {
+    ++bid_calls;
+    bid_auction = auctionid;
+    bid_iter = iter;
+    bid_price.assign(bid->price.begin(), bid->price.end());
+    bid_who.assign(bid->who.begin(), bid->who.end());
   }
 
   // coordination_ros.cpp:110-129 (formationCb); gains solved only when none
@@ -167,6 +183,40 @@ extern "C" int facade_run(const char* in_path, const char* out_path) {
       wr(out, Pv.data(), n);
       wr(out, &inv, 1);
       wr(out, &nc, 1);
+      if (c.bid_calls && c.bid_auction != (uint32_t)c.auctioneer_->auctionId())
+        throw std::runtime_error("send-bid handler: wrong auction id");
+      if (c.auctioneer_->lastStatus() != ACL_OK) throw std::runtime_error("start failed");
+    }
+    for (int v = 0; v < n; ++v) {
+      const Coordination& c = *veh[v];
+      const uint8_t bc = (uint8_t)c.bid_calls;
+      wr(out, &bc, 1);
+      wr(out, &c.bid_iter, 1);
+      std::vector<int32_t> w(n, -2);
+      std::vector<float> pr(n, -1.0f);
+      if (c.bid_calls) {
+        w = c.bid_who;
+        pr = c.bid_price;
+      }
+      wr(out, w.data(), n);
+      wr(out, pr.data(), n);
+    }
+    // start() that cannot run: a status, no exception, no handler, no auction
+    {
+      amd::Auctioneer a(0, (uint8_t)n, false);
+      int calls = 0;
+      a.setSendBidHandler([&](uint32_t, uint32_t, const amd::Auctioneer::BidConstPtr&) { ++calls; });
+      a.start(q);  // before setFormation
+      bool ok = a.lastStatus() == ACL_ERR_INVALID_ARG && a.isIdle() && calls == 0 &&
+                a.auctionId() == 0 && !a.lastError().empty();
+      a.setFormation(p, adj);
+      amd::PtsMat qbad(n, 2);
+      a.start(qbad);  // q not n x 3
+      ok = ok && a.lastStatus() == ACL_ERR_INVALID_ARG && calls == 0 && a.auctionId() == 0;
+      a.start(q);
+      ok = ok && a.lastStatus() == ACL_OK && calls == 1 && a.auctionId() == 1;
+      const uint8_t okb = ok ? 1 : 0;
+      wr(out, &okb, 1);
     }
 
     // control: each vehicle's DistCntrl with the assignment its handler set

@@ -51,11 +51,20 @@ def _run(tmp_path, p, adj, gains, q, vel, P_in, pts=None, adjf=None):
     for _ in range(n):
         P.append(np.frombuffer(raw, np.uint8, n, o)); o += n
         inv.append(raw[o]); calls.append(raw[o + 1]); o += 2
+    bid_calls, bid_iter, bid_who, bid_price = [], [], [], []
+    for _ in range(n):
+        bid_calls.append(raw[o]); o += 1
+        bid_iter.append(int(np.frombuffer(raw, np.uint32, 1, o)[0])); o += 4
+        bid_who.append(np.frombuffer(raw, np.int32, n, o)); o += 4 * n
+        bid_price.append(np.frombuffer(raw, np.float32, n, o)); o += 4 * n
+    start_errors_ok = raw[o]; o += 1
     u = np.frombuffer(raw, np.float64, 3 * n, o).reshape(n, 3); o += 24 * n
     its = np.frombuffer(raw, np.int32, 2, o); o += 8
     A = np.frombuffer(raw, np.float64, 9 * m * m, o).reshape(3 * m, 3 * m, order="F")
     return dict(P=np.array(P), invalid=np.array(inv), calls=np.array(calls), u=u,
-                iters=its, A=A)
+                iters=its, A=A, bid_calls=np.array(bid_calls), bid_iter=np.array(bid_iter),
+                bid_who=np.array(bid_who), bid_price=np.array(bid_price),
+                start_errors_ok=start_errors_ok)
 
 
 def _expect(p, adj, gains, q, vel, P_in):
@@ -80,6 +89,16 @@ def _check(got, p, adj, gains, q, vel, P_in):
     P, inv, u = _expect(p, adj, gains, q, vel, P_in)
     np.testing.assert_array_equal(got["invalid"], inv)
     np.testing.assert_array_equal(got["calls"], 1 - inv)
+    # the send-bid handler: once per vehicle per auction, iter = 2n, the bid
+    # equal to the oracle's final bid table row (who and price, bit for bit)
+    n = p.shape[0]
+    C, _ = O.prices(q, p, adj, np.asarray(P_in, np.uint16))
+    who, pr, _ = O.cbaa(C, adj, np.asarray(P_in, np.uint16))
+    np.testing.assert_array_equal(got["bid_calls"], np.ones(n))
+    np.testing.assert_array_equal(got["bid_iter"], np.full(n, 2 * n))
+    np.testing.assert_array_equal(got["bid_who"], who)
+    np.testing.assert_array_equal(got["bid_price"].view(np.uint32), pr.view(np.uint32))
+    assert got["start_errors_ok"] == 1
     for v in range(p.shape[0]):
         if not inv[v]:
             np.testing.assert_array_equal(got["P"][v], P[v], err_msg=f"vehicle {v}")

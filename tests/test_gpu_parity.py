@@ -324,6 +324,48 @@ def test_wide_n(cuda, n):
     _compare(gpu, ref)
 
 
+@pytest.mark.parametrize("early_exit", [True, False])
+def test_wide_unconverged_and_sparse_graphs(cuda, early_exit):
+    """n > 128 auctions that end at the 2n-round limit with re-selects in the
+    last round (chain and lollipop formation graphs: consensus needs more
+    than 2n lockstep rounds along a long path), and a 70%-dense graph whose
+    column updates leave many vehicles on other entries: the wide kernel's
+    sparse columns, their dense fallback and the fold-in of the last round's
+    bids against the oracle, tables bit for bit."""
+    rng = np.random.RandomState(136)
+    pts, adjs = [], []
+    for n_tail in (None, 60, 0):
+        n = 136
+        adj = np.zeros((n, n), np.uint8)
+        perm = rng.permutation(n)
+        if n_tail is None:      # a chain
+            chain = perm
+        elif n_tail == 0:       # 70% dense, no chain
+            adj = np.triu((rng.rand(n, n) < 0.7).astype(np.uint8), 1)
+            adj = adj + adj.T
+            chain = perm[:0]
+        else:                   # a lollipop: clique + tail
+            core = perm[:n - n_tail]
+            adj[np.ix_(core, core)] = 1
+            np.fill_diagonal(adj, 0)
+            chain = perm[n - n_tail - 1:]
+        for x, y in zip(chain[:-1], chain[1:]):
+            adj[x, y] = adj[y, x] = 1
+        pts.append(np.c_[rng.uniform(-34, 34, (n, 2)), rng.uniform(0, 2, n)])
+        adjs.append(adj)
+    gains = [H.synth_gains(rng, a) for a in adjs]
+    B = 6
+    fidx = np.arange(B) % 3
+    q = np.stack([np.c_[rng.uniform(-34, 34, (136, 2)), np.ones(136)] for _ in range(B)])
+    vel = np.zeros((B, 136, 3))
+    P_in = np.stack([H.random_perm(rng, 136) for _ in range(B)])
+    gpu = _gpu_solve(pts, adjs, gains, fidx, q, vel, P_in, early_exit=early_exit)
+    ref = _oracle(pts, adjs, gains, fidx, q, vel, P_in, early_exit=early_exit)
+    _compare(gpu, ref)
+    # the chain / lollipop swarms really ran to the limit
+    assert (gpu["status"]["eff_rounds"][fidx < 2] == 2 * 136).any()
+
+
 def test_wide_collision_avoidance(cuda):
     """Crowded n = 160 swarms: the collision-avoidance list over three chunks."""
     rng = np.random.RandomState(160)

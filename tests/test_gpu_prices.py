@@ -43,6 +43,8 @@ def test_price_fast_path_bit_exact(cuda):
     xs = [
         10.0 ** rng.uniform(-320, 308, 1 << 21),            # the whole double range
         rng.uniform(0, 40.0, 1 << 21) ** 2,                  # distances of the bench (C3)
+        10.0 ** rng.uniform(-9, -3, 1 << 18),                # around the fast path's 1e-6 cut
+        np.nextafter(1e-6, np.array([0.0, np.inf])),
         _midpoint_inputs(rng, 1 << 17),
         np.array([0.0, -0.0, 1e-320, 5e-324, 1e-200, 1e60, 1e300, np.inf, -1.0, np.nan,
                   np.finfo(np.float64).max, 1e-16, 1e-17]),
