@@ -249,6 +249,12 @@ struct SecProf {
 #ifndef ACL_CBAA_WAVES
 #define ACL_CBAA_WAVES 8
 #endif
+// Rounds in which the waves publish their gap bounds (ACL_PUBLISH_ROUNDS,
+// default all): later rounds prune against the last published value (an
+// upper bound of the swarm's minimum, so every pruning decision stays valid).
+#ifndef ACL_PUBLISH_ROUNDS
+#define ACL_PUBLISH_ROUNDS 0x7fffffff
+#endif
 
 // An upper bound of margin_gap(hi, lo) in f32 for the mid-auction
 // publications of the margin word (the walk bound's Gpub): (hi - lo) is exact
@@ -1002,6 +1008,13 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     // for the conservative f32 tests (at least Gw (1 + 2^-20)), refreshed after walks
     double Gw = fmin(Gpub, margin_gap_pair(uhi, ulo));
     float Gwf = (float)(Gw * (1.0 + 0x1p-20));
+    // 1 - Gw (1 + 2^-20) as a float one ulp below its rounding (a lower
+    // bound), 0 when not positive: the successor test's factor (below)
+    auto gfac = [](double gw) {
+      const double x = 1.0 - gw * (1.0 + 0x1p-20);
+      return x > 0.0 ? __uint_as_float(__float_as_uint((float)x) - 1u) : 0.0f;
+    };
+    float Gfacf = gfac(Gw);
     {
       // one loop over both words (the column body is emitted once)
       unsigned long long mm = mine[0], m1 = NC > 1 ? mine[NC - 1] : 0ull;
@@ -1126,10 +1139,12 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         if (!ACL_AUCTION_NO_MARGIN && !walk && kres != 0u && cum < n) {
           // the last resolving level's successor (the highest key below
           // kres) within Gw: an entry with a key in [low, kres), low the key
-          // of P(kres) (1 - Gw (1 + 2^-20)) rounded down (f64, then one f32
-          // ulp lower), so no successor within Gw is missed
-          const double lowd = (double)__uint_as_float(kres - 1u) * (1.0 - Gw * (1.0 + 0x1p-20));
-          const unsigned lowk = lowd > 0.0 ? __float_as_uint((float)lowd) : 1u;  // bits - 1 + 1
+          // of a lower bound of P(kres) (1 - Gw (1 + 2^-20)): the f32 product
+          // with the factor one ulp low, then one more ulp lower, so no
+          // successor within Gw is missed
+          const float lowf = __uint_as_float(kres - 1u) * Gfacf;
+          const unsigned lb = __float_as_uint(lowf);
+          const unsigned lowk = lb > 1u ? lb : 1u;  // (bits - 1) + 1
           unsigned long long any = 0ull;
 #pragma unroll
           for (int c = 0; c < NC; ++c) any |= __ballot(key[c] >= lowk && key[c] < kres);
@@ -1144,6 +1159,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           runner_up_walk<NC>(n, key, k1, Nd, vm, uhi, ulo);
           Gw = fmin(Gpub, margin_gap_pair(uhi, ulo));
           Gwf = (float)(Gw * (1.0 + 0x1p-20));
+          Gfacf = gfac(Gw);
           if (ACL_AUCTION_PROF) sp.walks++;
           sp.mark(PS_WALK);
         }
@@ -1220,7 +1236,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       const unsigned long long ob = __ballot((fl >> c) & 1u);
       if (ob && lane == 0) atomicOr(&obm[2 * par + c], ob);
     }
-    if (!ACL_AUCTION_NO_PUBLISH && (!ACL_CBAA_LAZY || evald)) {
+    if (!ACL_AUCTION_NO_PUBLISH && (!ACL_CBAA_LAZY || evald) && r <= ACL_PUBLISH_ROUNDS) {
       // publish this wave's smallest gap so far (its lanes' select and scan
       // evaluations, its walks' pair) for the next round's pruning: an upper
       // bound is enough there (gap_ub); only after a round in which the wave

@@ -115,7 +115,7 @@ __host__ __device__ inline WALayout make_walayout(int n) {
 
 // solve_wide_kernel's LDS
 struct WLayout {
-  int p, qv, vadj, Pin, Ptin, ccw, ccp, cuw, valid, masks, seen, misc, ecnt, elist, bids, total;
+  int p, qv, vadj, Pin, Ptin, ccw, ccp, cuw, valid, masks, seen, misc, ecnt, elist, bids, xcnt, total;
 };
 
 __host__ __device__ inline WLayout make_wlayout(int n) {
@@ -137,6 +137,7 @@ __host__ __device__ inline WLayout make_wlayout(int n) {
   L.ecnt = o;  o = wal(o + n);                         // exceptions of a sparse column
   L.elist = o; o = wal(o + n * kWSparseK * 4);         // [j][K] vehicle << 16 | who
   L.bids = o;  o = wal(o + 2 * n * 4);                 // [2][n] bid lists: vehicle << 16 | task
+  L.xcnt = o;  o = wal(o + n * 4);                     // [n] sparse columns a vehicle is an exception in
   L.total = o;
   return L;
 }
@@ -183,6 +184,7 @@ struct WTable {
   const unsigned char* ecnt;
   const unsigned* elist;
   const unsigned long long* spm;
+  const unsigned* xcnt;  // [u]: sparse columns whose exception list holds vehicle u
   int n;
   __device__ __forceinline__ bool sparse(int j) const { return (spm[j >> 6] >> (j & 63)) & 1ull; }
   __device__ __forceinline__ unsigned sparse_entry(int j, int u) const {
@@ -210,19 +212,34 @@ __device__ int wide_select(int n, int NW, int v, int lane, const WPrice& price,
   unsigned lm = 0u;
   int wv[kWMaxW];
   // row v of the tiled table: task j = lane + 64 c at Tv[lo + c * 512 n8];
-  // a sparse column's entry comes from LDS (its base or v's exception), so
+  // a sparse column's entry comes from LDS -- its base, unless v is one of
+  // its exceptions (only looked up when v is an exception somewhere) -- so
   // only the dense columns' entries are read from the table
   const int n8 = (n + 7) >> 3;
   const uint16_t* Tv = T + (((v >> 3) << 6) + (v & 7));
   const int lo = (((lane >> 3) * n8) << 6) + ((lane & 7) << 3);
+  const bool vx = !fresh && tab.xcnt[v] != 0;  // wave-uniform
+  if (vx) {
 #pragma unroll
-  for (int c = 0; c < kWMaxW; ++c) {
-    const int j = lane + 64 * c;
-    if (fresh || c >= NW || j >= n) {
-      wv[c] = n;
-    } else {
-      const bool spl = (tab.spm[c] >> lane) & 1ull;
-      wv[c] = spl ? (int)tab.sparse_entry(j, v) : (int)Tv[lo + c * (n8 << 9)];
+    for (int c = 0; c < kWMaxW; ++c) {
+      const int j = lane + 64 * c;
+      if (c >= NW || j >= n) {
+        wv[c] = n;
+      } else {
+        const bool spl = (tab.spm[c] >> lane) & 1ull;
+        wv[c] = spl ? (int)tab.sparse_entry(j, v) : (int)Tv[lo + c * (n8 << 9)];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < kWMaxW; ++c) {
+      const int j = lane + 64 * c;
+      if (fresh || c >= NW || j >= n) {
+        wv[c] = n;
+      } else {
+        const bool spl = (tab.spm[c] >> lane) & 1ull;
+        wv[c] = spl ? (int)tab.cuw[j] : (int)Tv[lo + c * (n8 << 9)];
+      }
     }
   }
 #pragma unroll
@@ -759,6 +776,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   unsigned char* ecnt = smem + L.ecnt;
   unsigned* elist = reinterpret_cast<unsigned*>(smem + L.elist);
   unsigned* bids = reinterpret_cast<unsigned*>(smem + L.bids);  // [2][n]
+  unsigned* xcnt = reinterpret_cast<unsigned*>(smem + L.xcnt);
 
   unsigned char* wsb = P.ws + P.W.wide + (size_t)b * P.W.wide_stride;
   uint16_t* T = reinterpret_cast<uint16_t*>(wsb);
@@ -818,6 +836,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     for (int k = tid; k < n; k += kWBlock) {
       ccw[k] = cuw[k] = (uint16_t)n;
       ecnt[k] = 0;
+      xcnt[k] = 0;
     }
     if (tid < 32) misc[tid] = 0;
   }
@@ -859,7 +878,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   }
   __syncthreads();
   const bool nonfinite = misc[M_NONFIN] != 0;
-  const WTable tab{T, cuw, ecnt, elist, spm, n};
+  const WTable tab{T, cuw, ecnt, elist, spm, xcnt, n};
   wstamp(P, b, 3);
 
   // ---------------- phase 3: CBAA ------------------------------------------
@@ -884,6 +903,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
 #if ACL_WIDE_PROF
   unsigned long long pf_col = 0, pf_scan = 0, pf_sel = 0, pf_bar = 0, pf_cnt = 0, pf_rounds = 0;
   unsigned long long pf_cload = 0, pf_clvl = 0, pf_cwb = 0;
+  unsigned long long pf_sparse = 0;  // sparse-column updates | dense ones << 21 | sparse->dense << 42
 #endif
   unsigned obf = 0u;  // per-lane outbid bits (bit c: vehicle lane + 64 c), one round
   const int max_rounds = 2 * n;
@@ -928,19 +948,31 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           s2m |= (ok ? 0u : 1u) << c;
         }
         if (spj) {
-          // vehicle u's entry is `who` (u wave-uniform): one lane of one chunk
+          // vehicle u's entry is `who` (u wave-uniform, in a scalar register:
+          // the chunk is chosen by a scalar branch, one select per entry)
           auto set_entry = [&](unsigned u, unsigned who) {
             const int cu = (int)(u >> 6);
             const bool me = lane == (int)(u & 63u);
-#pragma unroll
-            for (int c = 0; c < kWMaxW; ++c)
-              if (c == cu) wu[c] = me ? who : wu[c];
+            switch (cu) {
+#define ACL_SET_CHUNK(c_) \
+  case c_:                \
+    if (c_ < kWMaxW) wu[c_ < kWMaxW ? c_ : 0] = me ? who : wu[c_ < kWMaxW ? c_ : 0]; \
+    break;
+              ACL_SET_CHUNK(0) ACL_SET_CHUNK(1) ACL_SET_CHUNK(2) ACL_SET_CHUNK(3)
+              ACL_SET_CHUNK(4) ACL_SET_CHUNK(5) ACL_SET_CHUNK(6) ACL_SET_CHUNK(7)
+#undef ACL_SET_CHUNK
+              default: break;
+            }
           };
+          static_assert(kWMaxW <= 8, "set_entry covers 8 chunks");
           const int ne = ecnt[j];
           for (int k = 0; k < ne; ++k) {
-            const unsigned e = elist[j * kWSparseK + k];
+            const unsigned e =
+                (unsigned)__builtin_amdgcn_readfirstlane((int)elist[j * kWSparseK + k]);
             set_entry(e >> 16, e & 0xFFFFu);
           }
+          // (the list is rewritten below: its vehicles' counts drop here)
+          if (lane < ne) atomicSub(&xcnt[elist[j * kWSparseK + lane] >> 16], 1u);
           const int nb = misc[W_NBID + npar];
           const unsigned* bl = bids + npar * n;
           for (int k0 = 0; k0 < nb; k0 += 64) {
@@ -1112,10 +1144,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         // the new state: sparse around the top level's `who` (the entry most
         // vehicles take) when at most kWSparseK vehicles hold another, else
         // dense in T (all entries written if T was stale, else the changed ones)
-        bool same = true;
-#pragma unroll
-        for (int c = 0; c < kWMaxW; ++c) same &= !(c < NW && lane + 64 * c < n) || nw[c] == nw0;
-        const unsigned nbase = (__ballot(!same) == 0ull || wk0 < 0 || wk0 >= n) ? nw0 : (unsigned)wk0;
+        unsigned nbase = (wk0 < 0 || wk0 >= n) ? nw0 : (unsigned)wk0;
         unsigned long long em[kWMaxW];
         int nexc = 0;
 #pragma unroll
@@ -1124,7 +1153,24 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           em[c] = __ballot(ok && nw[c] != nbase);
           nexc += __popcll(em[c]);
         }
+        if (nexc == n && nbase != nw0) {
+          // (rare: no vehicle holds the top level's `who`, a tie) around
+          // vehicle 0's entry instead
+          nbase = nw0;
+          nexc = 0;
+#pragma unroll
+          for (int c = 0; c < kWMaxW; ++c) {
+            const bool ok = c < NW && lane + 64 * c < n;
+            em[c] = __ballot(ok && nw[c] != nbase);
+            nexc += __popcll(em[c]);
+          }
+        }
+        // every vehicle holds one `who` <=> no exception around nbase (when
+        // some vehicle holds nbase; else it is vehicle 0's entry, above)
+        const bool uniformj = nexc == 0;
         const bool nsparse = nexc <= kWSparseK;
+        WPROF_ADD(pf_sparse, spj ? 1ull : (1ull << 21));
+        WPROF_ADD(pf_sparse, (spj && !nsparse) ? (1ull << 42) : 0ull);
         int erank = 0;
 #pragma unroll
         for (int c = 0; c < kWMaxW; ++c) {
@@ -1136,6 +1182,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
                                         (unsigned)(em[c] >> 32),
                                         __builtin_amdgcn_mbcnt_lo((unsigned)em[c], 0u));
               elist[j * kWSparseK + k] = ((unsigned)u << 16) | nw[c];
+              atomicAdd(&xcnt[u], 1u);
             }
             erank += __popcll(em[c]);
           } else if (ok && (!tvalid || nw[c] != wu[c])) {
@@ -1144,8 +1191,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           // outbid (:502): a per-lane bit, published once per wave and round
           obf |= (vflag(ok) & vflag(wu[c] == (unsigned)u) & vflag(nw[c] != (unsigned)u)) << c;
           ch |= nw[c] != wu[c];
-          mx |= ok && nw[c] != nw0;
         }
+        mx = !uniformj;
         if (lane == 0) {
           if (nsparse) {
             cuw[j] = (uint16_t)nbase;
@@ -1241,6 +1288,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     atomicAdd(ps + 6, pf_cload);
     atomicAdd(ps + 7, pf_clvl);
     atomicAdd(ps + 8, pf_cwb);
+    atomicAdd(ps + 9, pf_sparse);
   }
 #endif
 

@@ -116,6 +116,11 @@ if args.n > 128 and sec[:, :4].any():
           f"{(cnt >> np.uint64(42)).astype(float).mean():.1f}, rounds {sec[:, 5].astype(float).mean():.1f}")
     for k, nm in enumerate(["T load + keys", "levels", "write-back"]):
         print(f"    column {nm:14s} wave-cycles/swarm {sec[:, 6 + k].astype(np.float64).mean():12.0f}")
+    spc = st.cpu().numpy()[:, SEC + 9].astype(np.uint64)
+    if spc.any():
+        g = lambda sh: ((spc >> np.uint64(sh)) & m21).astype(float).mean()
+        print(f"  column updates per swarm: sparse {g(0):.1f}, dense {g(21):.1f}, "
+              f"sparse -> dense {g(42):.1f}")
 # collision avoidance (a -DACL_CA_PROF=1 build, --crowd): ca_kernel wave-cycles
 if args.crowd and not args.no_control:
     x = st.cpu().numpy()[:, SEC + 8:SEC + 12].astype(np.float64)
