@@ -310,7 +310,7 @@ __device__ __forceinline__ unsigned entry_key(const float* C, int n, int w, int 
 // argmax over its row (lanes = tasks), with the margin of its decisive
 // comparisons (include/aclswarm_amd.h). fresh: the START bid on an all-`none`
 // row. Returns the selected task (wave-uniform) or -1.
-template <int NC>
+template <int NC, bool MG>
 __device__ __forceinline__ int wave_select(int n, int TS, int v, int lane, const float* C,
                                            const unsigned char* T, bool fresh, MarginPair& m,
                                            unsigned* selx = nullptr) {
@@ -348,7 +348,7 @@ __device__ __forceinline__ int wave_select(int n, int TS, int v, int lane, const
     // with a gap <= G has cmax - cv <= G cmax or |cv - pr| <= G max(cv, pr)
     // -- passed 92% of the selects at C3: the selects' gaps set the margin.)
     if (ACL_AUCTION_PROF && selx) ++*selx;
-    if (!ACL_AUCTION_NO_SELMARGIN) {
+    if (MG && !ACL_AUCTION_NO_SELMARGIN) {
       const int j = lane + 64 * c;
       const bool isjs = oth[c] && j == js;
       const bool elig = oth[c] && !isjs && key[c] != 0u;
@@ -643,11 +643,13 @@ __global__ void __launch_bounds__(64) align_kernel(const SolveParams P) {
 // FUSE: phase 5, the control law of a swarm whose vehicles all adopted one
 // assignment, runs in this workgroup right after its auction (see below);
 // GM: the fused phase also reports the gate margin.
-template <int NC, int kAB, bool FUSE, bool GM>
+template <int NC, int kAB, bool FUSE, bool GM, bool MG>
 __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   constexpr int kAW = kAB / 64;  // waves per swarm
   constexpr int kCW = kAW < ACL_CBAA_WAVES ? kAW : ACL_CBAA_WAVES;  // CBAA round waves
   static_assert((kCW & (kCW - 1)) == 0, "ACL_CBAA_WAVES: a power of two");
+  // the CBAA rounds' decision-margin work (MG false: skip_margin)
+  constexpr bool kMarg = MG && !ACL_AUCTION_NO_MARGIN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const ALayout L = make_alayout(n);
@@ -939,11 +941,11 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       // the select's decision gaps (wave_select's terms on a fresh row): the
       // winner against its price 0 (gap 1), every eligible loser against the
       // winner -- the closest is the runner-up
-      if (sec) margin_track(mp, __uint_as_float((unsigned)(w >> 8)), __uint_as_float(sec));
+      if (MG && sec) margin_track(mp, __uint_as_float((unsigned)(w >> 8)), __uint_as_float(sec));
     }
   }
   // the START selects' gaps, published for round 1's walk bound
-  if (!ACL_AUCTION_NO_PUBLISH) publish_gap_ub(margw, mp, 1.0f, 0.0f);
+  if (MG && !ACL_AUCTION_NO_PUBLISH) publish_gap_ub(margw, mp, 1.0f, 0.0f);
   __syncthreads();
   ACL_AUCTION_STOP_AT(4);
 
@@ -1118,7 +1120,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
             if (!left || ++k == kAL) break;
             // the next level
             Mk = level_key<NC>(key, Mk);
-            if (!ACL_AUCTION_NO_MARGIN) {
+            if (kMarg) {
               // gap(P(kres), P(Mk)) <= Gw, tested conservatively in f32
               // (kres == 0: a NaN pair, no effect; Mk == 0: lo = NaN, no effect)
               const float hk = __uint_as_float(kres - 1u), lk = __uint_as_float(Mk - 1u);
@@ -1136,7 +1138,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
           }
         }
         sp.mark(PS_LV);
-        if (!ACL_AUCTION_NO_MARGIN && !walk && kres != 0u && cum < n) {
+        if (kMarg && !walk && kres != 0u && cum < n) {
           // the last resolving level's successor (the highest key below
           // kres) within Gw: an entry with a key in [low, kres), low the key
           // of a lower bound of P(kres) (1 - Gw (1 + 2^-20)): the f32 product
@@ -1153,7 +1155,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         // the exact runner-ups only where a level pair could lower the
         // wave's running minimum or the published one (an evaluation skipped
         // here has gaps >= its level pairs' > Gw, so the minimum is unchanged)
-        walk = walk && !ACL_AUCTION_NO_MARGIN;
+        walk = walk && kMarg;
         sp.mark(PS_MB);
         if (walk) {
           runner_up_walk<NC>(n, key, k1, Nd, vm, uhi, ulo);
@@ -1200,7 +1202,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
                 }
               }
               nw[c] = bw;
-              if (have2) margin_track(mp, bp, p2);
+              if (MG && have2) margin_track(mp, bp, p2);
             }
           }
         }
@@ -1236,7 +1238,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       const unsigned long long ob = __ballot((fl >> c) & 1u);
       if (ob && lane == 0) atomicOr(&obm[2 * par + c], ob);
     }
-    if (!ACL_AUCTION_NO_PUBLISH && (!ACL_CBAA_LAZY || evald) && r <= ACL_PUBLISH_ROUNDS) {
+    if (MG && !ACL_AUCTION_NO_PUBLISH && (!ACL_CBAA_LAZY || evald) && r <= ACL_PUBLISH_ROUNDS) {
       // publish this wave's smallest gap so far (its lanes' select and scan
       // evaluations, its walks' pair) for the next round's pruning: an upper
       // bound is enough there (gap_ub); only after a round in which the wave
@@ -1268,7 +1270,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
         while (mv) {
           const int v = 64 * c + __ffsll((long long)mv) - 1;
           mv &= mv - 1;
-          const int task = wave_select<NC>(n, TS, v, lane, C, T, false, mp, &sp.selx);
+          const int task = wave_select<NC, MG>(n, TS, v, lane, C, T, false, mp, &sp.selx);
           if (ACL_AUCTION_PROF) sp.sels++;
           evald = true;
           smem[(task >= 0 && lane == 0) ? L.T + v * TS + task : L.dummy + lane] = (unsigned char)v;
@@ -1302,8 +1304,8 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   sp.flush(P, b, lane);
   stamp_phase(P, b, tid, 4);
   ACL_AUCTION_STOP_AT(5);
-  {  // swarm margin: every lane's pair and the wave's level pair (the
-     // alignments' gaps are in already)
+  if (MG) {  // swarm margin: every lane's pair and the wave's level pair (the
+             // alignments' gaps are in already)
     margin_track(mp, uhi, ulo);
     block_min_gap(margw, margin_gap(mp));
   }
@@ -1416,8 +1418,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       if (misc[M_AGREE]) fl |= ACL_SWARM_AGREE;
       if (misc[M_CHANGED]) fl |= ACL_SWARM_CHANGED;
       if (nonfinite) fl |= ACL_SWARM_NONFINITE;
-      const double g = nonfinite ? 0.0 : __longlong_as_double((long long)*margw);
-      if (g < ACL_FRAGILE_MARGIN) fl |= ACL_SWARM_FRAGILE;
+      // (MG false: acl_solve_args_t::skip_margin -- not tracked, -1)
+      const double g = !MG ? -1.0 : nonfinite ? 0.0 : __longlong_as_double((long long)*margw);
+      if (MG && g < ACL_FRAGILE_MARGIN) fl |= ACL_SWARM_FRAGILE;
       st.flags = fl;
       st.eff_rounds = (uint16_t)eff;
       st.rounds = (uint16_t)(2 * n);
@@ -1476,13 +1479,13 @@ static int auction_lds(int n, bool fuse) {
   return a > g ? a : g;
 }
 
-template <bool FUSE, bool GM>
+template <bool FUSE, bool GM, bool MG>
 static hipError_t launch_auction_t(const SolveParams& P, int nb, hipStream_t stream) {
   static PerDeviceOnce once;
   const hipError_t ea = once.run([] {
-    for (const void* k : {(const void*)auction_kernel<1, 128, FUSE, GM>,
-                          (const void*)auction_kernel<1, 256, FUSE, GM>,
-                          (const void*)auction_kernel<2, 512, FUSE, GM>}) {
+    for (const void* k : {(const void*)auction_kernel<1, 128, FUSE, GM, MG>,
+                          (const void*)auction_kernel<1, 256, FUSE, GM, MG>,
+                          (const void*)auction_kernel<2, 512, FUSE, GM, MG>}) {
       const hipError_t e =
           hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
@@ -1498,20 +1501,27 @@ static hipError_t launch_auction_t(const SolveParams& P, int nb, hipStream_t str
   const int lds = auction_lds(P.n, FUSE);
   // (64 threads for n <= 32 measured no faster at C2: 0.091 vs 0.088 ms)
   if (P.n <= 32)
-    hipLaunchKernelGGL((auction_kernel<1, 128, FUSE, GM>), dim3(nb), dim3(128), lds, stream, P);
+    hipLaunchKernelGGL((auction_kernel<1, 128, FUSE, GM, MG>), dim3(nb), dim3(128), lds, stream, P);
   else if (P.n <= 64)
-    hipLaunchKernelGGL((auction_kernel<1, 256, FUSE, GM>), dim3(nb), dim3(256), lds, stream, P);
+    hipLaunchKernelGGL((auction_kernel<1, 256, FUSE, GM, MG>), dim3(nb), dim3(256), lds, stream, P);
   else
-    hipLaunchKernelGGL((auction_kernel<2, 512, FUSE, GM>), dim3(nb), dim3(512), lds, stream, P);
+    hipLaunchKernelGGL((auction_kernel<2, 512, FUSE, GM, MG>), dim3(nb), dim3(512), lds, stream, P);
   return hipGetLastError();
 }
 
 // fuse: run the control phase in the auction's workgroups (P.ctl filled;
 // 5-plane gain records, n <= 128)
+// skip_margin: the decision margin is not tracked (status margin -1)
 hipError_t launch_auction(const SolveParams& P, int nb, hipStream_t stream, bool fuse) {
-  if (!fuse) return launch_auction_t<false, false>(P, nb, stream);
-  if (P.ctl.gate_margin) return launch_auction_t<true, true>(P, nb, stream);
-  return launch_auction_t<true, false>(P, nb, stream);
+  const bool mg = !P.skip_margin;
+  if (!fuse)
+    return mg ? launch_auction_t<false, false, true>(P, nb, stream)
+              : launch_auction_t<false, false, false>(P, nb, stream);
+  if (P.ctl.gate_margin)
+    return mg ? launch_auction_t<true, true, true>(P, nb, stream)
+              : launch_auction_t<true, true, false>(P, nb, stream);
+  return mg ? launch_auction_t<true, false, true>(P, nb, stream)
+            : launch_auction_t<true, false, false>(P, nb, stream);
 }
 
 }  // namespace acl_amd

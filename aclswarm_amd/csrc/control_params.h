@@ -160,6 +160,7 @@ struct SolveParams {
   acl_safety_params_t s;
   int early_exit;
   int do_control;
+  int skip_margin;    // acl_solve_args_t::skip_margin (n <= 128)
   unsigned char* ws;  // workspace base (WsLayout)
   WsLayout W;
   unsigned long long* stamps;  // diagnostic: [B][kStampStride] (above; NULL = off)

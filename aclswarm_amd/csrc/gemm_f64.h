@@ -77,6 +77,12 @@ struct GemmWave {  // a wave index as a type (per-wave specialised code)
 };
 
 constexpr int kGemmKStep = 16;
+#ifndef ACL_GEMM_WSPEC
+#define ACL_GEMM_WSPEC 1  // the 80-tile kernel's K loop specialised per wave
+#endif
+#ifndef ACL_GEMM_OPF
+#define ACL_GEMM_OPF 1  // LDS operands read one k4 step ahead
+#endif
 #ifndef ACL_GEMM_TILE_DEFAULT
 #define ACL_GEMM_TILE_DEFAULT 80  // the four-wave 80 tile
 #endif
@@ -422,34 +428,53 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
   };
   const int tmask = J.tmask;
   const double tinv = tmask ? 1.0 / *J.tnrm : 1.0, tdiag = J.tdiag;
-  auto load = [&](int k0) {
+  // Operand staging. The loads go through global (address space 1) pointers,
+  // unconditionally from clamped offsets: a flat load would count in lgkmcnt
+  // too, so the LDS-read waits before the MFMAs would also wait for the next
+  // K step's operands; bounds (zero fill) and the operand transform are
+  // applied when the registers are written to LDS, after this step's MFMAs,
+  // so nothing waits for the loads before then.
+  typedef const __attribute__((address_space(1))) double gdouble;
+  gdouble* const gA = (gdouble*)J.A;
+  gdouble* const gB = (gdouble*)J.B;
+  // elements r0 .. r1 - 1 of this thread's share (the K loop may stage a
+  // step in two parts: fewer registers held across the MFMAs)
+  auto load_part = [&](int k0, int r0, int r1) {
 #pragma unroll
-    for (int r = 0; r < EPT; ++r) {
+    for (int r = r0; r < r1; ++r) {
       int i, kk;
       a_idx(r, i, kk);
       const int gi = m0 + i, gk = k0 + kk;
       const bool ina = gi < J.m && gk < J.k;
-      ra[r] = ina ? (TA ? J.A[gk + (size_t)gi * J.lda] : J.A[gi + (size_t)gk * J.lda]) : 0.0;
-      if ((tmask & 1) && ina) ra[r] = (ra[r] - (gi == gk ? tdiag : 0.0)) * tinv;
+      const size_t oa = ina ? (TA ? gk + (size_t)gi * J.lda : gi + (size_t)gk * J.lda) : 0;
+      ra[r - r0] = gA[oa];
       int j, kb;
       b_idx(r, j, kb);
       const int gj = n0 + j, gkb = k0 + kb;
       const bool inb = gj < J.n && gkb < J.k;
-      rb[r] = inb ? (TB ? J.B[gj + (size_t)gkb * J.ldb] : J.B[gkb + (size_t)gj * J.ldb]) : 0.0;
-      if ((tmask & 2) && inb) rb[r] = (rb[r] - (gj == gkb ? tdiag : 0.0)) * tinv;
+      const size_t ob = inb ? (TB ? gj + (size_t)gkb * J.ldb : gkb + (size_t)gj * J.ldb) : 0;
+      rb[r - r0] = gB[ob];
     }
   };
-  auto store = [&](int buf) {
+  auto store_part = [&](int buf, int k0, int r0, int r1) {
 #pragma unroll
-    for (int r = 0; r < EPT; ++r) {
+    for (int r = r0; r < r1; ++r) {
       int i, kk;
       a_idx(r, i, kk);
-      a_at(buf, kk, i) = ra[r];
+      const int gi = m0 + i, gk = k0 + kk;
+      double va = (gi < J.m && gk < J.k) ? ra[r - r0] : 0.0;
+      if ((tmask & 1) && gi < J.m && gk < J.k) va = (va - (gi == gk ? tdiag : 0.0)) * tinv;
+      a_at(buf, kk, i) = va;
       int j, kb;
       b_idx(r, j, kb);
-      b_at(buf, kb, j) = rb[r];
+      const int gj = n0 + j, gkb = k0 + kb;
+      double vb = (gj < J.n && gkb < J.k) ? rb[r - r0] : 0.0;
+      if ((tmask & 2) && gj < J.n && gkb < J.k) vb = (vb - (gj == gkb ? tdiag : 0.0)) * tinv;
+      b_at(buf, kb, j) = vb;
     }
   };
+  auto load = [&](int k0) { load_part(k0, 0, EPT); };
+  auto store = [&](int buf, int k0) { store_part(buf, k0, 0, EPT); };
   const int nk = (J.k + kGemmKStep - 1) / kGemmKStep;
   // alpha, beta of the epilogue (the scaled Newton-Schulz update, the
   // quintic band)
@@ -518,7 +543,7 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
       for (int q = 0; q < NQ; ++q) dacc[q] = f64x4{0.0, 0.0, 0.0, 0.0};
       if (nk > 0) {
         load(0);
-        store(0);
+        store(0, 0);
         __syncthreads();
       }
       for (int kb = 0; kb < nk; ++kb) {
@@ -533,7 +558,7 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
                                                           a_at(cur, kr, RB[W][q] * 16 + (lane & 15)),
                                                           dacc[q], 0, 0, 0);
         }
-        if (kb + 1 < nk) store(cur ^ 1);
+        if (kb + 1 < nk) store(cur ^ 1, (kb + 1) * kGemmKStep);
         __syncthreads();
       }
       double alpha, beta;
@@ -557,36 +582,93 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
   f64x4 acc[NB], acc4w = f64x4{0.0, 0.0, 0.0, 0.0}, acc44 = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int b = 0; b < NB; ++b) acc[b] = f64x4{0.0, 0.0, 0.0, 0.0};
-  if (nk > 0) {
-    load(0);
-    store(0);
-    __syncthreads();
-  }
-  for (int kb = 0; kb < nk; ++kb) {
-    const int cur = kb & 1;
-    if (kb + 1 < nk) load((kb + 1) * kGemmKStep);
-#pragma unroll
-    for (int k4 = 0; k4 < kGemmKStep; k4 += 4) {
+  // The K loop, specialised per wave (ACL_GEMM_WSPEC): block (4, w)'s B
+  // operand and the k4 step of block (4, 4) are then compile-time choices
+  // (no selects, no exec-masked MFMA); ACL_GEMM_OPF: each k4 step's LDS
+  // operands are read one step ahead, while the previous step's MFMAs run.
+  auto kloop = [&](auto WC) {
+    constexpr int WS = decltype(WC)::value;  // -1: the wave index at run time
+    const int w = WS >= 0 ? WS : wave;
+    struct Ops {
+      double av, a4, bv[NB];
+    };
+    auto rd = [&](int cur, int k4, Ops& o) {
       const int kr = k4 + (lane >> 4);
-      const double av = a_at(cur, kr, wave * 16 + (lane & 15));
-      const double a4 = a_at(cur, kr, 4 * 16 + (lane & 15));
-      double bv[NB];
+      o.av = a_at(cur, kr, w * 16 + (lane & 15));
+      o.a4 = a_at(cur, kr, 4 * 16 + (lane & 15));
 #pragma unroll
-      for (int b = 0; b < NB; ++b) bv[b] = b_at(cur, kr, b * 16 + (lane & 15));
+      for (int b = 0; b < NB; ++b) o.bv[b] = b_at(cur, kr, b * 16 + (lane & 15));
+    };
+    auto mm = [&](int k4, const Ops& o) {
 #pragma unroll
       for (int b = 0; b < NB; ++b)
-        acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(bv[b], av, acc[b], 0, 0, 0);
-      // block (4, w): B column block w (a wave-uniform index: select, no
-      // dynamic register indexing)
-      double bw = bv[0];
+        acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.bv[b], o.av, acc[b], 0, 0, 0);
+      if constexpr (WS >= 0) {
+        acc4w = __builtin_amdgcn_mfma_f64_16x16x4f64(o.bv[WS], o.a4, acc4w, 0, 0, 0);
+        if (k4 == 4 * WS)  // block (4, 4) on this wave's k4 step
+          acc44 = __builtin_amdgcn_mfma_f64_16x16x4f64(o.bv[4], o.a4, acc44, 0, 0, 0);
+      } else {
+        // block (4, w): B column block w (a wave-uniform index: select, no
+        // dynamic register indexing)
+        double bw = o.bv[0];
 #pragma unroll
-      for (int b = 1; b < 4; ++b) bw = wave == b ? bv[b] : bw;
-      acc4w = __builtin_amdgcn_mfma_f64_16x16x4f64(bw, a4, acc4w, 0, 0, 0);
-      if (k4 == 4 * wave)  // block (4, 4) on this wave's k4 step
-        acc44 = __builtin_amdgcn_mfma_f64_16x16x4f64(bv[4], a4, acc44, 0, 0, 0);
+        for (int b = 1; b < 4; ++b) bw = wave == b ? o.bv[b] : bw;
+        acc4w = __builtin_amdgcn_mfma_f64_16x16x4f64(bw, o.a4, acc4w, 0, 0, 0);
+        if (k4 == 4 * wave)  // block (4, 4) on this wave's k4 step
+          acc44 = __builtin_amdgcn_mfma_f64_16x16x4f64(o.bv[4], o.a4, acc44, 0, 0, 0);
+      }
+    };
+    if (nk > 0) {
+      load(0);
+      store(0, 0);
+      __syncthreads();
     }
-    if (kb + 1 < nk) store(cur ^ 1);
-    __syncthreads();
+    for (int kb = 0; kb < nk; ++kb) {
+      const int cur = kb & 1;
+      if (!ACL_GEMM_OPF && kb + 1 < nk) load((kb + 1) * kGemmKStep);
+      if constexpr (ACL_GEMM_OPF) {
+        // the next step staged in two parts (3 + 2 elements per thread):
+        // the first stored to the other buffer mid-step, the second loaded then
+        const int kn = (kb + 1) * kGemmKStep;
+        const bool more = kb + 1 < nk;
+        if (more) load_part(kn, 0, 3);
+        Ops o0, o1;
+        rd(cur, 0, o0);
+        rd(cur, 4, o1);
+        mm(0, o0);
+        rd(cur, 8, o0);
+        mm(4, o1);
+        if (more) {
+          store_part(cur ^ 1, kn, 0, 3);
+          load_part(kn, 3, EPT);
+        }
+        rd(cur, 12, o1);
+        mm(8, o0);
+        mm(12, o1);
+        if (more) store_part(cur ^ 1, kn, 3, EPT);
+        __syncthreads();
+        continue;
+      } else {
+#pragma unroll
+        for (int k4 = 0; k4 < kGemmKStep; k4 += 4) {
+          Ops o;
+          rd(cur, k4, o);
+          mm(k4, o);
+        }
+      }
+      if (kb + 1 < nk) store(cur ^ 1, (kb + 1) * kGemmKStep);
+      __syncthreads();
+    }
+  };
+  if constexpr (ACL_GEMM_WSPEC) {
+    switch (__builtin_amdgcn_readfirstlane(wave)) {
+      case 0: kloop(GemmWave<0>{}); break;
+      case 1: kloop(GemmWave<1>{}); break;
+      case 2: kloop(GemmWave<2>{}); break;
+      default: kloop(GemmWave<3>{}); break;
+    }
+  } else {
+    kloop(GemmWave<-1>{});
   }
   // (4, 4): the four partial sums through LDS (the A buffer is free), added in
   // wave order

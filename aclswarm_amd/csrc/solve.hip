@@ -202,6 +202,7 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   P.status = a->status; P.u = a->u; P.u_safe = a->u_safe; P.ca_flag = a->ca_flag;
   P.who = a->who; P.align_Rt = a->align_Rt; P.g = a->cntrl; P.s = a->safety;
   P.early_exit = a->early_exit; P.do_control = a->do_control;
+  P.skip_margin = a->skip_margin;
   P.ws = (unsigned char*)a->workspace;
   P.W = ws_layout(n, a->B);
   P.stamps = g_stamps;

@@ -129,8 +129,11 @@ def workspace(n, B, device):
 
 def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
           do_control=True, want_who=False, want_align=False, want_gate_margin=False, out=None,
-          stream=None):
+          stream=None, margin=True):
     """Run acl_solve_batch for B = q.shape[0] swarms. All tensors on device.
+
+    margin=False sets acl_solve_args_t::skip_margin (n <= 128): the status
+    margin is -1 and FRAGILE is never set; everything else is unchanged.
 
     fidx [B] int32, q/vel [B][n][3] f64, P_in [B][n] int16 (uint16 bits).
     Returns a dict of device tensors: P_out, status (raw 16-byte records as
@@ -171,6 +174,7 @@ def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
     a.safety = safety or L.default_safety()
     a.early_exit = int(bool(early_exit))
     a.do_control = int(bool(do_control))
+    a.skip_margin = 0 if margin else 1
     F = table.struct()
     if stream is None:
         stream = torch.cuda.current_stream(dev).cuda_stream

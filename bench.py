@@ -387,6 +387,10 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="time the step (solve + device-side stats) as one captured HIP graph "
                          "replayed per step (launch-bound configurations such as C2; one GPU)")
+    ap.add_argument("--margin", action="store_true",
+                    help="time the headline with the decision margin tracked (default: the "
+                         "reference's work only, acl_solve_args_t::skip_margin; the margin-on "
+                         "rate is measured beside it either way)")
     ap.add_argument("--no-ca-probe", action="store_true",
                     help="skip the crowded (collision-avoidance) probe reported beside the headline")
     ap.add_argument("--dry-run", action="store_true",
@@ -441,72 +445,101 @@ def main():
         "ca_flag": torch.empty((B, n), dtype=torch.uint8, device=dev),
     }
 
-    def solve():
+    def solve(margin):
         engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], early_exit=not args.full_rounds,
-                     out=out, stream=stream.cuda_stream)
+                     out=out, stream=stream.cuda_stream, margin=margin)
 
-    for _ in range(args.warmup):
-        solve()
-        D.gather_results(out["P_out"], out["status"])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
     lib = L.lib()
-    lib.acl_internal_kernel_timing(1)   # HIP events around each launch, on its stream
-    t0 = time.perf_counter()
-    res = None
-    for k in range(args.steps):
-        evs[k][0].record(stream)
-        solve()
-        evs[k][1].record(stream)
-        res = D.gather_results(out["P_out"], out["status"])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.steps
-    call_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    kms = (ctypes.c_double * 3)()
-    kcnt = (ctypes.c_int * 3)()
-    if lib.acl_internal_kernel_times(kms, kcnt) != 0:
-        raise RuntimeError("kernel timing failed")
-    lib.acl_internal_kernel_timing(0)
-    if args.graph and world == 1:
-        # the same step captured once into a HIP graph and replayed: the
-        # per-kernel times above come from the eager pass, the step time from
-        # the replays (no host launch overhead between the step's kernels)
-        gs = torch.cuda.Stream()  # (capture needs a non-default stream)
-        gs.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(gs):  # one eager step on the capture stream first
-            engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], early_exit=not args.full_rounds,
-                         out=out, stream=gs.cuda_stream)
+
+    def timed(margin, ktimes):
+        """W warmup + K timed steps (barrier + synchronize on both sides),
+        the max over ranks; per-launch kernel times when ktimes"""
+        for _ in range(args.warmup):
+            solve(margin)
             D.gather_results(out["P_out"], out["status"])
         torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=gs):
-            engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], early_exit=not args.full_rounds,
-                         out=out, stream=gs.cuda_stream)
-            gres = D.gather_results(out["P_out"], out["status"])
-        with torch.cuda.stream(gs):
-            graph.replay()
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        if ktimes:
+            lib.acl_internal_kernel_timing(1)   # HIP events around each launch, on its stream
         t0 = time.perf_counter()
-        with torch.cuda.stream(gs):
-            for k in range(args.steps):
-                evs[k][0].record(gs)
-                graph.replay()
-                evs[k][1].record(gs)
+        res = None
+        for k in range(args.steps):
+            evs[k][0].record(stream)
+            solve(margin)
+            evs[k][1].record(stream)
+            res = D.gather_results(out["P_out"], out["status"])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.steps
         call_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-        res = gres
-    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    dt_max = float(dt_t.item())
+        kms = (ctypes.c_double * 3)()
+        kcnt = (ctypes.c_int * 3)()
+        if ktimes:
+            if lib.acl_internal_kernel_times(kms, kcnt) != 0:
+                raise RuntimeError("kernel timing failed")
+            lib.acl_internal_kernel_timing(0)
+        if args.graph and world == 1:
+            # the same step captured once into a HIP graph and replayed: the
+            # per-kernel times above come from the eager pass, the step time from
+            # the replays (no host launch overhead between the step's kernels)
+            gs = torch.cuda.Stream()  # (capture needs a non-default stream)
+            gs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(gs):  # one eager step on the capture stream first
+                engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"],
+                             early_exit=not args.full_rounds, out=out, stream=gs.cuda_stream,
+                             margin=margin)
+                D.gather_results(out["P_out"], out["status"])
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=gs):
+                engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"],
+                             early_exit=not args.full_rounds, out=out, stream=gs.cuda_stream,
+                             margin=margin)
+                gres = D.gather_results(out["P_out"], out["status"])
+            with torch.cuda.stream(gs):
+                graph.replay()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            with torch.cuda.stream(gs):
+                for k in range(args.steps):
+                    evs[k][0].record(gs)
+                    graph.replay()
+                    evs[k][1].record(gs)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / args.steps
+            call_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+            res = gres
+        dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+        return float(dt_t.item()), call_ms, kms, kcnt, res
+
+    # the headline: the reference's work (no decision-margin bookkeeping,
+    # skip_margin) unless --margin; then the other mode on the same swarms,
+    # whose margin-on run gives the swarm statistics (fragile counts, min margin)
+    # (the margin-on run last: its outputs stay in `out` for the CPU check)
+    if args.margin:
+        dt_alt, _, _, _, _ = timed(False, False)
+        dt_max, call_ms, kms, kcnt, res = timed(True, True)
+    else:
+        dt_max, call_ms, kms, kcnt, _ = timed(False, True)
+        dt_alt, _, _, _, res = timed(True, False)
+    margin_line = {
+        "headline_tracks_margin": bool(args.margin),
+        "value_margin_on": world * B / (dt_max if args.margin else dt_alt),
+        "value_margin_off": world * B / (dt_alt if args.margin else dt_max),
+        "ms_per_step_margin_on": (dt_max if args.margin else dt_alt) * 1e3,
+        "what": "decision-margin bookkeeping (include/aclswarm_amd.h, a parity diagnostic the "
+                "reference does not compute) on / off (acl_solve_args_t::skip_margin); the same "
+                "assignments, rounds and commands bit for bit (tests/test_gpu_fused.py::"
+                "test_skip_margin_same_outcome); `stats` comes from the margin-on run",
+    }
     stats = D.stats_dict(res[2], res[3])
 
     # collision-avoidance probe: the same swarms crowded (positions scaled by
@@ -523,7 +556,7 @@ def main():
 
         def solve_c():
             engine.solve(T, w["fidx"], qc, w["vel"], w["P_in"], early_exit=not args.full_rounds,
-                         out=outc, stream=stream.cuda_stream)
+                         out=outc, stream=stream.cuda_stream, margin=args.margin)
         solve_c()
         torch.cuda.synchronize()
         lib.acl_internal_kernel_timing(1)
@@ -555,20 +588,21 @@ def main():
     # per-vehicle rows (none here).
     a_all, g_all, s_all, e_avg = algorithmic_bytes(w, 0, B)
     fused = w["planes"] == 5
+    mg = "true" if args.margin else "false"  # the timed kernels' margin template argument
     if fused:
         per_launch = {"auction": a_all + g_all, "gain": 0, "ca": s_all}
-        auction_sym = ("acl_amd::auction_kernel<1, 128, true, false>" if n <= 32 else
-                       "acl_amd::auction_kernel<1, 256, true, false>" if n <= 64 else
-                       "acl_amd::auction_kernel<2, 512, true, false>" if n <= 128 else
+        auction_sym = (f"acl_amd::auction_kernel<1, 128, true, false, {mg}>" if n <= 32 else
+                       f"acl_amd::auction_kernel<1, 256, true, false, {mg}>" if n <= 64 else
+                       f"acl_amd::auction_kernel<2, 512, true, false, {mg}>" if n <= 128 else
                        "acl_amd::solve_wide_kernel<true, false>")
         gain_sym = (f"acl_amd::gain_kernel<{w['planes']}, false>" if n <= 128 else
                     f"acl_amd::gain_kernel<{w['planes']}, false, 1024>")
         align_sym = "acl_amd::align_kernel<2>" if n <= 128 else "acl_amd::align_wide_kernel"
     else:
         per_launch = {"auction": a_all, "gain": g_all, "ca": s_all}
-        auction_sym = (("acl_amd::auction_kernel<1, 128, false, false>" if n <= 32 else
-                        "acl_amd::auction_kernel<1, 256, false, false>" if n <= 64 else
-                        "acl_amd::auction_kernel<2, 512, false, false>") if n <= 128
+        auction_sym = ((f"acl_amd::auction_kernel<1, 128, false, false, {mg}>" if n <= 32 else
+                        f"acl_amd::auction_kernel<1, 256, false, false, {mg}>" if n <= 64 else
+                        f"acl_amd::auction_kernel<2, 512, false, false, {mg}>") if n <= 128
                        else "acl_amd::solve_wide_kernel")
         # n > 128: the control law is the directed walk on 1 024-thread workgroups
         gain_sym = ("acl_amd::gain_pair_kernel<false, false>" if w["planes"] == 5 and n <= 128
@@ -652,6 +686,8 @@ def main():
             "n": n, "B_per_gpu": B, "B_total": world * B,
             "edges_per_formation_avg": e_avg,
             "cbaa": "all 2N rounds" if args.full_rounds else "exact fixed-point exit",
+            "decision_margin": ("tracked" if args.margin else
+                                "not tracked in the timed steps (skip_margin); see `margin`"),
             "parallelism": f"swarm-sharded x{world}",
             "launch": ("one captured HIP graph per step (solve + device-side stats), replayed"
                        if args.graph and world == 1 else "eager launches on one stream"),
@@ -682,6 +718,7 @@ def main():
                     "); the CBAA rounds are issue-port bound (kernels.auction.roofline)",
             "kernels": kern,
         },
+        "margin": margin_line,
         "ca_probe": ca_probe,
         "stats": stats,
         "gen_s": t_gen,

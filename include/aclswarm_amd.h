@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define ACL_ABI_VERSION 6
+#define ACL_ABI_VERSION 7
 
 typedef enum {
   ACL_OK = 0,
@@ -293,6 +293,12 @@ typedef struct {
                           and |e_z| > e_z_thr (distcntrl.cpp:75,80); +inf
                           without edges. The gates themselves are decided on
                           correctly rounded e (the oracle's arithmetic) */
+  int32_t skip_margin; /* ABI 7. 0 (default): status.margin is the decision
+                          margin above. 1 (n <= 128): the auction does not
+                          track it -- status.margin = -1, FRAGILE never set;
+                          assignments, round counts and commands are the same
+                          bits (the margin only observes the comparisons).
+                          n > 128 tracks it either way. */
 } acl_solve_args_t;
 
 /* Largest n acl_solve_batch accepts (512). */

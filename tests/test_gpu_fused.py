@@ -112,3 +112,33 @@ def test_fused_is_deterministic_and_order_free(cuda):
     sample = [0, 5, 17, 47]
     ref = _oracle(pts, adjs, gains, fidx[sample], q[sample], vel[sample], P_in[sample])
     _compare({k: v[sample] for k, v in a.items()}, ref)
+
+
+@pytest.mark.parametrize("n", [20, 100, 129])
+def test_skip_margin_same_outcome(cuda, n):
+    """acl_solve_args_t::skip_margin: the auction without its decision-margin
+    bookkeeping (n <= 128) gives the same tables, assignments, round counts
+    and commands bit for bit; the status margin is -1 and FRAGILE is never
+    set. n > 128 tracks the margin either way."""
+    rng = np.random.RandomState(5100 + n)
+    F, B = 3, 32
+    pts, adjs, gains = _case(rng, n, F, disconnected=True)
+    fidx = np.arange(B) % F
+    q = np.stack([H.dense_positions(rng, n, 2.0 * n) for _ in range(B)])
+    vel = rng.normal(0, 0.3, (B, n, 3))
+    P_in = np.stack([H.random_perm(rng, n) for _ in range(B)])
+    for early in (True, False):
+        a = _gpu_solve(pts, adjs, gains, fidx, q, vel, P_in, early_exit=early)
+        b = _gpu_solve(pts, adjs, gains, fidx, q, vel, P_in, early_exit=early, margin=False)
+        for k in ("P_out", "who", "u", "u_safe", "ca_flag", "gate_margin"):
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+        for k in ("eff_rounds", "rounds", "n_invalid", "n_ca"):
+            np.testing.assert_array_equal(a["status"][k], b["status"][k], err_msg=k)
+        if n <= 128:
+            np.testing.assert_array_equal(a["status"]["flags"] & np.uint32(0xFFFFFFBF), b["status"]["flags"])
+            assert (b["status"]["margin"] == -1.0).all()
+        else:
+            np.testing.assert_array_equal(a["status"]["flags"], b["status"]["flags"])
+            np.testing.assert_array_equal(a["status"]["margin"], b["status"]["margin"])
+    ref = _oracle(pts, adjs, gains, fidx[:6], q[:6], vel[:6], P_in[:6])
+    _compare({k: v[:6] for k, v in a.items()}, ref)

@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
 U_RTOL = 1e-5  # north_star: control commands within 1e-5 relative (fp64)
 
 
-def _gpu_solve(points, adjs, gains, fidx, q, vel, P_in, early_exit=True, do_control=True):
+def _gpu_solve(points, adjs, gains, fidx, q, vel, P_in, early_exit=True, do_control=True,
+               margin=True):
     import torch
     from aclswarm_amd import engine
     dev = torch.device("cuda:0")
@@ -26,7 +27,7 @@ def _gpu_solve(points, adjs, gains, fidx, q, vel, P_in, early_exit=True, do_cont
         torch.from_numpy(np.ascontiguousarray(vel)).to(dev),
         torch.from_numpy(np.asarray(P_in, np.uint16).view(np.int16)).to(dev),
         early_exit=early_exit, do_control=do_control, want_who=True,
-        want_gate_margin=do_control)
+        want_gate_margin=do_control, margin=margin)
     torch.cuda.synchronize()
     res = {k: v.cpu().numpy() for k, v in out.items()}
     res["P_out"] = res["P_out"].view(np.uint16)
