@@ -19,6 +19,8 @@ ap.add_argument("--control", action="store_true", help="run the control kernels 
 ap.add_argument("--crowd", type=float, default=None,
                 help="scale positions about each swarm's centre (bench.py's ca_probe: 0.3)")
 ap.add_argument("--hist", action="store_true", help="print the eff_rounds histogram")
+ap.add_argument("--margin", action="store_true",
+                help="track the decision margin (default: skip_margin, the bench headline's kernel)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 gen = torch.Generator(device=dev)
@@ -29,13 +31,14 @@ if a.crowd is not None:
     w["q"][:, :, :2] = cen + a.crowd * (w["q"][:, :, :2] - cen)
 T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"],
                               w["planes"])
-engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=a.control)  # warm
+engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=a.control, margin=a.margin)  # warm
 torch.cuda.synchronize()
 ms = []
 for _ in range(a.reps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    out = engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=a.control)
+    out = engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=a.control,
+                       margin=a.margin)
     e1.record()
     torch.cuda.synchronize()
     ms.append(e0.elapsed_time(e1))
