@@ -15,8 +15,11 @@ ROOT = os.path.dirname(HERE)
 # C++ facade exerciser (include/aclswarm_amd.hpp), run by tests/test_gpu_facade.py
 DRIVER_SRC = os.path.join(ROOT, "tests", "facade_driver.cpp")
 DRIVER = os.path.join(HERE, "lib", "libfacade_driver.so")
+# the codegen-compatible ADMM entry points driven as aclswarm/src/admm.cpp does
+CG_DRIVER_SRC = os.path.join(ROOT, "tests", "codegen_driver.cpp")
+CG_DRIVER = os.path.join(HERE, "lib", "libcodegen_driver.so")
 SOURCES = ["solve.hip", "auction.hip", "solve_wide.hip", "control.hip", "admm.hip", "hungarian.hip", "episode.hip",
-           "formation_gen.hip", "api.cpp"]
+           "formation_gen.hip", "api.cpp", "codegen_api.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
          "-fPIC", "-shared", "-Wall", "-Wno-unused-function"]
@@ -68,21 +71,29 @@ def _compile_objects(force, verbose, extra=()):
     return objs
 
 
-def build_driver(force=False, verbose=False):
-    """g++ against the library, found next to the binary ($ORIGIN)."""
-    deps = [DRIVER_SRC, OUT, os.path.join(ROOT, "include", "aclswarm_amd.hpp")]
-    if not force and os.path.exists(DRIVER) and all(
-            os.path.getmtime(d) <= os.path.getmtime(DRIVER) for d in deps):
-        return DRIVER
-    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fPIC", "-shared",
-           "-I" + os.path.join(ROOT, "include"), DRIVER_SRC,
-           "-L" + os.path.dirname(OUT), "-laclswarm_amd", "-Wl,-rpath,$ORIGIN",
-           "-o", DRIVER + ".tmp"]
+def _gxx_driver(src, out, incs, deps, force, verbose):
+    if not force and os.path.exists(out) and all(
+            os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
+        return out
+    cmd = (["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fPIC", "-shared"] +
+           ["-I" + i for i in incs] +
+           [src, "-L" + os.path.dirname(OUT), "-laclswarm_amd", "-Wl,-rpath,$ORIGIN",
+            "-o", out + ".tmp"])
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    os.replace(DRIVER + ".tmp", DRIVER)
-    return DRIVER
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build_driver(force=False, verbose=False):
+    """g++ against the library, found next to the binary ($ORIGIN): the C++
+    facade exerciser and the codegen-entry-point driver."""
+    inc = os.path.join(ROOT, "include")
+    _gxx_driver(CG_DRIVER_SRC, CG_DRIVER, [os.path.join(inc, "codegen_admm")],
+                [CG_DRIVER_SRC, OUT, os.path.join(inc, "aclswarm_amd_codegen.h")], force, verbose)
+    return _gxx_driver(DRIVER_SRC, DRIVER, [inc],
+                       [DRIVER_SRC, OUT, os.path.join(inc, "aclswarm_amd.hpp")], force, verbose)
 
 
 def build(force=False, verbose=False):

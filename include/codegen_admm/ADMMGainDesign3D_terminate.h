@@ -1,0 +1,3 @@
+/* ADMMGainDesign3D_terminate.h: forwards to the aclswarm_amd codegen entry points (include/aclswarm_amd_codegen.h) */
+#pragma once
+#include "../aclswarm_amd_codegen.h"

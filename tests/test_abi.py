@@ -196,3 +196,22 @@ def test_gain_planes_detection_and_packing():
     G3[3 * k, 3 * l + 2] = 7.0
     assert engine.gain_planes_host(A, G3) == 5
     assert lib.acl_pack_gains_planes(n, None, None, 7, None) == 1
+
+
+def test_codegen_entry_points_export_and_reject_bad_shapes_without_gpu():
+    """include/aclswarm_amd_codegen.h: the generated library's ADMM entry
+    points with their C++ names (the ones aclswarm/src/admm.cpp links), and a
+    driver built against include/codegen_admm/ (-Werror); a malformed call
+    (Qs 2 x n) leaves an empty result without touching the GPU."""
+    from aclswarm_amd import _lib as L
+    from aclswarm_amd import build
+    lib = L.lib()
+    for sym in ("_Z16ADMMGainDesign3DPK15emxArray_real_TS1_PS_",
+                "_Z27ADMMGainDesign3D_initializev", "_Z26ADMMGainDesign3D_terminatev",
+                "_Z14emxInit_real_TPP15emxArray_real_Ti", "_Z14emxFree_real_TPP15emxArray_real_T",
+                "_Z23emxCreateWrapper_real_TPdii", "_Z22emxDestroyArray_real_TP15emxArray_real_T"):
+        assert hasattr(lib, sym), sym
+    build.build_driver()
+    drv = ct.CDLL(build.CG_DRIVER)
+    assert drv.codegen_bad_call(5) == 0
+    assert b"3 x n" in lib.acl_last_error()
