@@ -1303,6 +1303,22 @@ struct JobLists {
   int NP = 0;
   int njob[J_COUNT] = {};
   int mx[J_COUNT][2] = {};
+  // the kind's operands may be staged by LDS-DMA (gemm_f64.h): no operand
+  // transform, 16-byte aligned operands, even leading dimensions and sizes,
+  // 32-bit byte offsets (checked on the host over every job of the kind)
+  bool dma[J_COUNT] = {};
+  void check_dma(const GemmJob* jobs) {
+    for (int k = 0; k < J_COUNT; ++k) {
+      bool ok = njob[k] > 0;
+      for (int i = 0; ok && i < njob[k]; ++i) {
+        const GemmJob& j = jobs[(size_t)k * NP + i];
+        const uintptr_t al = (uintptr_t)j.A | (uintptr_t)j.B | (uintptr_t)j.qB;
+        ok = j.tmask == 0 && (al & 15) == 0 && ((j.lda | j.ldb | j.m | j.k) & 1) == 0 &&
+             (long long)j.lda * j.k * 8 < (1ll << 30) && (long long)j.ldb * j.n * 8 < (1ll << 30);
+      }
+      dma[k] = ok;
+    }
+  }
   // symmetric products (exact arithmetic): G = Q Q^T, the Newton-Schulz
   // Z^2 and Z Z^2 (polynomials in one symmetric Z commute), W sign(W)
   static bool sym(int kind) {
@@ -1312,7 +1328,7 @@ struct JobLists {
   }
   hipError_t run(int kind, bool ta, bool tb, hipStream_t st) const {
     return gemm_f64(ta, tb, dj + (size_t)kind * NP, njob[kind], mx[kind][0], mx[kind][1], st,
-                    g_flops, sym(kind) && mx[kind][0] == mx[kind][1]);
+                    g_flops, sym(kind) && mx[kind][0] == mx[kind][1], dma[kind]);
   }
 };
 
@@ -1617,6 +1633,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     ACL_HIP(hipMemcpyAsync(dp, hp.data(), NP * sizeof(Part), hipMemcpyHostToDevice, st),
             "hipMemcpyAsync");
     JL.dj = dj;
+    JL.check_dma(jobs.data());
     auto gemm = [&](int kind, bool ta, bool tb) -> hipError_t { return JL.run(kind, ta, tb, st); };
     int max_s = 0, max_np = 0, maxK1 = 1;
     for (const Info& in : info) {

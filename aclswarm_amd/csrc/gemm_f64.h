@@ -71,6 +71,9 @@ struct GemmJob {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
+// 16 zero bytes: the source of the LDS-DMA lanes outside an operand
+__device__ __attribute__((aligned(16))) double g_gemm_zero16[2];
+
 template <int W>
 struct GemmWave {  // a wave index as a type (per-wave specialised code)
   static constexpr int value = W;
@@ -82,6 +85,12 @@ constexpr int kGemmKStep = 16;
 #endif
 #ifndef ACL_GEMM_OPF
 #define ACL_GEMM_OPF 1  // LDS operands read one k4 step ahead
+#endif
+#ifndef ACL_GEMM_DMA
+#define ACL_GEMM_DMA 1  // untransposed products staged by LDS-DMA where the host allows
+#endif
+#ifndef ACL_GEMM_DMA_WAVES
+#define ACL_GEMM_DMA_WAVES 3  // the 80-tile kernel's occupancy bound (waves per SIMD)
 #endif
 #ifndef ACL_GEMM_TILE_DEFAULT
 #define ACL_GEMM_TILE_DEFAULT 80  // the four-wave 80 tile
@@ -351,10 +360,10 @@ __global__ void __launch_bounds__(320) gemm80_f64_kernel(const GemmJob* __restri
 // its own k4 step (k4 = w in every K step of 16): 25 MFMAs per wave per K
 // step. The four partial (4, 4) accumulators are summed through LDS in wave
 // order after the K loop.
-template <bool TA, bool TB, bool SYM>
-__global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __restrict__ jobs,
-                                                            int njobs, int tm, int tiles,
-                                                            unsigned long long* flops) {
+template <bool TA, bool TB, bool SYM, bool DMA = false>
+__global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
+    const GemmJob* __restrict__ jobs, int njobs, int tm, int tiles, unsigned long long* flops) {
+  static_assert(!DMA || (!TA && !TB), "LDS-DMA staging: A and B untransposed only");
   constexpr int TILE = 80, NB = 5, EPT = 5;  // 80 x 16 operands / 256 threads = 5
   const int blk = blockIdx.x;
   const int slot = blk >> 3;
@@ -404,13 +413,17 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
   }
   constexpr bool AT = TA, BT = !TB;  // staged i-major (k contiguous in memory)
   constexpr int KM = TILE, IM = 18;
-  constexpr int SZ = TILE * IM;
-  __shared__ double Ash[2][SZ];
-  __shared__ double Bsh[2][SZ];
+  // DMA: dense images, A k-major [16][80], B as [80 columns][8 k-pairs] with
+  // the pair slot xor-swizzled by the column, (kp ^ ((j >> 1) & 7)): the MFMA
+  // reads (16 columns x 2 k of one pair per half-wave) hit 64 distinct banks
+  constexpr int SZ = DMA ? TILE * kGemmKStep : TILE * IM;
+  __shared__ __attribute__((aligned(16))) double Ash[2][SZ];
+  __shared__ __attribute__((aligned(16))) double Bsh[2][SZ];
   auto a_at = [&](int buf, int kk, int i) -> double& {
     return AT ? Ash[buf][i * IM + kk] : Ash[buf][kk * KM + i];
   };
   auto b_at = [&](int buf, int kk, int j) -> double& {
+    if constexpr (DMA) return Bsh[buf][2 * (j * 8 + ((kk >> 1) ^ ((j >> 1) & 7))) + (kk & 1)];
     return BT ? Bsh[buf][j * IM + kk] : Bsh[buf][kk * KM + j];
   };
   const int tid = threadIdx.x;
@@ -475,6 +488,61 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
   };
   auto load = [&](int k0) { load_part(k0, 0, EPT); };
   auto store = [&](int buf, int k0) { store_part(buf, k0, 0, EPT); };
+  // LDS-DMA staging (DMA): a K step's operands are 20 pieces of 1 KiB (A:
+  // 10 x 64 lanes x one pair of rows of one k; B: 10 x 64 lanes x one k-pair
+  // of one column), wave w issuing pieces w + 4t, t < 5, as global_load_lds
+  // (16 bytes per lane straight into LDS: no registers, no VALU beyond the
+  // addresses). A lane outside the matrix (rows >= m, columns >= n, k >= K)
+  // reads a 16-byte zero block instead. The loads are inline asm: the
+  // compiler would otherwise wait for them before every LDS read (it cannot
+  // tell the buffers apart); the K loop waits for them itself, before the
+  // barrier that publishes a step's buffer.
+  unsigned doff[5];
+  int dkk[5];
+  if constexpr (DMA) {
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const int q = wv + 4 * t;
+      if (q < 10) {
+        const int u = q * 64 + lane, k = u / 40, row = m0 + 2 * (u % 40);
+        doff[t] = (unsigned)(row + k * J.lda) * 8u;
+        dkk[t] = row < J.m ? k : (1 << 28);
+      } else {
+        const int P = (q - 10) * 64 + lane, j = P >> 3, kp = (P & 7) ^ ((j >> 1) & 7);
+        const int col = n0 + j;
+        doff[t] = (unsigned)(2 * kp + col * J.ldb) * 8u;
+        dkk[t] = col < J.n ? 2 * kp : (1 << 28);
+      }
+    }
+  }
+  auto dma = [&](int buf, int k0) {
+    if constexpr (DMA) {
+      const int wv = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const int q = wv + 4 * t;
+        const bool isA = q < 10;  // wave-uniform
+        const char* base = (const char*)(isA ? J.A : J.B);
+        const unsigned step = isA ? (unsigned)(k0 * J.lda) * 8u : (unsigned)k0 * 8u;
+        const void* src = k0 + dkk[t] < J.k ? (const void*)(base + doff[t] + step)
+                                            : (const void*)g_gemm_zero16;
+        const double* dst = isA ? &Ash[buf][q * 128] : &Bsh[buf][(q - 10) * 128];
+        const unsigned lds = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) double*)dst;
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(src), "s"(lds)
+            : "memory");
+      }
+    }
+  };
+  // the DMA K loop's wait: this wave's pieces have landed in LDS
+  auto dma_wait = [&]() {
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
   const int nk = (J.k + kGemmKStep - 1) / kGemmKStep;
   // alpha, beta of the epilogue (the scaled Newton-Schulz update, the
   // quintic band)
@@ -541,14 +609,7 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
       f64x4 dacc[NQ];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) dacc[q] = f64x4{0.0, 0.0, 0.0, 0.0};
-      if (nk > 0) {
-        load(0);
-        store(0, 0);
-        __syncthreads();
-      }
-      for (int kb = 0; kb < nk; ++kb) {
-        const int cur = kb & 1;
-        if (kb + 1 < nk) load((kb + 1) * kGemmKStep);
+      auto dstep = [&](int cur) {
 #pragma unroll
         for (int k4 = 0; k4 < kGemmKStep; k4 += 4) {
           const int kr = k4 + (lane >> 4);
@@ -558,8 +619,30 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
                                                           a_at(cur, kr, RB[W][q] * 16 + (lane & 15)),
                                                           dacc[q], 0, 0, 0);
         }
-        if (kb + 1 < nk) store(cur ^ 1, (kb + 1) * kGemmKStep);
+      };
+      if constexpr (DMA) {
+        if (nk > 0) dma(0, 0);
+        for (int kb = 0; kb < nk; ++kb) {
+          const int cur = kb & 1;
+          dma_wait();
+          __syncthreads();  // step kb's pieces landed; step kb - 1's buffer free
+          if (kb + 1 < nk) dma(cur ^ 1, (kb + 1) * kGemmKStep);
+          dstep(cur);
+        }
         __syncthreads();
+      } else {
+        if (nk > 0) {
+          load(0);
+          store(0, 0);
+          __syncthreads();
+        }
+        for (int kb = 0; kb < nk; ++kb) {
+          const int cur = kb & 1;
+          if (kb + 1 < nk) load((kb + 1) * kGemmKStep);
+          dstep(cur);
+          if (kb + 1 < nk) store(cur ^ 1, (kb + 1) * kGemmKStep);
+          __syncthreads();
+        }
       }
       double alpha, beta;
       scales(alpha, beta);
@@ -618,6 +701,26 @@ __global__ void __launch_bounds__(256, 3) gemm80w4_f64_kernel(const GemmJob* __r
           acc44 = __builtin_amdgcn_mfma_f64_16x16x4f64(o.bv[4], o.a4, acc44, 0, 0, 0);
       }
     };
+    if constexpr (DMA) {
+      if (nk > 0) dma(0, 0);
+      for (int kb = 0; kb < nk; ++kb) {
+        const int cur = kb & 1;
+        dma_wait();
+        __syncthreads();  // step kb's pieces landed; step kb - 1's buffer free
+        if (kb + 1 < nk) dma(cur ^ 1, (kb + 1) * kGemmKStep);
+        Ops o0, o1;
+        rd(cur, 0, o0);
+        rd(cur, 4, o1);
+        mm(0, o0);
+        rd(cur, 8, o0);
+        mm(4, o1);
+        rd(cur, 12, o1);
+        mm(8, o0);
+        mm(12, o1);
+      }
+      __syncthreads();
+      return;
+    }
     if (nk > 0) {
       load(0);
       store(0, 0);
@@ -718,7 +821,8 @@ constexpr int gemm_tile_size() { return gemm_tile() == 85 ? 80 : gemm_tile(); }
 // are bounded by mmax, nmax. sym: every job's D is symmetric in exact
 // arithmetic (and square): upper-triangle tiles only, mirrored.
 inline hipError_t gemm_f64(bool ta, bool tb, const GemmJob* jobs, int njobs, int mmax, int nmax,
-                           hipStream_t s, unsigned long long* flops = nullptr, bool sym = false) {
+                           hipStream_t s, unsigned long long* flops = nullptr, bool sym = false,
+                           bool dma = false) {
   if (njobs <= 0 || mmax <= 0 || nmax <= 0) return hipSuccess;
   const int TT = gemm_tile(), T = TT == 85 ? 80 : TT;
   const int tm = (mmax + T - 1) / T, tn = (nmax + T - 1) / T;
@@ -727,7 +831,10 @@ inline hipError_t gemm_f64(bool ta, bool tb, const GemmJob* jobs, int njobs, int
   const dim3 grid(8 * ((njobs + 7) / 8) * tiles);
 #define ACL_GEMM_LAUNCH2(TA_, TB_, SYM_)                                                   \
   do {                                                                                     \
-    if (TT == 80)                                                                          \
+    if (TT == 80 && ACL_GEMM_DMA && dma && !TA_ && !TB_)                                   \
+      hipLaunchKernelGGL((gemm80w4_f64_kernel<false, false, SYM_, true>), grid, dim3(256), 0, s, \
+                         jobs, njobs, tm, tiles, flops);                                   \
+    else if (TT == 80)                                                                     \
       hipLaunchKernelGGL((gemm80w4_f64_kernel<TA_, TB_, SYM_>), grid, dim3(256), 0, s, jobs, \
                          njobs, tm, tiles, flops);                                         \
     else if (TT == 85)                                                                     \

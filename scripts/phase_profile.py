@@ -32,6 +32,8 @@ ap.add_argument("--formations", type=int, default=0)
 ap.add_argument("--L", type=float, default=None)
 ap.add_argument("--crowd", type=float, default=None,
                 help="scale positions about each swarm's centre (collision avoidance active)")
+ap.add_argument("--margin", action="store_true",
+                help="track the decision margin (default: skip_margin, the bench headline's kernel)")
 ap.add_argument("--no-control", action="store_true",
                 help="auction only (the PROF build's CBAA section counters are not overwritten "
                      "by the collision-avoidance kernel's)")
@@ -52,10 +54,10 @@ lib.acl_internal_set_stamps.argtypes = [ct.c_void_p]
 SS, RT0, RT1, SEC = 32, 8, 9, 16  # csrc/control_params.h kStamp*
 st = torch.zeros((args.B, SS), dtype=torch.int64, device=dev)
 ctl = not args.no_control
-engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=ctl)  # warm
+engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=ctl, margin=args.margin)  # warm
 torch.cuda.synchronize()
 lib.acl_internal_set_stamps(ct.c_void_p(st.data_ptr()))
-engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=ctl)
+engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], do_control=ctl, margin=args.margin)
 torch.cuda.synchronize()
 lib.acl_internal_set_stamps(ct.c_void_p(0))
 s = st.cpu().numpy().astype(np.float64)

@@ -26,7 +26,9 @@ def _driver():
 
 
 @pytest.mark.parametrize("k", range(0, len(CASES), max(1, len(CASES) // 6)))
-def test_codegen_entry_point_equals_batched_design(k):
+def test_codegen_entry_point_equals_batched_design(cuda, k):
+    # (`cuda` first: torch brings its own HIP runtime, which must be the
+    # process's first to initialise the device; the library then shares it)
     c = CASES[k]
     p = np.ascontiguousarray(c["p"], dtype=np.float64)
     n = p.shape[0]
