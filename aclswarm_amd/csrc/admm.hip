@@ -1303,8 +1303,8 @@ struct JobLists {
   int NP = 0;
   int njob[J_COUNT] = {};
   int mx[J_COUNT][2] = {};
-  // the kind's operands may be staged by LDS-DMA (gemm_f64.h): no operand
-  // transform, 16-byte aligned operands, even leading dimensions and sizes,
+  // the kind's operands may be staged by LDS-DMA (gemm_f64.h): 16-byte
+  // aligned operands, even leading dimensions and sizes,
   // 32-bit byte offsets (checked on the host over every job of the kind)
   bool dma[J_COUNT] = {};
   void check_dma(const GemmJob* jobs) {
@@ -1313,7 +1313,7 @@ struct JobLists {
       for (int i = 0; ok && i < njob[k]; ++i) {
         const GemmJob& j = jobs[(size_t)k * NP + i];
         const uintptr_t al = (uintptr_t)j.A | (uintptr_t)j.B | (uintptr_t)j.qB;
-        ok = j.tmask == 0 && (al & 15) == 0 && ((j.lda | j.ldb | j.m | j.k) & 1) == 0 &&
+        ok = (j.tmask & ~7) == 0 && (al & 15) == 0 && ((j.lda | j.ldb | j.m | j.k) & 1) == 0 &&
              (long long)j.lda * j.k * 8 < (1ll << 30) && (long long)j.ldb * j.n * 8 < (1ll << 30);
       }
       dma[k] = ok;

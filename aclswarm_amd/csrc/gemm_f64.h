@@ -539,9 +539,36 @@ __global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
       }
     }
   };
-  // the DMA K loop's wait: this wave's pieces have landed in LDS
-  auto dma_wait = [&]() {
-    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the DMA K loop's wait: this wave's pieces have landed in LDS; for a job
+  // with an operand transform (tmask: the Newton-Schulz start) each lane then
+  // applies it to its own landed 16 bytes, as store_part does to a staged
+  // element (the same expression: the same bits), before the barrier that
+  // publishes the buffer
+  auto dma_wait = [&](int buf, int k0) {
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tmask & 3) {  // workgroup-uniform
+        const int wv = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+          const int q = wv + 4 * t;
+          const bool isA = q < 10;
+          if (!(tmask & (isA ? 1 : 2)) || !(k0 + dkk[t] < J.k)) continue;
+          double* e = (isA ? &Ash[buf][q * 128] : &Bsh[buf][(q - 10) * 128]) + 2 * lane;
+          int gi0, gk0, di, dk;  // element 0's (row, k); element 1 steps by (di, dk)
+          if (isA) {
+            const int u = q * 64 + lane;
+            gi0 = m0 + 2 * (u % 40); gk0 = k0 + u / 40; di = 1; dk = 0;
+          } else {
+            const int P = (q - 10) * 64 + lane, j = P >> 3;
+            gi0 = n0 + j; gk0 = k0 + dkk[t]; di = 0; dk = 1;
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            e[h] = (e[h] - (gi0 + h * di == gk0 + h * dk ? tdiag : 0.0)) * tinv;
+        }
+      }
+    }
   };
   const int nk = (J.k + kGemmKStep - 1) / kGemmKStep;
   // alpha, beta of the epilogue (the scaled Newton-Schulz update, the
@@ -624,7 +651,7 @@ __global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
         if (nk > 0) dma(0, 0);
         for (int kb = 0; kb < nk; ++kb) {
           const int cur = kb & 1;
-          dma_wait();
+          dma_wait(cur, kb * kGemmKStep);
           __syncthreads();  // step kb's pieces landed; step kb - 1's buffer free
           if (kb + 1 < nk) dma(cur ^ 1, (kb + 1) * kGemmKStep);
           dstep(cur);
@@ -705,7 +732,7 @@ __global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
       if (nk > 0) dma(0, 0);
       for (int kb = 0; kb < nk; ++kb) {
         const int cur = kb & 1;
-        dma_wait();
+        dma_wait(cur, kb * kGemmKStep);
         __syncthreads();  // step kb's pieces landed; step kb - 1's buffer free
         if (kb + 1 < nk) dma(cur ^ 1, (kb + 1) * kGemmKStep);
         Ops o0, o1;
