@@ -397,6 +397,7 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
   sa.B = B; sa.fidx = a->fidx; sa.q = a->q; sa.vel = a->vel; sa.P_in = seed; sa.P_out = Pnew;
   sa.status = st; sa.workspace = ws + W.solve;
   sa.cntrl = a->cntrl; sa.safety = a->safety; sa.early_exit = 1; sa.do_control = 0;
+  sa.skip_margin = 1;  // the episode reads assignments and flags, never the decision margin
   acl_control_args_t cs = {};
   cs.B = B; cs.fidx = a->fidx; cs.q = a->q; cs.vel = a->vel; cs.P = a->P;
   cs.u = u; cs.u_safe = us; cs.ca_flag = ca;
