@@ -922,6 +922,20 @@ __global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
 // n - 1 <= 127), so the LDS image stays bounded.
 constexpr int kCaPairCap = 1024;
 constexpr int kCaPT = 256;
+// diagnostic builds only (-DACL_CA_DIAG_FASTTRIG: wrong results): the pair
+// kernel's atan2 / asin / cos / sin in f32, to bound what the f64 library
+// calls cost
+#ifdef ACL_CA_DIAG_FASTTRIG
+#define CA_ATAN2(y, x) ((double)atan2f((float)(y), (float)(x)))
+#define CA_ASIN(x) ((double)asinf((float)(x)))
+#define CA_COS(x) ((double)cosf((float)(x)))
+#define CA_SIN(x) ((double)sinf((float)(x)))
+#else
+#define CA_ATAN2(y, x) atan2(y, x)
+#define CA_ASIN(x) asin(x)
+#define CA_COS(x) cos(x)
+#define CA_SIN(x) sin(x)
+#endif
 
 struct CaPairLayout {
   int q, cl, cmd, psi, cnt, off, wr, flg, edge, cmk, lists, pairs, ang, sA, sS, tA, tS, misc,
@@ -1078,7 +1092,7 @@ __global__ void __launch_bounds__(kCaPT, 4) ca_pair_kernel(const CtlParams P) {
       double c0 = gu[0], c1 = gu[1], c2 = gu[2];
       saturate(sp, c0, c1, c2);
       cmd[3 * k] = c0; cmd[3 * k + 1] = c1; cmd[3 * k + 2] = c2;
-      psiv[k] = atan2(c1, c0);
+      psiv[k] = CA_ATAN2(c1, c0);
       wr[k] = 0;
       flg[k] = 0;
     }
@@ -1145,9 +1159,9 @@ __global__ void __launch_bounds__(kCaPT, 4) ca_pair_kernel(const CtlParams P) {
         const int v = cl[k];
         const double dx = q[3 * j] - q[3 * v], dy = q[3 * j + 1] - q[3 * v + 1];
         const double dd = sqrt(dx * dx + dy * dy);
-        const double theta = atan2(dy, dx);
+        const double theta = CA_ATAN2(dy, dx);
         const double x = sp.r_keep_out / dd;
-        const double alpha = fabs(asin(x < 1.0 ? x : 1.0));
+        const double alpha = fabs(CA_ASIN(x < 1.0 ? x : 1.0));
         const double beg = wrap_to_pi(theta - alpha);
         const double end = wrap_to_pi(theta + alpha);
         ang[2 * p] = beg;
@@ -1250,8 +1264,8 @@ __global__ void __launch_bounds__(kCaPT, 4) ca_pair_kernel(const CtlParams P) {
         if (res == 1) {
           const double edge = edg[k];
           const double umag = sqrt(c0 * c0 + c1 * c1);
-          c0 = umag * cos(edge);
-          c1 = umag * sin(edge);
+          c0 = umag * CA_COS(edge);
+          c1 = umag * CA_SIN(edge);
         } else if (res == 2) {
           c0 = c1 = 0.0;
           c2 = 0.0;
