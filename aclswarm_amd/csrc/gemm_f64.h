@@ -19,7 +19,9 @@
 // per SIMD, 25 MFMA 16x16 blocks split evenly over the four waves
 // (gemm80w4_f64_kernel); alternatives 64 x 64 / 32 x 32 (four waves in a 2 x 2
 // arrangement) and the 80 tile on five waves. K staged through LDS in steps of
-// 16 with a register-prefetched double buffer (one barrier per step).
+// 16, double-buffered, one barrier per step: untransposed jobs the host
+// marks eligible by LDS-DMA (global_load_lds, no staging registers: four
+// waves per SIMD), the others through a register prefetch (three).
 // The MFMA is issued with the operands swapped (it computes the tile of D^T),
 // so the accumulator's lane index runs along D's rows and every epilogue
 // load/store is a contiguous 128-byte column segment.
