@@ -1326,9 +1326,9 @@ struct JobLists {
            kind == J_NSU1 || kind == J_S || kind == J_S1 || kind == J_NSYF || kind == J_NSUF ||
            kind == J_NST;
   }
-  hipError_t run(int kind, bool ta, bool tb, hipStream_t st, const int* gate = nullptr) const {
+  hipError_t run(int kind, bool ta, bool tb, hipStream_t st) const {
     return gemm_f64(ta, tb, dj + (size_t)kind * NP, njob[kind], mx[kind][0], mx[kind][1], st,
-                    g_flops, sym(kind) && mx[kind][0] == mx[kind][1], dma[kind], gate);
+                    g_flops, sym(kind) && mx[kind][0] == mx[kind][1], dma[kind]);
   }
 };
 
@@ -1403,18 +1403,15 @@ hipError_t psd_project(const JobLists& J, Part* dp, int NP, int n2max, double ep
   for (int it = 0; it < kNsMax; ++it) {
     const bool odd = it & 1;
     const bool first = tr && it == 0;
-    // from the second step on, the last step's count of parts still
-    // iterating (nsstep_kernel) ends the launches at once when it is 0
-    const int* gate = it > 0 ? X.d_cnt : nullptr;
-    if ((e = J.run(first ? J_NSYF : (odd ? J_NSY1 : J_NSY0), false, false, st, gate)) != hipSuccess)
+    if ((e = J.run(first ? J_NSYF : (odd ? J_NSY1 : J_NSY0), false, false, st)) != hipSuccess)
       return e;
     if (!fuse_err)
       hipLaunchKernelGGL(nserr_kernel, dim3(std::min(grid1((long long)n2max * n2max), 64), NP),
                          dim3(kT), 0, st, dp);
     // the quintic band's T (no jobs unless add_sign_jobs made them; each
     // gated on its part's check)
-    if ((e = J.run(J_NST, false, false, st, gate)) != hipSuccess) return e;
-    if ((e = J.run(first ? J_NSUF : (odd ? J_NSU1 : J_NSU0), false, false, st, gate)) != hipSuccess)
+    if ((e = J.run(J_NST, false, false, st)) != hipSuccess) return e;
+    if ((e = J.run(first ? J_NSUF : (odd ? J_NSU1 : J_NSU0), false, false, st)) != hipSuccess)
       return e;
     hipLaunchKernelGGL(nsstep_kernel, dim3(1), dim3(1024), 0, st, dp, NP,
                        it == kNsMax - 1 ? 1 : 0, tol, X.d_cnt);

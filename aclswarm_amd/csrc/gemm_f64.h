@@ -364,13 +364,9 @@ __global__ void __launch_bounds__(320) gemm80_f64_kernel(const GemmJob* __restri
 // order after the K loop.
 template <bool TA, bool TB, bool SYM, bool DMA = false>
 __global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
-    const GemmJob* __restrict__ jobs, int njobs, int tm, int tiles, unsigned long long* flops,
-    const int* gate) {
+    const GemmJob* __restrict__ jobs, int njobs, int tm, int tiles, unsigned long long* flops) {
   static_assert(!DMA || (!TA && !TB), "LDS-DMA staging: A and B untransposed only");
   constexpr int TILE = 80, NB = 5, EPT = 5;  // 80 x 16 operands / 256 threads = 5
-  // gate (optional): a count of jobs still to run (the Newton-Schulz
-  // iteration's parts left); 0 ends every workgroup at its first load
-  if (gate && *gate == 0) return;
   const int blk = blockIdx.x;
   const int slot = blk >> 3;
   const int job = (blk & 7) + 8 * (slot / tiles);
@@ -855,7 +851,7 @@ constexpr int gemm_tile_size() { return gemm_tile() == 85 ? 80 : gemm_tile(); }
 // arithmetic (and square): upper-triangle tiles only, mirrored.
 inline hipError_t gemm_f64(bool ta, bool tb, const GemmJob* jobs, int njobs, int mmax, int nmax,
                            hipStream_t s, unsigned long long* flops = nullptr, bool sym = false,
-                           bool dma = false, const int* gate = nullptr) {
+                           bool dma = false) {
   if (njobs <= 0 || mmax <= 0 || nmax <= 0) return hipSuccess;
   const int TT = gemm_tile(), T = TT == 85 ? 80 : TT;
   const int tm = (mmax + T - 1) / T, tn = (nmax + T - 1) / T;
@@ -866,10 +862,10 @@ inline hipError_t gemm_f64(bool ta, bool tb, const GemmJob* jobs, int njobs, int
   do {                                                                                     \
     if (TT == 80 && ACL_GEMM_DMA && dma && !TA_ && !TB_)                                   \
       hipLaunchKernelGGL((gemm80w4_f64_kernel<false, false, SYM_, true>), grid, dim3(256), 0, s, \
-                         jobs, njobs, tm, tiles, flops, gate);                             \
+                         jobs, njobs, tm, tiles, flops);                                   \
     else if (TT == 80)                                                                     \
       hipLaunchKernelGGL((gemm80w4_f64_kernel<TA_, TB_, SYM_>), grid, dim3(256), 0, s, jobs, \
-                         njobs, tm, tiles, flops, gate);                                   \
+                         njobs, tm, tiles, flops);                                         \
     else if (TT == 85)                                                                     \
       hipLaunchKernelGGL((gemm80_f64_kernel<TA_, TB_, SYM_>), grid, dim3(320), 0, s, jobs,  \
                          njobs, tm, tiles, flops);                                         \
