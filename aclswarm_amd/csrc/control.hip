@@ -1033,7 +1033,10 @@ __device__ __forceinline__ int ca_resolve_seg(int lane, int m, double a, int sg,
   return fabs(wrap_to_pi(edge - psi)) <= kPi / 2 ? 1 : 2;
 }
 
-__global__ void __launch_bounds__(kCaPT, 4) ca_pair_kernel(const CtlParams P) {
+#ifndef ACL_CA_OCC
+#define ACL_CA_OCC 4  // ca_pair_kernel's occupancy bound (waves per SIMD)
+#endif
+__global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const int NW = (n + 63) >> 6;
