@@ -531,7 +531,8 @@ def main():
         dt_max, call_ms, kms, kcnt, _ = timed(False, True)
         dt_alt, _, _, _, res = timed(True, False)
     margin_line = {
-        "headline_tracks_margin": bool(args.margin),
+        # (n > 128: the wide kernel tracks the margin either way)
+        "headline_tracks_margin": bool(args.margin) or n > 128,
         "value_margin_on": world * B / (dt_max if args.margin else dt_alt),
         "value_margin_off": world * B / (dt_alt if args.margin else dt_max),
         "ms_per_step_margin_on": (dt_max if args.margin else dt_alt) * 1e3,
@@ -686,7 +687,7 @@ def main():
             "n": n, "B_per_gpu": B, "B_total": world * B,
             "edges_per_formation_avg": e_avg,
             "cbaa": "all 2N rounds" if args.full_rounds else "exact fixed-point exit",
-            "decision_margin": ("tracked" if args.margin else
+            "decision_margin": ("tracked" if args.margin or n > 128 else
                                 "not tracked in the timed steps (skip_margin); see `margin`"),
             "parallelism": f"swarm-sharded x{world}",
             "launch": ("one captured HIP graph per step (solve + device-side stats), replayed"
