@@ -203,6 +203,7 @@ struct WTable {
   }
 };
 
+template <bool MG>
 __device__ int wide_select(int n, int NW, int v, int lane, const WPrice& price,
                            const uint16_t* T, const uint16_t* ccw, const float* ccp,
                            const WTable& tab, bool fresh, MarginPair& m) {
@@ -282,8 +283,9 @@ __device__ int wide_select(int n, int NW, int v, int lane, const WPrice& price,
     const bool elig = other[c] && !isjs && key[c] != 0u;
     const bool near = other[c] && !isjs && key[c] == 0u && cvs[c] > 0.0f &&
                       (js < 0 || cvs[c] > cmax || (cvs[c] == cmax && j < js));
-    margin_track_sel(m, isjs ? cvs[c] : (elig ? cmax : prs[c]), isjs ? prs[c] : cvs[c],
-                     isjs || elig || near);
+    if (MG)
+      margin_track_sel(m, isjs ? cvs[c] : (elig ? cmax : prs[c]), isjs ? prs[c] : cvs[c],
+                       isjs || elig || near);
   }
   return js;
 }
@@ -737,7 +739,10 @@ __global__ void __launch_bounds__(kWABlock, 2) align_wide_kernel(const SolvePara
 #endif
 typedef const __attribute__((address_space(4))) SolveParams KSolveParams;
 
-template <bool FUSE, bool GM>
+// MG false (acl_solve_args_t::skip_margin): no decision margin -- the level
+// walk stops once every vehicle has its winning level (the runner-up levels
+// only bound the margin), the selects and scans track nothing
+template <bool FUSE, bool GM, bool MG>
 __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParams P_) {
 #if ACL_WIDE_KARG
   KSolveParams* Pk = (KSolveParams*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -895,7 +900,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     atomicAnd(&unif[task >> 6], ~(1ull << (task & 63)));
   };
   for (int v = wave; v < n; v += kWWaves) {
-    const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, tab, true, mp);
+    const int task = wide_select<MG>(n, NW, v, lane, price, T, ccw, ccp, tab, true, mp);
     if (task >= 0 && lane == 0) place_bid(v, task, 0);  // round 1 (parity 1) reads list 0
   }
   __syncthreads();
@@ -1045,7 +1050,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           // hit: the vehicle's closed neighbourhood holds a vehicle of this
           // level; holder-word outer loop, so the vehicle words' LDS loads
           // issue together, stopping once every active vehicle is hit
-          const unsigned actm = ~(s2m | needm) & ((1u << kWMaxW) - 1u);
+          // (MG false: done at the winner; s2m then only marks the lanes past n)
+          const unsigned actm = ~((MG ? s2m : (s1m | s2m)) | needm) & ((1u << kWMaxW) - 1u);
           unsigned hitm = 0u;
 #pragma unroll
           for (int w2 = 0; w2 < kWMaxW; ++w2) {
@@ -1076,7 +1082,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           s1m |= first;
           s2m |= second;
           if (tk) needm |= first;
-          const bool open = (~(s2m | needm) & ((1u << kWMaxW) - 1u)) != 0u;
+          const bool open = (~((MG ? s2m : (s1m | s2m)) | needm) & ((1u << kWMaxW) - 1u)) != 0u;
           if (__ballot(open) == 0ull) break;
           cap = Mk;
         }
@@ -1084,12 +1090,14 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
         WPROF_ADD(pf_clvl, pl - pk);
         // undecided, or the runner-up level not found before the level cap
         needm |= ~(s1m | s2m) & ((1u << kWMaxW) - 1u);
-        if (!exhausted) needm |= s1m & ~s2m;
-        const unsigned donem = s2m & ~needm;
+        if (MG && !exhausted) needm |= s1m & ~s2m;
+        if (MG) {
+          const unsigned donem = s2m & ~needm;
 #pragma unroll
-        for (int c = 0; c < kWMaxW; ++c)
-          if (((donem >> c) & 1u) && k2[c] != 0u)
-            margin_track(mp, __uint_as_float(k1[c] - 1u), __uint_as_float(k2[c] - 1u));
+          for (int c = 0; c < kWMaxW; ++c)
+            if (((donem >> c) & 1u) && k2[c] != 0u)
+              margin_track(mp, __uint_as_float(k1[c] - 1u), __uint_as_float(k2[c] - 1u));
+        }
         WPROF_T(ps0);
         bool tvalid = !spj;  // T holds the column's entries (before this update)
         if (__ballot(needm != 0u) != 0ull) {
@@ -1132,7 +1140,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
                 }
               }
               nw[c] = bw;
-              if (have2) margin_track(mp, bp, p2);
+              if (MG && have2) margin_track(mp, bp, p2);
             }
           }
         }
@@ -1255,7 +1263,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
           const int v = kth_bit(obm + par * NW, NW, tk);
           WPROF_T(pr0);
           WPROF_ADD(pf_cnt, 1ull << 42);
-          const int task = wide_select(n, NW, v, lane, price, T, ccw, ccp, tab, false, mp);
+          const int task = wide_select<MG>(n, NW, v, lane, price, T, ccw, ccp, tab, false, mp);
           if (task >= 0 && lane == 0) place_bid(v, task, par);
           WPROF_T(pr1);
           WPROF_ADD(pf_sel, pr1 - pr0);
@@ -1330,7 +1338,7 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   wstamp(P, b, 4);
   // swarm margin: min over every thread's CBAA pair (the alignment gaps are
   // in the word already)
-  block_min_gap(reinterpret_cast<unsigned long long*>(misc + M_MARG), margin_gap(mp));
+  if (MG) block_min_gap(reinterpret_cast<unsigned long long*>(misc + M_MARG), margin_gap(mp));
 
   // ---------------- phase 4: adoption --------------------------------------
   // Do all vehicles hold vehicle 0's table? T is column-major, so compare
@@ -1445,9 +1453,10 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
     if (misc[M_AGREE]) fl |= ACL_SWARM_AGREE;
     if (misc[M_CHANGED]) fl |= ACL_SWARM_CHANGED;
     if (nonfinite) fl |= ACL_SWARM_NONFINITE;
-    const double g = nonfinite ? 0.0
+    // (MG false: skip_margin -- not tracked, -1)
+    const double g = !MG ? -1.0 : nonfinite ? 0.0
         : __longlong_as_double((long long)*reinterpret_cast<unsigned long long*>(misc + M_MARG));
-    if (g < ACL_FRAGILE_MARGIN) fl |= ACL_SWARM_FRAGILE;
+    if (MG && g < ACL_FRAGILE_MARGIN) fl |= ACL_SWARM_FRAGILE;
     st.flags = fl;
     st.eff_rounds = (uint16_t)eff;
     st.rounds = (uint16_t)(2 * n);
@@ -1473,9 +1482,13 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
 hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream, bool fuse) {
   static PerDeviceOnce once;
   const hipError_t e = once.run([] {
-    for (const void* k : {(const void*)align_wide_kernel, (const void*)solve_wide_kernel<false, false>,
-                          (const void*)solve_wide_kernel<true, false>,
-                          (const void*)solve_wide_kernel<true, true>}) {
+    for (const void* k : {(const void*)align_wide_kernel,
+                          (const void*)solve_wide_kernel<false, false, true>,
+                          (const void*)solve_wide_kernel<true, false, true>,
+                          (const void*)solve_wide_kernel<true, true, true>,
+                          (const void*)solve_wide_kernel<false, false, false>,
+                          (const void*)solve_wide_kernel<true, false, false>,
+                          (const void*)solve_wide_kernel<true, true, false>}) {
       const hipError_t r =
           hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (r != hipSuccess) return r;
@@ -1491,12 +1504,21 @@ hipError_t launch_wide(const SolveParams& P, int nb, hipStream_t stream, bool fu
     const int c = make_wclayout(P.n, L.qv + wal(P.n * 24)).total;
     lds = c > lds ? c : lds;
   }
-  if (!fuse)
-    hipLaunchKernelGGL((solve_wide_kernel<false, false>), dim3(nb), dim3(kWBlock), lds, stream, P);
-  else if (P.ctl.gate_margin)
-    hipLaunchKernelGGL((solve_wide_kernel<true, true>), dim3(nb), dim3(kWBlock), lds, stream, P);
-  else
-    hipLaunchKernelGGL((solve_wide_kernel<true, false>), dim3(nb), dim3(kWBlock), lds, stream, P);
+#define ACL_WIDE_LAUNCH(MG_)                                                                   \
+  do {                                                                                         \
+    if (!fuse)                                                                                 \
+      hipLaunchKernelGGL((solve_wide_kernel<false, false, MG_>), dim3(nb), dim3(kWBlock), lds,   \
+                         stream, P);                                                           \
+    else if (P.ctl.gate_margin)                                                                \
+      hipLaunchKernelGGL((solve_wide_kernel<true, true, MG_>), dim3(nb), dim3(kWBlock), lds,     \
+                         stream, P);                                                           \
+    else                                                                                       \
+      hipLaunchKernelGGL((solve_wide_kernel<true, false, MG_>), dim3(nb), dim3(kWBlock), lds,    \
+                         stream, P);                                                           \
+  } while (0)
+  if (P.skip_margin) ACL_WIDE_LAUNCH(false);
+  else ACL_WIDE_LAUNCH(true);
+#undef ACL_WIDE_LAUNCH
   return hipGetLastError();
 }
 

@@ -531,8 +531,7 @@ def main():
         dt_max, call_ms, kms, kcnt, _ = timed(False, True)
         dt_alt, _, _, _, res = timed(True, False)
     margin_line = {
-        # (n > 128: the wide kernel tracks the margin either way)
-        "headline_tracks_margin": bool(args.margin) or n > 128,
+        "headline_tracks_margin": bool(args.margin),
         "value_margin_on": world * B / (dt_max if args.margin else dt_alt),
         "value_margin_off": world * B / (dt_alt if args.margin else dt_max),
         "ms_per_step_margin_on": (dt_max if args.margin else dt_alt) * 1e3,
@@ -595,7 +594,7 @@ def main():
         auction_sym = (f"acl_amd::auction_kernel<1, 128, true, false, {mg}>" if n <= 32 else
                        f"acl_amd::auction_kernel<1, 256, true, false, {mg}>" if n <= 64 else
                        f"acl_amd::auction_kernel<2, 512, true, false, {mg}>" if n <= 128 else
-                       "acl_amd::solve_wide_kernel<true, false>")
+                       f"acl_amd::solve_wide_kernel<true, false, {mg}>")
         gain_sym = (f"acl_amd::gain_kernel<{w['planes']}, false>" if n <= 128 else
                     f"acl_amd::gain_kernel<{w['planes']}, false, 1024>")
         align_sym = "acl_amd::align_kernel<2>" if n <= 128 else "acl_amd::align_wide_kernel"
@@ -687,7 +686,7 @@ def main():
             "n": n, "B_per_gpu": B, "B_total": world * B,
             "edges_per_formation_avg": e_avg,
             "cbaa": "all 2N rounds" if args.full_rounds else "exact fixed-point exit",
-            "decision_margin": ("tracked" if args.margin or n > 128 else
+            "decision_margin": ("tracked" if args.margin else
                                 "not tracked in the timed steps (skip_margin); see `margin`"),
             "parallelism": f"swarm-sharded x{world}",
             "launch": ("one captured HIP graph per step (solve + device-side stats), replayed"

@@ -294,11 +294,11 @@ typedef struct {
                           without edges. The gates themselves are decided on
                           correctly rounded e (the oracle's arithmetic) */
   int32_t skip_margin; /* ABI 7. 0 (default): status.margin is the decision
-                          margin above. 1 (n <= 128): the auction does not
-                          track it -- status.margin = -1, FRAGILE never set;
-                          assignments, round counts and commands are the same
-                          bits (the margin only observes the comparisons).
-                          n > 128 tracks it either way. */
+                          margin above. 1: the auction does not track it --
+                          status.margin = -1, FRAGILE never set; assignments,
+                          round counts and commands are the same bits (the
+                          margin only observes the comparisons; n > 128 the
+                          wide kernel's level walk stops at each winner). */
 } acl_solve_args_t;
 
 /* Largest n acl_solve_batch accepts (512). */
