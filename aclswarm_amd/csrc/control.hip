@@ -966,6 +966,53 @@ __host__ __device__ inline CaPairLayout ca_pair_layout(int n) {
   return L;
 }
 
+// The value of lane ^ J (J = 1 ... 32) without the LDS unit (ds_bpermute:
+// a dependent chain of LDS round trips per sorting stage): quad_perm for 1
+// and 2, row_half_mirror after a quad reversal for 4 (l ^ 3 ^ 7), row_ror:8
+// for 8, and for 16 / 32 gfx950's permlane swaps of a copy with itself,
+// which leave {x[l], x[l ^ J]} in the lane's two registers in some order:
+// the one that is not x[l] is the partner's (equal values: either is).
+template <int J>
+__device__ __forceinline__ unsigned xlane_u32(unsigned x) {
+  if constexpr (J == 1) return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);
+  else if constexpr (J == 2) return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);
+  else if constexpr (J == 4)
+    return (unsigned)__builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp((int)x, 0x1B, 0xF, 0xF, true),
+                                              0x141, 0xF, 0xF, true);
+  else if constexpr (J == 8) return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, true);
+  else {
+    static_assert(J == 16 || J == 32, "lane xor 1 ... 32");
+    const auto v = J == 16 ? __builtin_amdgcn_permlane16_swap(x, x, false, false)
+                           : __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return v[0] == x ? v[1] : v[0];
+  }
+}
+template <int J>
+__device__ __forceinline__ unsigned long long xlane_u64(unsigned long long x) {
+  return ((unsigned long long)xlane_u32<J>((unsigned)(x >> 32)) << 32) | xlane_u32<J>((unsigned)x);
+}
+// runtime j (a power of two <= 32; unrolled loops fold it to a constant)
+__device__ __forceinline__ unsigned long long xlane64(unsigned long long x, int j) {
+  switch (j) {
+    case 1: return xlane_u64<1>(x);
+    case 2: return xlane_u64<2>(x);
+    case 4: return xlane_u64<4>(x);
+    case 8: return xlane_u64<8>(x);
+    case 16: return xlane_u64<16>(x);
+    default: return xlane_u64<32>(x);
+  }
+}
+__device__ __forceinline__ unsigned xlane32(unsigned x, int j) {
+  switch (j) {
+    case 1: return xlane_u32<1>(x);
+    case 2: return xlane_u32<2>(x);
+    case 4: return xlane_u32<4>(x);
+    case 8: return xlane_u32<8>(x);
+    case 16: return xlane_u32<16>(x);
+    default: return xlane_u32<32>(x);
+  }
+}
+
 // Segmented resolution: S-lane segments (S = 16, 32, 64), one vehicle each;
 // lane e of a segment holds element e of its vehicle (m elements, e >= m an
 // unused slot sorting last). As ca_resolve_wave, per segment. Returns the
@@ -979,28 +1026,36 @@ __device__ __forceinline__ int ca_resolve_seg(int lane, int m, double a, int sg,
     a = 0.0;
     sg = 0;
   }
+  // bitonic network on (key, sign); the key travels with the angle (the
+  // angle itself, -0.0 included, is what the later steps read)
+  unsigned long long mk = ca_key(a, sg);
 #pragma unroll
   for (int k = 2; k <= S; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      const double pa = __shfl_xor(a, j, 64);
-      const int ps = __shfl_xor(sg, j, 64);
-      const unsigned long long mk = ca_key(a, sg), pk = ca_key(pa, ps);
+      const unsigned long long pk = xlane64(mk, j);
+      const double pa = __longlong_as_double((long long)xlane64(
+          (unsigned long long)__double_as_longlong(a), j));
+      const int ps = (int)xlane32((unsigned)sg, j);
       const bool pless = pk < mk || (pk == mk && ps < sg);
       const bool mless = mk < pk || (mk == pk && sg < ps);
       const bool take_min = ((e & k) == 0) == ((e & j) == 0);
       if (take_min ? pless : mless) {
         a = pa;
         sg = ps;
+        mk = pk;
       }
     }
   }
+  // inclusive prefix of the signs within the segment: row_shr 1, 2, 4, 8
+  // (zero past the row's start), then row_bcast 15 / 31 into the next row(s)
   int incl = sg;
-#pragma unroll
-  for (int o = 1; o < S; o <<= 1) {
-    const int y = __shfl_up(incl, o, 64);
-    if (e >= o) incl += y;
-  }
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, true);
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, true);
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, true);
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, true);
+  if constexpr (S >= 32) incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xA, 0xF, false);
+  if constexpr (S == 64) incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false);
   const int excl = incl - sg;
   const bool isEnd = sg != 0 && incl == 0;
   const unsigned long long endMask = __ballot(isEnd) & segm;
@@ -1035,6 +1090,12 @@ __device__ __forceinline__ int ca_resolve_seg(int lane, int m, double a, int sg,
 
 #ifndef ACL_CA_OCC
 #define ACL_CA_OCC 4  // ca_pair_kernel's occupancy bound (waves per SIMD)
+#endif
+// diagnostic builds only (-DACL_CA_STOP=k, wrong results): ca_pair_kernel
+// without its phases after k (1: A + B and the prefix, 2: the pair lists,
+// 3: C, 4: D and the general paths), to split the launch's time by phase
+#ifndef ACL_CA_STOP
+#define ACL_CA_STOP 9
 #endif
 __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1136,9 +1197,11 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
     __syncthreads();
     unsigned mine = 0;  // commands this thread modified (E)
     // batches of whole vehicles with at most kCaPairCap pairs
-    for (int k0 = 0; k0 < nc;) {
+    for (int k0 = ACL_CA_STOP < 2 ? nc : 0; k0 < nc;) {
       int k1 = k0 + 1;
-      while (k1 < nc && off[k1 + 1] - off[k0] <= kCaPairCap) ++k1;
+      if (off[nc] - off[k0] <= kCaPairCap) k1 = nc;  // (the usual case: one batch)
+      else
+        while (k1 < nc && off[k1 + 1] - off[k0] <= kCaPairCap) ++k1;
       const int p0 = off[k0], np = off[k1] - p0;
       // the batch's pair list (a wave per vehicle)
       for (int k = k0 + wave; k < k1; k += kW) {
@@ -1154,6 +1217,10 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
       }
       if (tid < 4) misc[1 + tid] = 0;
       __syncthreads();
+      if (ACL_CA_STOP < 3) {
+        k0 = k1;
+        continue;
+      }
       // C: the sector edges of every pair
       #pragma unroll 1
       for (int p = tid; p < np; p += kCaPT) {
@@ -1180,6 +1247,10 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
         if (m > 0) lists[cls * n + atomicAdd(&misc[1 + cls], 1)] = (uint16_t)k;
       }
       __syncthreads();
+      if (ACL_CA_STOP < 4) {
+        k0 = k1;
+        continue;
+      }
       // D: 4 / 2 / 1 vehicles per wave
       {
         const int n16 = misc[1], n32 = misc[2], n64 = misc[3];
@@ -1259,7 +1330,7 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
       __syncthreads();
       // E: the modified commands
       #pragma unroll 1
-      for (int k = k0 + tid; k < k1; k += kCaPT) {
+      for (int k = k0 + tid; k < (ACL_CA_STOP < 5 ? k0 : k1); k += kCaPT) {
         const int res = flg[k] >> 8;
         if (!res) continue;
         const int v = cl[k];
