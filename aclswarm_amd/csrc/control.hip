@@ -954,7 +954,7 @@ __host__ __device__ inline CaPairLayout ca_pair_layout(int n) {
   L.flg = o;   o = cal16(o + n * 4);        // NaN edge (bit 0); result: 1 edge, 2 stop (bits 8..)
   L.edge = o;  o = cal16(o + n * 8);        // the chosen edge
   L.cmk = o;   o = cal16(o + n * 2 * 8);    // candidate masks [k][2]
-  L.lists = o; o = cal16(o + 4 * n * 2);    // vehicles per resolve class (16/32/64/general)
+  L.lists = o; o = cal16(o + 5 * n * 2);    // vehicles per resolve class (8/16/32/64/general)
   L.pairs = o; o = cal16(o + kCaPairCap * 2);   // neighbour of each pair (u8 k | u8 j)
   L.ang = o;   o = cal16(o + kCaPairCap * 2 * 8);
   L.sA = o;    o = cal16(o + 4 * n * 8);    // general / serial paths: one vehicle's slots
@@ -1017,43 +1017,60 @@ __device__ __forceinline__ unsigned xlane32(unsigned x, int j) {
 // lane e of a segment holds element e of its vehicle (m elements, e >= m an
 // unused slot sorting last). As ca_resolve_wave, per segment. Returns the
 // outcome for the lane's vehicle: 0 safe, 1 new direction `edge`, 2 stop.
+// A vehicle's edge x (m = c2 + 2 wraps of them): its pairs' edges from av
+// (beg, end alternating), then the wraps' (-pi, +1), (pi, -1).
+__device__ __forceinline__ double ca_edge_of(const double* av, int c2, int x) {
+  return x < c2 ? av[x] : (((x - c2) & 1) ? kPi : -kPi);
+}
 template <int S>
-__device__ __forceinline__ int ca_resolve_seg(int lane, int m, double a, int sg, bool didWrap,
-                                              double psi, double& edge) {
+__device__ __forceinline__ int ca_resolve_seg(int lane, int m, int c2, const double* av,
+                                              bool didWrap, double psi, double& edge) {
   const int e = lane & (S - 1), base = lane & ~(S - 1);
   const unsigned long long segm = S == 64 ? ~0ull : (((1ull << S) - 1ull) << base);
-  if (e >= m) {
-    a = 0.0;
-    sg = 0;
+  // bitonic network on (key, sign): the key travels with the slot and its
+  // sign packed as slot << 2 | sign + 1 (an edge's sign is its slot's parity:
+  // c2 is even), and the angle itself -- -0.0 included, which the later
+  // steps read -- is fetched by slot once sorted
+  unsigned long long mk = ~0ull;
+  unsigned sv = (unsigned)e << 2 | 1u;  // unused slot: sign 0, sorting last
+  if (e < m) {
+    mk = ca_key(ca_edge_of(av, c2, e), 1);
+    sv = (unsigned)e << 2 | ((e & 1) ? 0u : 2u);
   }
-  // bitonic network on (key, sign); the key travels with the angle (the
-  // angle itself, -0.0 included, is what the later steps read)
-  unsigned long long mk = ca_key(a, sg);
 #pragma unroll
   for (int k = 2; k <= S; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
       const unsigned long long pk = xlane64(mk, j);
-      const double pa = __longlong_as_double((long long)xlane64(
-          (unsigned long long)__double_as_longlong(a), j));
-      const int ps = (int)xlane32((unsigned)sg, j);
-      const bool pless = pk < mk || (pk == mk && ps < sg);
-      const bool mless = mk < pk || (mk == pk && sg < ps);
+      const unsigned ps = xlane32(sv, j);
+      const bool pless = pk < mk || (pk == mk && (ps & 3u) < (sv & 3u));
+      const bool mless = mk < pk || (mk == pk && (sv & 3u) < (ps & 3u));
       const bool take_min = ((e & k) == 0) == ((e & j) == 0);
       if (take_min ? pless : mless) {
-        a = pa;
-        sg = ps;
+        sv = ps;
         mk = pk;
       }
     }
   }
+  const int sg = (int)(sv & 3u) - 1;
+  const double a = sg != 0 ? ca_edge_of(av, c2, (int)(sv >> 2)) : 0.0;
   // inclusive prefix of the signs within the segment: row_shr 1, 2, 4, 8
-  // (zero past the row's start), then row_bcast 15 / 31 into the next row(s)
+  // (zero past the row's start; S = 8 masks the other half row), then
+  // row_bcast 15 / 31 into the next row(s)
   int incl = sg;
-  incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, true);
-  incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, true);
-  incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, true);
-  incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, true);
+  if constexpr (S == 8) {
+    int y = __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, true);
+    incl += e >= 1 ? y : 0;
+    y = __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, true);
+    incl += e >= 2 ? y : 0;
+    y = __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, true);
+    incl += e >= 4 ? y : 0;
+  } else {
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, true);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, true);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, true);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, true);
+  }
   if constexpr (S >= 32) incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xA, 0xF, false);
   if constexpr (S == 64) incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false);
   const int excl = incl - sg;
@@ -1070,15 +1087,16 @@ __device__ __forceinline__ int ca_resolve_seg(int lane, int m, double a, int sg,
   const unsigned long long km = __ballot(keep) & segm;
   const int m2 = __popcll(km);
   if (m2 == 0) return 2;
-  const int it = __popcll(__ballot(keep && a < psi) & segm);  // std::lower_bound
-  auto nth = [&](int r) -> int {  // lane of the r-th kept edge of the segment
-    unsigned long long x = km;
-    for (int t = 0; t < r; ++t) x &= x - 1ull;
-    return __ffsll((long long)x) - 1;
-  };
+  // std::lower_bound: the segment is sorted, so the kept edges below psi are
+  // the first `it` kept lanes -- the (it - 1)-th kept edge is the highest of
+  // them, the it-th the lowest kept lane above
+  const unsigned long long kb = __ballot(keep && a < psi) & segm;
+  const int it = __popcll(kb);
+  const unsigned long long ka = km & ~kb;
   // (the shuffles are wave-wide: every lane computes its own segment's indices)
   int idx;
-  const int lo_l = nth(it > 0 ? it - 1 : 0), hi_l = nth(it < m2 ? it : m2 - 1);
+  const int lo_l = it > 0 ? 63 - __clzll(kb) : __ffsll((long long)km) - 1;
+  const int hi_l = it < m2 ? __ffsll((long long)ka) - 1 : 63 - __clzll(km);
   const double lo = __shfl(a, lo_l, 64), hi = __shfl(a, hi_l, 64);
   if (it == 0) idx = 0;
   else if (it == m2) idx = it - 1;
@@ -1092,7 +1110,7 @@ __device__ __forceinline__ int ca_resolve_seg(int lane, int m, double a, int sg,
 #define ACL_CA_OCC 4  // ca_pair_kernel's occupancy bound (waves per SIMD)
 #endif
 // diagnostic builds only (-DACL_CA_STOP=k, wrong results): ca_pair_kernel
-// without its phases after k (1: A + B and the prefix, 2: the pair lists,
+// without its phases after k (0: nothing, 1: A + B and the prefix, 2: the pair lists,
 // 3: C, 4: D and the general paths), to split the launch's time by phase
 #ifndef ACL_CA_STOP
 #define ACL_CA_STOP 9
@@ -1123,10 +1141,11 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
   signed char* sS = reinterpret_cast<signed char*>(smem + L.sS);
   double* tA = reinterpret_cast<double*>(smem + L.tA);
   signed char* tS = reinterpret_cast<signed char*>(smem + L.tS);
-  int* misc = reinterpret_cast<int*>(smem + L.misc);  // [0] nc, [1..4] class counts, [5] modified
+  // [0] nc, [5] modified, [6] pairs handed out, [8..12] class counts
+  int* misc = reinterpret_cast<int*>(smem + L.misc);
   const acl_safety_params_t sp = P.s;
   const unsigned count = *P.ca_count;
-  for (unsigned itb = blockIdx.x; itb < count; itb += gridDim.x) {
+  for (unsigned itb = blockIdx.x; itb < (ACL_CA_STOP < 1 ? 0u : count); itb += gridDim.x) {
     const int b = (int)P.ca_list[itb];
     const double* gq = P.q + (size_t)b * n * 3;
     for (int k = tid; k < 3 * n; k += kCaPT) q[k] = gq[k];
@@ -1144,6 +1163,7 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
       if (lane == 0) {
         misc[0] = base;
         misc[5] = 0;
+        misc[6] = 0;
       }
     }
     __syncthreads();
@@ -1160,26 +1180,71 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
       wr[k] = 0;
       flg[k] = 0;
     }
-    // B: candidates of every close vehicle (a wave per vehicle, lanes over j)
+    // B: candidates of every close vehicle (a wave per vehicle, lanes over j;
+    // the lane's own points j held in registers). The squared distance
+    // decides outside a 2^-40 band around the threshold; inside it (and for
+    // NaN) the exact test of safety.cpp:421 runs
+    {
+      const double thr = sp.d_avoid_thresh;
+      const bool band = thr > 0.0 && thr < 1e150;  // (else always the exact test)
+      const double lo2 = band ? (thr * (1.0 - 0x1p-40)) * (thr * (1.0 - 0x1p-40)) : -1.0;
+      const double hi2 = band ? (thr * (1.0 + 0x1p-40)) * (thr * (1.0 + 0x1p-40)) : __builtin_inf();
+      double qj0[2], qj1[2];
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const int j = lane + 64 * w;
+        qj0[w] = (w < NW && j < n) ? q[3 * j] : 0.0;
+        qj1[w] = (w < NW && j < n) ? q[3 * j + 1] : 0.0;
+      }
     for (int k = wave; k < nc; k += kW) {
       const int v = cl[k];
       const double qv0 = q[3 * v], qv1 = q[3 * v + 1];
-      int c = 0;
-      for (int w = 0; w < NW; ++w) {
+      unsigned long long mw[2] = {0ull, 0ull};
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        if (w >= NW) break;
         const int j = lane + 64 * w;
         bool cand = false;
         if (j < n && j != v) {
-          const double dx = q[3 * j] - qv0, dy = q[3 * j + 1] - qv1;
-          cand = !(sqrt(dx * dx + dy * dy) > sp.d_avoid_thresh);
+          const double dx = qj0[w] - qv0, dy = qj1[w] - qv1;
+          const double d2 = dx * dx + dy * dy;
+          cand = d2 < lo2;
+          if (!cand && !(d2 > hi2)) cand = !(sqrt(d2) > thr);
         }
-        const unsigned long long m = __ballot(cand);
-        if (lane == 0) cmk[2 * k + w] = m;
-        c += __popcll(m);
+        mw[w] = __ballot(cand);
       }
-      if (lane == 0) cnt[k] = c;
+      const int c = __popcll(mw[0]) + __popcll(mw[1]);
+      // the vehicle's run of pairs: any order of vehicles serves (each
+      // vehicle's sectors are resolved on their own), so a running total
+      // hands out the runs; when every pair fits one batch (the usual case)
+      // the list is written here and the prefix and list passes are skipped
+      int o = 0;
+      if (lane == 0) {
+        cmk[2 * k] = mw[0];
+        cmk[2 * k + 1] = mw[1];
+        cnt[k] = c;
+        o = atomicAdd(&misc[6], c);
+        off[k] = o;
+      }
+      o = __builtin_amdgcn_readfirstlane(o);
+      if (o + c <= kCaPairCap) {
+        int base = o;
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          const unsigned long long m = mw[w];
+          if ((m >> lane) & 1ull)
+            pairs[base + (int)__builtin_amdgcn_mbcnt_hi(
+                             (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                (uint16_t)((k << 8) | (64 * w + lane));
+          base += __popcll(m);
+        }
+      }
+    }
     }
     __syncthreads();
-    if (wave == 0) {  // exclusive prefix of the counts (nc <= 128: two per lane)
+    const int npairs = misc[6];
+    const bool one = npairs <= kCaPairCap;  // workgroup-uniform: one batch, listed in B
+    if (!one && wave == 0) {  // exclusive prefix of the counts (nc <= 128: two per lane)
       int base = 0;
       for (int k0 = 0; k0 < nc; k0 += 64) {
         const int k = k0 + lane;
@@ -1194,17 +1259,17 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
       }
       if (lane == 0) off[nc] = base;
     }
-    __syncthreads();
+    if (!one) __syncthreads();
     unsigned mine = 0;  // commands this thread modified (E)
     // batches of whole vehicles with at most kCaPairCap pairs
     for (int k0 = ACL_CA_STOP < 2 ? nc : 0; k0 < nc;) {
       int k1 = k0 + 1;
-      if (off[nc] - off[k0] <= kCaPairCap) k1 = nc;  // (the usual case: one batch)
+      if (one) k1 = nc;
       else
         while (k1 < nc && off[k1 + 1] - off[k0] <= kCaPairCap) ++k1;
-      const int p0 = off[k0], np = off[k1] - p0;
-      // the batch's pair list (a wave per vehicle)
-      for (int k = k0 + wave; k < k1; k += kW) {
+      const int p0 = one ? 0 : off[k0], np = one ? npairs : off[k1] - p0;
+      // the batch's pair list (a wave per vehicle; listed in B when `one`)
+      for (int k = k0 + wave; k < (one ? k0 : k1); k += kW) {
         int base = off[k] - p0;
         for (int w = 0; w < NW; ++w) {
           const unsigned long long m = cmk[2 * k + w];
@@ -1215,8 +1280,8 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
           base += __popcll(m);
         }
       }
-      if (tid < 4) misc[1 + tid] = 0;
-      __syncthreads();
+      if (tid < 5) misc[8 + tid] = 0;
+      if (!one) __syncthreads();  // (one: the barrier after B ordered the list)
       if (ACL_CA_STOP < 3) {
         k0 = k1;
         continue;
@@ -1243,43 +1308,39 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
       // resolve classes: edges m = 2 cnt + 2 wraps
       for (int k = k0 + tid; k < k1; k += kCaPT) {
         const int m = 2 * (cnt[k] + wr[k]);
-        const int cls = (flg[k] & 1) || m > 64 ? 3 : (m > 32 ? 2 : (m > 16 ? 1 : 0));
-        if (m > 0) lists[cls * n + atomicAdd(&misc[1 + cls], 1)] = (uint16_t)k;
+        const int cls =
+            (flg[k] & 1) || m > 64 ? 4 : (m > 32 ? 3 : (m > 16 ? 2 : (m > 8 ? 1 : 0)));
+        if (m > 0) lists[cls * n + atomicAdd(&misc[8 + cls], 1)] = (uint16_t)k;
       }
       __syncthreads();
       if (ACL_CA_STOP < 4) {
         k0 = k1;
         continue;
       }
-      // D: 4 / 2 / 1 vehicles per wave
+      // D: 8 / 4 / 2 / 1 vehicles per wave
       {
-        const int n16 = misc[1], n32 = misc[2], n64 = misc[3];
-        const int g16 = (n16 + 3) >> 2, g32 = (n32 + 1) >> 1;
-        for (int item = wave; item < g16 + g32 + n64; item += kW) {
+        const int n8 = misc[8], n16 = misc[9], n32 = misc[10], n64 = misc[11];
+        const int g8 = (n8 + 7) >> 3, g16 = (n16 + 3) >> 2, g32 = (n32 + 1) >> 1;
+        for (int item = wave; item < g8 + g16 + g32 + n64; item += kW) {
           int cls, slot, S;
-          if (item < g16) { cls = 0; S = 16; slot = 4 * item + (lane >> 4); }
-          else if (item < g16 + g32) { cls = 1; S = 32; slot = 2 * (item - g16) + (lane >> 5); }
-          else { cls = 2; S = 64; slot = item - g16 - g32; }
-          const int ncls = misc[1 + cls];
+          if (item < g8) { cls = 0; S = 8; slot = 8 * item + (lane >> 3); }
+          else if (item < g8 + g16) { cls = 1; S = 16; slot = 4 * (item - g8) + (lane >> 4); }
+          else if (item < g8 + g16 + g32) {
+            cls = 2; S = 32; slot = 2 * (item - g8 - g16) + (lane >> 5);
+          } else { cls = 3; S = 64; slot = item - g8 - g16 - g32; }
+          const int ncls = misc[8 + cls];
           const bool has = slot < ncls;
           const int k = has ? lists[cls * n + slot] : k0;
           const int c2 = has ? 2 * cnt[k] : 0, m = has ? c2 + 2 * wr[k] : 0;
           const int e = lane & (S - 1);
-          double a = 0.0;
-          int sg = 0;
-          if (e < c2) {
-            a = ang[2 * (off[k] - p0) + e];
-            sg = (e & 1) ? -1 : +1;
-          } else if (e < m) {
-            a = ((e - c2) & 1) ? kPi : -kPi;
-            sg = ((e - c2) & 1) ? -1 : +1;
-          }
+          const double* av = ang + 2 * (off[k] - p0);
           double edge = 0.0;
           const double psi = psiv[k];
           int res;
-          if (S == 16) res = ca_resolve_seg<16>(lane, m, a, sg, wr[k] > 0, psi, edge);
-          else if (S == 32) res = ca_resolve_seg<32>(lane, m, a, sg, wr[k] > 0, psi, edge);
-          else res = ca_resolve_seg<64>(lane, m, a, sg, wr[k] > 0, psi, edge);
+          if (S == 8) res = ca_resolve_seg<8>(lane, m, c2, av, wr[k] > 0, psi, edge);
+          else if (S == 16) res = ca_resolve_seg<16>(lane, m, c2, av, wr[k] > 0, psi, edge);
+          else if (S == 32) res = ca_resolve_seg<32>(lane, m, c2, av, wr[k] > 0, psi, edge);
+          else res = ca_resolve_seg<64>(lane, m, c2, av, wr[k] > 0, psi, edge);
           if (has && e == 0) {
             flg[k] |= res << 8;
             edg[k] = edge;
@@ -1289,9 +1350,9 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
       // more than 64 edges or a NaN angle: one vehicle at a time (wave 0) on
       // the general and serial paths over its slots in sA / sS
       if (wave == 0) {
-        const int ng = misc[4];
+        const int ng = misc[12];
         for (int s = 0; s < ng; ++s) {
-          const int k = lists[3 * n + s];
+          const int k = lists[4 * n + s];
           const int c2 = 2 * cnt[k], m = c2 + 2 * wr[k];
           for (int e = lane; e < m; e += 64) {
             if (e < c2) {

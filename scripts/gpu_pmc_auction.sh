@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counters of the auction kernel alone (instruction mix, stalls), one
 # rocprofv3 pass per counter group, counters only. OUT=<dir under gpurun_out>
-# (default pmca).
+# (default pmca). KPAT: the kernels kept (default: the solve kernels).
 set -o pipefail
 cd /root/repo
 export TMPDIR=/tmp
@@ -24,6 +24,6 @@ for C in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BU
       python3 scripts/auction_only.py --reps 2 ${AUCTION_ARGS} > gpurun_out/$OUT/out_$i.txt 2> gpurun_out/$OUT/err_$i.txt || { echo "pmc pass $i failed"; tail -20 gpurun_out/$OUT/err_$i.txt; exit 1; }
   f=$(find /tmp/pmca_$i -name "*counter_collection.csv" | head -1)
   head -1 "$f" > gpurun_out/$OUT/pass_$i.csv
-  grep -E "solve_kernel|auction_kernel|solve_wide_kernel|align_wide_kernel|align_kernel" "$f" >> gpurun_out/$OUT/pass_$i.csv
+  grep -E "${KPAT:-solve_kernel|auction_kernel|solve_wide_kernel|align_wide_kernel|align_kernel}" "$f" >> gpurun_out/$OUT/pass_$i.csv
 done
 python3 scripts/pmc_show.py gpurun_out/$OUT
