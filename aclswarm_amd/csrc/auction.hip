@@ -689,6 +689,8 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   const bool fbad = f_in < 0 || f_in >= P.F;
   const int f = fbad ? 0 : f_in;
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+  // the vehicles hold their own assignments (acl_solve_args_t::P_rows)
+  const bool rowsm = P.P_rows != nullptr && P.P_rows_on[b] != 0;  // workgroup-uniform
   MarginPair mp;
   margin_init(mp);
   stamp_phase(P, b, tid, 0);
@@ -758,6 +760,30 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     }
   }
   __syncthreads();
+  if (rowsm && !misc[M_BAD]) {
+    // each vehicle's own row: checked, its neighbourhood mask and its
+    // alignment (thread v; align_own_row), the alignment at out[Pin[v]] with
+    // itm the identity, so the price phase reads it as a row's item
+    double galign = 1.0;
+    if (hv) {
+      const int v = tid, i = Pin[v];
+      const uint16_t* row = P.P_rows + ((size_t)b * n + v) * n;
+      unsigned long long nbm[2];
+      const bool ok = align_own_row<2>(
+          n, NC, v, i, adjF + 2 * i, p, [&](int j) { return (int)row[j]; },
+          [&](int u, double& x, double& y) {
+            x = qf[3 * Pin[u]];
+            y = qf[3 * Pin[u] + 1];
+          },
+          nbm, out + 6 * i, galign);
+      if (!ok) misc[M_BAD] = 1;
+      vadj[2 * v] = nbm[0];
+      vadj[2 * v + 1] = nbm[1];
+    }
+    for (int i = tid; i < n; i += kAB) itm[i] = (unsigned char)i;
+    block_min_gap(margw, galign);
+    __syncthreads();
+  }
   if (misc[M_BAD]) {
     // P_in is not a permutation (or fidx is out of range): nothing is solved
     for (int v = tid; v < n; v += kAB) {
@@ -781,8 +807,8 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     return;
   }
   // closed neighbourhoods in vehicle space (bidIterComplete, auctioneer.cpp:
-  // 419-437): u ~ v iff u == v or adj(P[v], P[u])
-  {
+  // 419-437): u ~ v iff u == v or adj(P[v], P[u]) (rows: built above)
+  if (!rowsm) {
     int pu[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) pu[c] = (lane + 64 * c < n) ? Pin[lane + 64 * c] : 0;
@@ -800,7 +826,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       if (NC == 1 && lane == 0) vadj[2 * v + 1] = 0ull;
     }
   }
-  if (kInlineAlign && wave == 0) {
+  if (kInlineAlign && wave == 0 && !rowsm) {
     const int ni = align_worklist<NC>(n, adjF, items, itm, lane);
     if (lane == 0) misc[A_NITEMS] = ni;
   }
@@ -812,7 +838,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   // Auctioneer::alignFormation per distinct neighbourhood (auctioneer.cpp:
   // 347-415) ran in align_kernel: read back the items' (R, t), the item of
   // every formation row and the swarm's smallest alignment gap
-  if constexpr (kInlineAlign) {
+  if (rowsm) {
+    // (the own-row alignments are in out already)
+  } else if constexpr (kInlineAlign) {
     const int nitems = misc[A_NITEMS];
     double galign = 1.0;
     if (wave * 64 < nitems) align_chunk<NC>(n, pq, adjF, items, nitems, wave * 64, lane, out, galign);
@@ -1395,7 +1423,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   // and identical, or none valid), else one row per vehicle.
   const int ninv = misc[M_NINV];
   const bool allvalid = ninv == 0;
-  const bool uniform = (allvalid && misc[M_AGREE]) || ninv == n;
+  // (own rows: a vehicle without a valid table keeps its own row, so only an
+  // agreed valid table is one row for all)
+  const bool uniform = (allvalid && misc[M_AGREE]) || (ninv == n && !rowsm);
   // this thread's entry of the shared row (fused control phase)
   const int ptv = (uniform && tid < n) ? (allvalid ? T[tid] : Ptin[tid]) : 0;
   {
@@ -1407,7 +1437,8 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
       uint16_t* rows = reinterpret_cast<uint16_t*>(P.ws + P.W.rows) + (size_t)b * n * n;
       for (int k = tid; k < n * n; k += kAB) {
         const int v = k / n, jj = k - v * n;
-        rows[k] = validv[v] ? T[v * TS + jj] : Ptin[jj];
+        rows[k] = validv[v] ? T[v * TS + jj]
+                  : rowsm ? P.P_rows[(size_t)b * n * n + k] : Ptin[jj];
       }
       for (int v = tid; v < n; v += kAB) P.ws[P.W.vvalid + (size_t)b * n + v] = validv[v];
     }

@@ -1431,7 +1431,7 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
 // acl_control_batch's hand-off: P must be a permutation (else BAD_INPUT and
 // zero commands, as for the auction's P_in); the inverse assignment is the
 // shared row the gain kernel reads. Episodes: swarms flagged in P.keep keep
-// their per-vehicle rows; the others' P is also copied to P.seed_out.
+// their per-vehicle rows.
 __global__ void __launch_bounds__(256) control_prep_kernel(const CtlParams P,
                                                            const uint16_t* Pg) {
   __shared__ unsigned long long seen[kMaxNWide / 64];
@@ -1460,7 +1460,6 @@ __global__ void __launch_bounds__(256) control_prep_kernel(const CtlParams P,
       if (atomicOr(&seen[pv >> 6], bit) & bit) bad = 1;
       wsPt[pv] = (uint16_t)v;
     }
-    if (P.seed_out) P.seed_out[(size_t)b * n + v] = (uint16_t)pv;
   }
   __syncthreads();
   if (tid == 0) {

@@ -123,10 +123,9 @@ struct CtlParams {
   unsigned long long* stamps;  // diagnostic (SolveParams::stamps; NULL = off)
   // control_prep_kernel, episodes only (NULL otherwise): a swarm with
   // keep[b * keep_stride] != 0 flies per-vehicle tables already in wsRows
-  // (mode 1, no permutation check); seed_out[b] <- P for the others
+  // (mode 1, no permutation check)
   const uint8_t* keep = nullptr;
   int keep_stride = 0;
-  uint16_t* seed_out = nullptr;
 };
 
 // Diagnostic stamps (acl_internal_set_stamps; scripts/phase_profile.py):
@@ -160,7 +159,9 @@ struct SolveParams {
   acl_safety_params_t s;
   int early_exit;
   int do_control;
-  int skip_margin;    // acl_solve_args_t::skip_margin (n <= 128)
+  int skip_margin;    // acl_solve_args_t::skip_margin
+  const uint16_t* P_rows;    // acl_solve_args_t::P_rows / P_rows_on (optional)
+  const uint8_t* P_rows_on;
   unsigned char* ws;  // workspace base (WsLayout)
   WsLayout W;
   unsigned long long* stamps;  // diagnostic: [B][kStampStride] (above; NULL = off)

@@ -35,11 +35,10 @@ constexpr int kEpBlock = 128;  // traj_kernel threads (64 for n <= 64: fewer wav
 // Episode workspace: the auction's solve workspace, the control stage's own
 // hand-off region (the head of a WsLayout: pt, mode, rows, ...; kept apart
 // so that an auction still pending does not overwrite the tables the
-// vehicles fly meanwhile), the auction's output, the control stage's output
-// of the current step, and the next auction's P_in (`seed`: the last agreed
-// assignment, which differs from P while a swarm flies per-vehicle tables).
+// vehicles fly meanwhile -- and the next auction's own rows, P_rows), the
+// auction's output and the control stage's output of the current step.
 struct EpLayout {
-  size_t solve, ctl, seed, Pnew, st, cst, u, us, ca, lat, total;
+  size_t solve, ctl, Pnew, st, cst, u, us, ca, lat, total;
 };
 
 inline EpLayout ep_layout(int n, int B) {
@@ -48,7 +47,6 @@ inline EpLayout ep_layout(int n, int B) {
   size_t o = 0;
   L.solve = o; o = ws_al(o + ws_layout(n, B).total);
   L.ctl = o;   o = ws_al(o + ws_layout(n, B).wide);  // pt .. camask: what run_control uses
-  L.seed = o;  o = ws_al(o + bb * nb * 2);
   L.Pnew = o;  o = ws_al(o + bb * nb * 2);
   L.st = o;    o = ws_al(o + bb * sizeof(acl_swarm_status_t));
   L.cst = o;   o = ws_al(o + bb * sizeof(acl_swarm_status_t));
@@ -109,7 +107,7 @@ __global__ void __launch_bounds__(64) latency_kernel(int n, const int32_t* fidx,
 //   step has come completes.
 // Completion, each vehicle as auctioneer.cpp:250-295 (oracle
 // episode_oracle.adopt): agreed and valid -- every vehicle adopts the one
-// table (P, seed, the control stage's shared row); agreed and invalid -- all
+// table (P, the control stage's shared row); agreed and invalid -- all
 // keep theirs and the swarm skips its next auto-auction; disagreement -- each
 // vehicle whose own final table is valid adopts it (its row of the auction's
 // per-vehicle hand-off, vvalid), the others keep their own, and the swarm
@@ -120,7 +118,6 @@ struct AdoptArgs {
   int n, step, mode;
   const int32_t* lat;
   uint16_t* P;
-  uint16_t* seed;
   const uint16_t* Pnew;
   const acl_swarm_status_t* st;
   const uint16_t* sRows;   // the auction's per-vehicle rows / validity (solve workspace)
@@ -178,7 +175,6 @@ __global__ void __launch_bounds__(256) adopt_kernel(const AdoptArgs A) {
     for (int v = tid; v < n; v += 256) {
       const uint16_t pv = A.Pnew[bn + v];
       A.P[bn + v] = pv;
-      A.seed[bn + v] = pv;
       A.ctlPt[bn + pv] = (uint16_t)v;  // a valid permutation
     }
     if (tid == 0) {
@@ -389,12 +385,18 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
   double* us = reinterpret_cast<double*>(ws + W.us);
   uint8_t* ca = ws + W.ca;
 
-  uint16_t* seed = reinterpret_cast<uint16_t*>(ws + W.seed);
   const WsLayout WS = ws_layout(n, B);
   unsigned char* wc = ws + W.ctl;  // the control stage's hand-off region
 
+  // every auction starts from the vehicles' own assignments: P (each
+  // vehicle's point) and, for swarms flying per-vehicle tables (the control
+  // hand-off's mode 1), each vehicle's own table as its row
+  // (acl_solve_args_t::P_rows: alignment and neighbours, auctioneer.cpp:
+  // 357,369,422-427)
   acl_solve_args_t sa = {};
-  sa.B = B; sa.fidx = a->fidx; sa.q = a->q; sa.vel = a->vel; sa.P_in = seed; sa.P_out = Pnew;
+  sa.B = B; sa.fidx = a->fidx; sa.q = a->q; sa.vel = a->vel; sa.P_in = a->P; sa.P_out = Pnew;
+  sa.P_rows = reinterpret_cast<const uint16_t*>(wc + WS.rows);
+  sa.P_rows_on = wc + WS.mode;
   sa.status = st; sa.workspace = ws + W.solve;
   sa.cntrl = a->cntrl; sa.safety = a->safety; sa.early_exit = 1; sa.do_control = 0;
   sa.skip_margin = 1;  // the episode reads assignments and flags, never the decision margin
@@ -414,22 +416,21 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
 
   // The call's hand-off, before its first auction: swarms flying one
   // assignment get the inverse of P (permutation check, as
-  // acl_control_batch) and seed = P; swarms flying per-vehicle tables
-  // (est.per_vehicle, from an earlier call on this workspace) keep theirs.
+  // acl_control_batch); swarms flying per-vehicle tables (est.per_vehicle,
+  // from an earlier call on this workspace) keep theirs.
   {
     CtlParams C;
     const acl_status_t r = ctl_params(F, &cs, C);
     if (r != ACL_OK) return r;
     C.keep = reinterpret_cast<const uint8_t*>(a->est) + offsetof(acl_episode_status_t, per_vehicle);
     C.keep_stride = (int)sizeof(acl_episode_status_t);
-    C.seed_out = seed;
     if (hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
       return acl__set_error("hipMemsetAsync failed");
     if (launch_control_prep(C, a->P, B, s) != hipSuccess)
       return acl__set_error("control_prep launch failed");
   }
   AdoptArgs A;
-  A.n = n; A.lat = nullptr; A.P = a->P; A.seed = seed; A.Pnew = Pnew; A.st = st;
+  A.n = n; A.lat = nullptr; A.P = a->P; A.Pnew = Pnew; A.st = st;
   A.sRows = reinterpret_cast<const uint16_t*>(ws + W.solve + WS.rows);
   A.sValid = ws + W.solve + WS.vvalid;
   A.flush = a->flush; A.est = a->est;

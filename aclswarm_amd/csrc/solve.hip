@@ -203,6 +203,10 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
   P.who = a->who; P.align_Rt = a->align_Rt; P.g = a->cntrl; P.s = a->safety;
   P.early_exit = a->early_exit; P.do_control = a->do_control;
   P.skip_margin = a->skip_margin;
+  if (a->P_rows && !a->P_rows_on)
+    return acl__set_error("acl_solve_batch: P_rows needs P_rows_on");
+  P.P_rows = a->P_rows;
+  P.P_rows_on = a->P_rows ? a->P_rows_on : nullptr;
   P.ws = (unsigned char*)a->workspace;
   P.W = ws_layout(n, a->B);
   P.stamps = g_stamps;

@@ -620,6 +620,37 @@ __global__ void __launch_bounds__(kWABlock, 2) align_wide_kernel(const SolvePara
     if (tid == 0) *wflags = 1u;
     return;
   }
+  unsigned long long* gw = reinterpret_cast<unsigned long long*>(misc + 12);  // (8-byte aligned)
+  if (P.P_rows != nullptr && P.P_rows_on[b] != 0) {  // workgroup-uniform
+    // the vehicles hold their own assignments (acl_solve_args_t::P_rows):
+    // thread v checks its row, builds its neighbourhood and aligns with it
+    double galign = 1.0;
+    if (tid == 0) *gw = (unsigned long long)__double_as_longlong(1.0);
+    __syncthreads();
+    for (int v = tid; v < n; v += kWABlock) {
+      const int i = Pin[v];
+      const uint16_t* row = P.P_rows + ((size_t)b * n + v) * n;
+      unsigned long long nbm[kWMaxW];
+      const bool ok = align_own_row<kWMaxW>(
+          n, NW, v, i, adjF + (size_t)i * NW, p, [&](int j) { return (int)row[j]; },
+          [&](int u, double& x, double& y) {
+            x = qf[3 * Pin[u]];
+            y = qf[3 * Pin[u] + 1];
+          },
+          nbm, out + 6 * v, galign);
+      if (!ok) misc[M_BAD] = 1;
+#pragma unroll
+      for (int c = 0; c < kWMaxW; ++c)
+        if (c < NW) vadj[c * n + v] = nbm[c];
+    }
+    block_min_gap(gw, galign);
+    __syncthreads();
+    if (tid == 0) {
+      *reinterpret_cast<unsigned long long*>(wsa + WW.gal) = *gw;
+      *wflags = misc[M_BAD] ? 1u : (misc[M_PINF] ? 2u : 0u);
+    }
+    return;
+  }
   // vehicle-space closed neighbourhoods (bidIterComplete, auctioneer.cpp:419-437)
   for (int v = wave; v < n; v += kAW) {
     const int i = Pin[v];
@@ -715,7 +746,6 @@ __global__ void __launch_bounds__(kWABlock, 2) align_wide_kernel(const SolvePara
     o[0] = R[0]; o[1] = R[1]; o[2] = R[2]; o[3] = R[3]; o[4] = t[0]; o[5] = t[1];
   }
   // the swarm's smallest alignment gap and the flags
-  unsigned long long* gw = reinterpret_cast<unsigned long long*>(misc + 12);  // (8-byte aligned)
   if (tid == 0) *gw = (unsigned long long)__double_as_longlong(1.0);
   __syncthreads();
   block_min_gap(gw, galign);
@@ -1431,7 +1461,9 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   wstamp(P, b, 5);
   {
     const bool allvalid = misc[M_NINV] == 0;
-    const bool uniform = (allvalid && misc[M_AGREE]) || misc[M_NINV] == n;
+    // (own rows: a vehicle without a valid table keeps its own row)
+    const bool rowsm = P.P_rows != nullptr && P.P_rows_on[b] != 0;
+    const bool uniform = (allvalid && misc[M_AGREE]) || (misc[M_NINV] == n && !rowsm);
     uint16_t* wsPt = reinterpret_cast<uint16_t*>(P.ws + P.W.pt) + (size_t)b * n;
     if (tid == 0) P.ws[P.W.mode + b] = uniform ? 0 : 1;
     if (uniform) {
@@ -1440,7 +1472,8 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
       uint16_t* rows = reinterpret_cast<uint16_t*>(P.ws + P.W.rows) + (size_t)b * n * n;
       for (int k = tid; k < n * n; k += kWBlock) {
         const int v = k / n, jj = k - v * n;
-        rows[k] = validv[v] ? (uint16_t)tab(jj, v) : Ptin[jj];
+        rows[k] = validv[v] ? (uint16_t)tab(jj, v)
+                  : rowsm ? P.P_rows[(size_t)b * n * n + k] : Ptin[jj];
       }
       for (int v = tid; v < n; v += kWBlock) P.ws[P.W.vvalid + (size_t)b * n + v] = validv[v];
     }

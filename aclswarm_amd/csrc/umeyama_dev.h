@@ -189,4 +189,95 @@ __device__ inline bool umeyama_finish(const double* S, const double* sm, const d
   return true;
 }
 
+// One vehicle that holds its own assignment (acl_solve_args_t::P_rows): its
+// row (formation point -> vehicle) is checked to be a permutation with the
+// vehicle at its point i, its closed CBAA neighbourhood in vehicle space is
+// {row[j] : j = i or adj(i, j)} (bidIterComplete, auctioneer.cpp:419-437,
+// with the vehicle's own P_ / Pt_), and Auctioneer::alignFormation (:347-415)
+// runs on the members j of formation row i's closed neighbourhood ascending,
+// src p_j.xy, dst the q of vehicle row[j] (qxy(u, x, y)). The arithmetic is
+// align_chunk's / align_wide_kernel's: sums from -0.0 in ascending order, the
+// lazy (k + 4 < 20) or GEMM product form. adjrow: formation row i's words
+// (NW of them, masked past n); NWM: the mask arrays' size. Returns false when
+// the row is not such a permutation (the swarm is BAD_INPUT).
+template <int NWM, class RowAt, class QXY>
+__device__ inline bool align_own_row(int n, int NW, int v, int i, const unsigned long long* adjrow,
+                                     const double* p, RowAt row, QXY qxy,
+                                     unsigned long long (&nb)[NWM], double* o6, double& gap) {
+  unsigned long long mem[NWM], seen[NWM];
+#pragma unroll
+  for (int w = 0; w < NWM; ++w) {
+    mem[w] = w < NW ? adjrow[w] : 0ull;
+    if (w == (i >> 6)) mem[w] |= 1ull << (i & 63);
+    seen[w] = 0ull;
+    nb[w] = 0ull;
+  }
+  bool ok = row(i) == v;
+  int k = 0;
+  double s0 = -0.0, s1 = -0.0, s2 = -0.0, s3 = -0.0;
+  for (int j = 0; j < n; ++j) {
+    const int u = row(j);
+    const unsigned long long bu = 1ull << (u & 63);
+    bool dup = false;
+#pragma unroll
+    for (int w = 0; w < NWM; ++w)
+      if (w == (u >> 6)) {
+        dup = (seen[w] & bu) != 0ull;
+        seen[w] |= bu;
+      }
+    ok = ok && u < n && !dup;
+    bool m = false;
+#pragma unroll
+    for (int w = 0; w < NWM; ++w)
+      if (w == (j >> 6)) m = ((mem[w] >> (j & 63)) & 1ull) != 0ull;
+    if (m && u < n) {
+#pragma unroll
+      for (int w = 0; w < NWM; ++w)
+        if (w == (u >> 6)) nb[w] |= bu;
+      double qx, qy;
+      qxy(u, qx, qy);
+      s0 = s0 + p[3 * j];
+      s1 = s1 + p[3 * j + 1];
+      s2 = s2 + qx;
+      s3 = s3 + qy;
+      ++k;
+    }
+  }
+  if (!ok) return false;
+  const double oon = 1.0 / (double)k;
+  const double sm[2] = {s0 * oon, s1 * oon};
+  const double dm[2] = {s2 * oon, s3 * oon};
+  const bool lazy = (k + 4) < 20;
+  const double z0 = lazy ? -0.0 : 0.0;
+  double c0 = z0, c1 = z0, c2 = z0, c3 = z0;
+  for (int j = 0; j < n; ++j) {
+    bool m = false;
+#pragma unroll
+    for (int w = 0; w < NWM; ++w)
+      if (w == (j >> 6)) m = ((mem[w] >> (j & 63)) & 1ull) != 0ull;
+    if (!m) continue;
+    double qx, qy;
+    qxy(row(j), qx, qy);
+    const double e0 = p[3 * j] - sm[0], e1 = p[3 * j + 1] - sm[1];
+    double d0 = qx - dm[0], d1 = qy - dm[1];
+    if (lazy) {
+      d0 = oon * d0;
+      d1 = oon * d1;
+    }
+    c0 = c0 + d0 * e0;
+    c1 = c1 + d0 * e1;
+    c2 = c2 + d1 * e0;
+    c3 = c3 + d1 * e1;
+  }
+  if (!lazy) {
+    c0 = c0 * oon; c1 = c1 * oon; c2 = c2 * oon; c3 = c3 * oon;
+  }
+  const double S[4] = {c0, c2, c1, c3};
+  double R[4], t[2], g;
+  umeyama_finish(S, sm, dm, R, t, &g);
+  gap = g < gap ? g : gap;
+  o6[0] = R[0]; o6[1] = R[1]; o6[2] = R[2]; o6[3] = R[3]; o6[4] = t[0]; o6[5] = t[1];
+  return true;
+}
+
 }  // namespace acl_amd

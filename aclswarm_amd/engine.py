@@ -129,11 +129,16 @@ def workspace(n, B, device):
 
 def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
           do_control=True, want_who=False, want_align=False, want_gate_margin=False, out=None,
-          stream=None, margin=True):
+          stream=None, margin=True, P_rows=None, P_rows_on=None):
     """Run acl_solve_batch for B = q.shape[0] swarms. All tensors on device.
 
-    margin=False sets acl_solve_args_t::skip_margin (n <= 128): the status
-    margin is -1 and FRAGILE is never set; everything else is unchanged.
+    margin=False sets acl_solve_args_t::skip_margin: the status margin is -1
+    and FRAGILE is never set; everything else is unchanged.
+
+    P_rows [B][n][n] int16 (uint16 bits) and P_rows_on [B] uint8
+    (acl_solve_args_t::P_rows): a swarm with P_rows_on[b] != 0 runs its
+    auction from each vehicle's own assignment, row v = vehicle v's table
+    (formation point -> vehicle) with P_in[b][v] its point in it.
 
     fidx [B] int32, q/vel [B][n][3] f64, P_in [B][n] int16 (uint16 bits).
     Returns a dict of device tensors: P_out, status (raw 16-byte records as
@@ -175,6 +180,11 @@ def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
     a.early_exit = int(bool(early_exit))
     a.do_control = int(bool(do_control))
     a.skip_margin = 0 if margin else 1
+    if P_rows is not None:
+        if P_rows_on is None or P_rows.shape != (B, n, n) or P_rows_on.shape != (B,):
+            raise ValueError("P_rows [B][n][n] needs P_rows_on [B]")
+        a.P_rows = P_rows.data_ptr()
+        a.P_rows_on = P_rows_on.data_ptr()
     F = table.struct()
     if stream is None:
         stream = torch.cuda.current_stream(dev).cuda_stream

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define ACL_ABI_VERSION 7
+#define ACL_ABI_VERSION 8
 
 typedef enum {
   ACL_OK = 0,
@@ -299,6 +299,18 @@ typedef struct {
                           round counts and commands are the same bits (the
                           margin only observes the comparisons; n > 128 the
                           wide kernel's level walk stops at each winner). */
+  const uint16_t* P_rows;   /* ABI 8. Optional (NULL: every swarm uses P_in)
+                          [B][n][n]: for a swarm with P_rows_on[b] != 0, row v
+                          is vehicle v's own assignment as formation point ->
+                          vehicle (its Pt_), and P_in[b][v] must be v's point
+                          in it (row v at P_in[b][v] holds v). Each vehicle
+                          then aligns the formation with its own assignment
+                          (auctioneer.cpp:357,369), takes its CBAA neighbours
+                          from it (:422-427), and keeps it when its final
+                          table is invalid -- the reference's auction while
+                          the vehicles hold different assignments. A row that
+                          is not such a permutation: BAD_INPUT. */
+  const uint8_t* P_rows_on; /* [B] (with P_rows) */
 } acl_solve_args_t;
 
 /* Largest n acl_solve_batch accepts (512). */
@@ -431,15 +443,16 @@ acl_status_t acl_hungarian_batch(const acl_formations_t* formations,
  *      (CoordinationROS::autoauctionCb, coordination_ros.cpp:322-359): a swarm
  *      whose previous auction converged on an invalid assignment flushes and
  *      skips this one (:339-345, Auctioneer::flush); otherwise CBAA from the
- *      current q (acl_solve_batch's auction, P_in = the swarm's last agreed
- *      assignment), and each vehicle's adoption as auctioneer.cpp:250-295:
+ *      current q (acl_solve_batch's auction from the vehicles' own
+ *      assignments: P_in = P, and for a swarm flying per-vehicle tables each
+ *      vehicle's own table as its P_rows row, so every vehicle aligns and
+ *      finds its neighbours with its own assignment as in the reference),
+ *      and each vehicle's adoption as auctioneer.cpp:250-295:
  *      an agreed valid result is adopted by every vehicle; an agreed invalid
  *      one sets `flush`; on disagreement each vehicle whose own final table
  *      is valid adopts it and the others keep theirs -- the swarm then flies
  *      per-vehicle tables (est.per_vehicle) until an agreed valid auction
- *      (model limits: the next auction aligns every vehicle with the last
- *      agreed assignment, where the reference's vehicles each use their own;
- *      and a vehicle whose own table is invalid after a disagreeing auction
+ *      (model limit: a vehicle whose own table is invalid after a disagreeing auction
  *      only keeps its old table, where the reference's vehicle also sets
  *      invalid_assignment_ (auctioneer.cpp:291) and flushes and skips its
  *      next auto-auction alone (coordination_ros.cpp:339-345) -- a per-vehicle

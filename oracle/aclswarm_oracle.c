@@ -332,10 +332,20 @@ void orc_prices(int n, const double* q, const double* p, const uint8_t* adj,
 
 void orc_prices_gap(int n, const double* q, const double* p, const uint8_t* adj,
                     const uint16_t* P, float* C, double* Rt, double* gap_min) {
+  orc_prices_rows(n, q, p, adj, P, NULL, C, Rt, gap_min);
+}
+
+void orc_prices_rows(int n, const double* q, const double* p, const uint8_t* adj,
+                     const uint16_t* P, const uint16_t* Prows, float* C, double* Rt,
+                     double* gap_min) {
+  /* Prows (optional [n][n]): vehicle v aligns with its own assignment, the
+   * inverse of its row (auctioneer.cpp:357,369: P_, Pt_ are the vehicle's) */
+  uint16_t* Pv = Prows ? (uint16_t*)malloc(sizeof(uint16_t) * (size_t)n) : NULL;
   if (gap_min) *gap_min = 1.0;
   for (int v = 0; v < n; ++v) {
     double R[4], t[2], g = 1.0;
-    orc_align_gap(n, v, q, p, adj, P, R, t, &g);
+    if (Pv) invert_perm(n, Prows + (size_t)v * n, Pv);
+    orc_align_gap(n, v, q, p, adj, Pv ? Pv : P, R, t, &g);
     if (gap_min && g < *gap_min) *gap_min = g;
     if (Rt) {
       Rt[6 * v + 0] = R[0]; Rt[6 * v + 1] = R[1];
@@ -355,6 +365,7 @@ void orc_prices_gap(int n, const double* q, const double* p, const uint8_t* adj,
       C[(size_t)v * n + j] = (float)(1.0 / (nrm + 1e-8));
     }
   }
+  free(Pv);
 }
 
 /* Decision-margin tracker (include/aclswarm_amd.h): the compared pair
@@ -421,6 +432,12 @@ int orc_cbaa(int n, const float* C, const uint8_t* adj, const uint16_t* P,
 
 int orc_cbaa_m(int n, const float* C, const uint8_t* adj, const uint16_t* P,
                int early_exit, int32_t* who_out, float* price_out, float* m) {
+  return orc_cbaa_rows(n, C, adj, P, NULL, early_exit, who_out, price_out, m);
+}
+
+int orc_cbaa_rows(int n, const float* C, const uint8_t* adj, const uint16_t* P,
+                  const uint16_t* Prows, int early_exit, int32_t* who_out,
+                  float* price_out, float* m) {
   const size_t nn = (size_t)n * n;
   int32_t* who = (int32_t*)malloc(sizeof(int32_t) * nn);
   int32_t* who2 = (int32_t*)malloc(sizeof(int32_t) * nn);
@@ -432,12 +449,21 @@ int orc_cbaa_m(int n, const float* C, const uint8_t* adj, const uint16_t* P,
   /* Closed neighbourhood in vehicle space, ascending vehid = std::map order
    * of bids_curr_ (auctioneer.cpp:419-437, 480): u is a neighbour of v iff
    * adj(P[v], P[u]) (u = Pt[j] <=> j = P[u]), plus v itself. */
+  /* Prows (optional): v's neighbours come from its own assignment, the
+   * inverse of its row (bidIterComplete uses the vehicle's P_ and Pt_) */
+  uint16_t* Pv = Prows ? (uint16_t*)malloc(sizeof(uint16_t) * (size_t)n) : NULL;
   for (int v = 0; v < n; ++v) {
+    const uint16_t* Pw = P;
+    if (Pv) {
+      invert_perm(n, Prows + (size_t)v * n, Pv);
+      Pw = Pv;
+    }
     int d = 0;
     for (int u = 0; u < n; ++u)
-      if (u == v || adj[(size_t)P[v] * n + P[u]]) nb[(size_t)v * n + d++] = u;
+      if (u == v || adj[(size_t)Pw[v] * n + Pw[u]]) nb[(size_t)v * n + d++] = u;
     deg[v] = d;
   }
+  free(Pv);
   /* reset (auctioneer.cpp:448-465) and the START bid (round 0) */
   for (size_t k = 0; k < nn; ++k) {
     who[k] = ORC_NONE;
@@ -709,11 +735,30 @@ void orc_solve_g(int n, const double* q, const double* vel, const double* p,
                  int early_exit, uint16_t* P_out, acl_swarm_status_t* st,
                  double* u, double* u_safe, uint8_t* ca, uint16_t* who_out,
                  double* gate_margin) {
+  orc_solve_rows(n, q, vel, p, adj, gains, P_in, NULL, g, s, early_exit, P_out, st, u,
+                 u_safe, ca, who_out, gate_margin);
+}
+
+/* every row of Prows a permutation that puts its vehicle at its P_in point */
+static int rows_ok(int n, const uint16_t* P_in, const uint16_t* Prows) {
+  for (int v = 0; v < n; ++v) {
+    const uint16_t* r = Prows + (size_t)v * n;
+    if (!is_perm(n, r) || r[P_in[v]] != v) return 0;
+  }
+  return 1;
+}
+
+void orc_solve_rows(int n, const double* q, const double* vel, const double* p,
+                    const uint8_t* adj, const double* gains, const uint16_t* P_in,
+                    const uint16_t* Prows, const acl_cntrl_gains_t* g,
+                    const acl_safety_params_t* s, int early_exit, uint16_t* P_out,
+                    acl_swarm_status_t* st, double* u, double* u_safe, uint8_t* ca,
+                    uint16_t* who_out, double* gate_margin) {
   const size_t nn = (size_t)n * n;
   if (gate_margin) *gate_margin = INFINITY;
   memset(st, 0, sizeof(*st));
   st->rounds = (uint16_t)(2 * n);
-  if (!is_perm(n, P_in)) {
+  if (!is_perm(n, P_in) || (Prows && !rows_ok(n, P_in, Prows))) {
     st->flags = ACL_SWARM_BAD_INPUT;
     st->margin = 1.0f; /* nothing compared */
     for (int v = 0; v < n; ++v) {
@@ -736,13 +781,13 @@ void orc_solve_g(int n, const double* q, const double* vel, const double* p,
   double* dz = (double*)malloc(sizeof(double) * nn);
   invert_perm(n, P_in, Pt_in);
   double gmin = 1.0;
-  orc_prices_gap(n, q, p, adj, P_in, C, NULL, &gmin);
+  orc_prices_rows(n, q, p, adj, P_in, Prows, C, NULL, &gmin);
   uint32_t flags = 0;
   for (size_t k = 0; k < nn; ++k)
     if (isnan(C[k])) flags |= ACL_SWARM_NONFINITE;
   float mpair[2] = {1.0f, 0.0f};
-  st->eff_rounds = (uint16_t)orc_cbaa_m(n, C, adj, P_in, early_exit, who, NULL,
-                                        orc_no_margin ? NULL : mpair);
+  st->eff_rounds = (uint16_t)orc_cbaa_rows(n, C, adj, P_in, Prows, early_exit, who, NULL,
+                                           orc_no_margin ? NULL : mpair);
   {
     const double gc = orc_margin_gap(mpair);
     if (gc < gmin) gmin = gc;
@@ -766,9 +811,9 @@ void orc_solve_g(int n, const double* q, const double* vel, const double* p,
       for (int j = 0; j < n; ++j) Pt_v[j] = (uint16_t)w[j];
       valid = is_perm(n, Pt_v);
     }
-    if (!valid) {
+    if (!valid) {  /* the vehicle keeps its own assignment */
       ++n_invalid;
-      memcpy(Pt_v, Pt_in, sizeof(uint16_t) * (size_t)n);
+      memcpy(Pt_v, Prows ? Prows + (size_t)v * n : Pt_in, sizeof(uint16_t) * (size_t)n);
     }
     int i = 0;
     while (Pt_v[i] != v) ++i;

@@ -77,6 +77,12 @@ void orc_align_gap(int n, int v, const double* q, const double* p,
 void orc_prices_gap(int n, const double* q, const double* p, const uint8_t* adj,
                     const uint16_t* P, float* C, double* Rt, double* gap_min);
 
+/* orc_prices_gap with each vehicle's own assignment: Prows (optional,
+ * [n][n]) row v = vehicle v's assignment as formation point -> vehicle. */
+void orc_prices_rows(int n, const double* q, const double* p, const uint8_t* adj,
+                     const uint16_t* P, const uint16_t* Prows, float* C, double* Rt,
+                     double* gap_min);
+
 /* getPrice for every (vehicle v, task j) with v's own alignment:
  * C[v*n+j] = (float)(1.0 / (||q_v - (R_v p_j + t_v)|| + 1e-8)).
  * Rt (optional, [n][6]) receives R00,R01,R10,R11,t0,t1 per vehicle. */
@@ -94,6 +100,11 @@ int orc_cbaa(int n, const float* C, const uint8_t* adj, const uint16_t* P,
  * comparisons (include/aclswarm_amd.h); m may be NULL. */
 int orc_cbaa_m(int n, const float* C, const uint8_t* adj, const uint16_t* P,
                int early_exit, int32_t* who_out, float* price_out, float* m);
+/* orc_cbaa_m with each vehicle's neighbours from its own assignment (Prows
+ * as in orc_prices_rows; NULL: every vehicle uses P). */
+int orc_cbaa_rows(int n, const float* C, const uint8_t* adj, const uint16_t* P,
+                  const uint16_t* Prows, int early_exit, int32_t* who_out,
+                  float* price_out, float* m);
 void orc_margin_track(float* m, float hi, float lo);
 double orc_margin_gap(const float* m);
 
@@ -138,6 +149,19 @@ void orc_solve_g(int n, const double* q, const double* vel, const double* p,
                  int early_exit, uint16_t* P_out, acl_swarm_status_t* st,
                  double* u, double* u_safe, uint8_t* ca, uint16_t* who_out,
                  double* gate_margin);
+
+/* orc_solve_g for a swarm whose vehicles hold their own assignments
+ * (acl_solve_args_t::P_rows): Prows [n][n], row v = vehicle v's assignment
+ * as formation point -> vehicle, with Prows[v][P_in[v]] == v; each vehicle
+ * aligns (auctioneer.cpp:357,369), finds its neighbours (:422-427) and, with
+ * an invalid final table, keeps its assignment from its own row. A row that
+ * is not such a permutation is BAD_INPUT. Prows NULL: orc_solve_g. */
+void orc_solve_rows(int n, const double* q, const double* vel, const double* p,
+                    const uint8_t* adj, const double* gains, const uint16_t* P_in,
+                    const uint16_t* Prows, const acl_cntrl_gains_t* g,
+                    const acl_safety_params_t* s, int early_exit, uint16_t* P_out,
+                    acl_swarm_status_t* st, double* u, double* u_safe, uint8_t* ca,
+                    uint16_t* who_out, double* gate_margin);
 
 /* Batched solve over a thread pool (the CPU baseline). Swarm b uses
  * formation fidx[b]: p [F][n][3], adj [F][n][n], gains [F][3n][3n].

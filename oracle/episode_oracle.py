@@ -150,26 +150,30 @@ def is_perm(w):
 
 class SwarmState:
     """One swarm's assignment state across auctions: P (each vehicle's own
-    formation point), seed (the last agreed assignment: the next auction's
-    P_in) and tables (None while every vehicle holds one assignment, else
-    [n][n] per-vehicle inverse tables)."""
+    formation point) and tables (None while every vehicle holds one
+    assignment, else [n][n] per-vehicle inverse tables: row v = vehicle v's
+    own assignment as formation point -> vehicle)."""
 
     def __init__(self, P):
         self.P = np.array(P, np.uint16)
-        self.seed = self.P.copy()
         self.tables = None
 
     def copy(self):
         c = SwarmState(self.P)
-        c.seed = self.seed.copy()
         c.tables = None if self.tables is None else self.tables.copy()
         return c
+
+    def solve_args(self):
+        """(P_in, P_rows) of the swarm's next auction: every vehicle starts
+        from its own assignment (auctioneer.cpp:357,369,422-427) --
+        acl_solve_args_t::P_rows while the vehicles hold different ones."""
+        return self.P, self.tables
 
 
 def adopt(state, flush, res):
     """autoauctionCb's flush rule + each vehicle's adoption
     (auctioneer.cpp:250-295) for one swarm after an auction result `res`
-    (pyoracle.solve from state.seed). Mutates `state`; returns (flush, event)
+    (pyoracle.solve from state.solve_args()). Mutates `state`; returns (flush, event)
     with event one of 'skipped', 'adopted', 'invalid', 'disagree'.
 
     agree + valid: every vehicle adopts the one table. agree + invalid: every
@@ -177,9 +181,8 @@ def adopt(state, flush, res):
     (coordination_ros.cpp:339-345). Disagreement: each vehicle whose own final
     table is a permutation adopts it (its row of `who`), the others keep
     theirs; the swarm then flies per-vehicle tables until an agreed valid
-    auction (seed unchanged: the model seeds every vehicle's next alignment
-    with the last agreed assignment, where the reference aligns each vehicle
-    with its own P_).
+    auction, and each vehicle starts its next auction (alignment and
+    neighbours) from its own table, as the reference's vehicles do.
 
     Model limit: a vehicle whose own table is invalid after a disagreeing
     auction keeps its old table here; the reference's vehicle also sets
@@ -194,7 +197,6 @@ def adopt(state, flush, res):
     valid, agree = bool(fl & 0x01), bool(fl & 0x02)
     if agree and valid:
         state.P = res["P_out"].astype(np.uint16).copy()
-        state.seed = state.P.copy()
         state.tables = None
         return 0, "adopted"
     if agree:
@@ -247,8 +249,9 @@ class Auctions:
         self.counts = dict(skipped=0, auctions=0, adopted=0, invalid=0, disagree=0, restarted=0)
 
     def auto(self, step, state, solve):
-        """An auto-auction step; solve(seed) runs CBAA from the current q
-        with P_in = state.seed. Mutates `state`."""
+        """An auto-auction step; solve(P_in, P_rows) runs CBAA from the
+        current q with the vehicles' own assignments (state.solve_args()).
+        Mutates `state`."""
         if self.flush:
             self.flush = 0
             self.counts["skipped"] += 1
@@ -256,7 +259,7 @@ class Auctions:
         self.counts["auctions"] += 1
         if self.pending >= 0:
             self.counts["restarted"] += 1
-        self.res = solve(state.seed)
+        self.res = solve(*state.solve_args())
         if self.latency <= 0:
             self.pending = -1
             return self._complete(state)
@@ -288,7 +291,8 @@ def run_episode(q, vel, P, p, adj, gains, steps, ep, step0=0, g=None, s=None):
     for k in range(steps):
         step = step0 + k
         if step % ep["auction_every"] == 0:
-            auc.auto(step, st, lambda seed: O.solve(q, vel, p, adj, gains, seed, g, s))
+            auc.auto(step, st, lambda P_in, rows: O.solve(q, vel, p, adj, gains, P_in, g, s,
+                                                          P_rows=rows))
         else:
             auc.tick(step, st)
         u, us, ca = control_step(q, vel, p, adj, gains, st.P, g, s, st.tables)

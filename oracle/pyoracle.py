@@ -84,6 +84,9 @@ def lib():
                                 ct.POINTER(CntrlGains), ct.POINTER(SafetyParams),
                                 ct.c_int, U16, ct.POINTER(SwarmStatus), D, D, U8, U16]
         L.orc_solve_g.argtypes = L.orc_solve.argtypes + [D]
+        L.orc_solve_rows.argtypes = [ct.c_int, D, D, D, U8, D, U16, U16,
+                                     ct.POINTER(CntrlGains), ct.POINTER(SafetyParams),
+                                     ct.c_int, U16, ct.POINTER(SwarmStatus), D, D, U8, U16, D]
         L.orc_solve_batch.argtypes = [ct.c_int, ct.c_int, ct.c_int, I32, D, D, D,
                                       U8, D, U16, ct.POINTER(CntrlGains),
                                       ct.POINTER(SafetyParams), ct.c_int, U16,
@@ -210,8 +213,10 @@ def collision_avoidance(v, q, cmd, s=None):
     return c, bool(mod)
 
 
-def solve(q, vel, p, adj, gains, P_in, g=None, s=None, early_exit=True):
-    """One swarm. gains dense [3n][3n] row-major."""
+def solve(q, vel, p, adj, gains, P_in, g=None, s=None, early_exit=True, P_rows=None):
+    """One swarm. gains dense [3n][3n] row-major. P_rows (optional [n][n]):
+    row v = vehicle v's own assignment as formation point -> vehicle
+    (orc_solve_rows; acl_solve_args_t::P_rows)."""
     n = q.shape[0]
     g = g or default_gains(); s = s or default_safety()
     q = _c(q, np.float64); vel = _c(vel, np.float64); p = _c(p, np.float64)
@@ -220,11 +225,13 @@ def solve(q, vel, p, adj, gains, P_in, g=None, s=None, early_exit=True):
     u = np.zeros((n, 3)); us = np.zeros((n, 3)); ca = np.zeros(n, np.uint8)
     who = np.zeros((n, n), np.uint16)
     gm = np.zeros(1)
-    lib().orc_solve_g(n, _p(q, ct.c_double), _p(vel, ct.c_double), _p(p, ct.c_double),
-                      _p(adj, ct.c_uint8), _p(gains, ct.c_double), _p(P_in, ct.c_uint16),
-                      ct.byref(g), ct.byref(s), int(early_exit), _p(P_out, ct.c_uint16),
-                      ct.byref(st), _p(u, ct.c_double), _p(us, ct.c_double),
-                      _p(ca, ct.c_uint8), _p(who, ct.c_uint16), _p(gm, ct.c_double))
+    rows = None if P_rows is None else _c(P_rows, np.uint16)
+    lib().orc_solve_rows(n, _p(q, ct.c_double), _p(vel, ct.c_double), _p(p, ct.c_double),
+                         _p(adj, ct.c_uint8), _p(gains, ct.c_double), _p(P_in, ct.c_uint16),
+                         None if rows is None else _p(rows, ct.c_uint16),
+                         ct.byref(g), ct.byref(s), int(early_exit), _p(P_out, ct.c_uint16),
+                         ct.byref(st), _p(u, ct.c_double), _p(us, ct.c_double),
+                         _p(ca, ct.c_uint8), _p(who, ct.c_uint16), _p(gm, ct.c_double))
     status = {k: getattr(st, k) for k, _ in SwarmStatus._fields_}
     return dict(P_out=P_out, status=status, u=u, u_safe=us, ca=ca, who=who,
                 gate_margin=float(gm[0]))

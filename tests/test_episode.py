@@ -114,7 +114,8 @@ def test_adopt_rule():
     bad = {"P_out": newP, "status": {"flags": 0x02}, "who": who_new}
     st = E.SwarmState(P)
     assert E.adopt(st, 0, ok) == (0, "adopted") and (st.P == newP).all() and st.tables is None
-    assert (st.seed == newP).all()
+    P_in, rows = st.solve_args()
+    assert (P_in == newP).all() and rows is None  # the next auction: one shared P_in
     st = E.SwarmState(P)
     assert E.adopt(st, 0, bad) == (1, "invalid") and (st.P == P).all()
     assert E.adopt(st, 1, ok) == (0, "skipped") and (st.P == P).all()   # flushed: skipped
@@ -127,7 +128,10 @@ def test_adopt_rule():
     assert st.P.tolist() == [1, 1, 2, 3]          # own points: 0 and 1 adopted, 2, 3 kept
     assert st.tables[0].tolist() == [1, 0, 3, 2] and st.tables[1].tolist() == [0, 1, 2, 3]
     assert st.tables[2].tolist() == [0, 1, 2, 3] and st.tables[3].tolist() == [0, 1, 2, 3]
-    assert (st.seed == P).all()                   # the next auction's P_in
+    P_in, rows = st.solve_args()                  # the next auction: each vehicle's own
+    assert P_in.tolist() == [1, 1, 2, 3] and rows is st.tables
+    for v in range(4):
+        assert rows[v][P_in[v]] == v              # acl_solve_args_t::P_rows' contract
     # a second disagreement: the invalid vehicle keeps its own previous row
     who2 = np.array([[4, 4, 4, 4], [2, 3, 0, 1], [3, 2, 1, 0], [0, 1, 2, 3]], np.uint16)
     E.adopt(st, 0, {"P_out": None, "status": {"flags": 0x00}, "who": who2})

@@ -141,7 +141,8 @@ def test_episode_teacher_forced_parity(cuda, ci):
         conv = grid = -1
         for k in range(case["steps"]):
             if k % ep["auction_every"] == 0:
-                res = O.solve(qprev, vprev, p, adj, G, state.seed)
+                P_in, rows = state.solve_args()
+                res = O.solve(qprev, vprev, p, adj, G, P_in, P_rows=rows)
                 flush, ev = E.adopt(state, flush, res)
                 counts[ev] += 1
             assert (h["P"][k, b] == state.P).all(), (b, k)
@@ -253,7 +254,8 @@ def test_episode_auction_latency(cuda, lat, ci):
         qprev, vprev = case["q"][b], case["vel"][b]
         for k in range(case["steps"]):
             if k % ep["auction_every"] == 0:
-                auc.auto(k, state, lambda seed: O.solve(qprev, vprev, p, adj, G, seed))
+                auc.auto(k, state, lambda P_in, rows: O.solve(qprev, vprev, p, adj, G, P_in,
+                                                              P_rows=rows))
             else:
                 auc.tick(k, state)
             assert (h["P"][k, b] == state.P).all(), (lat, b, k)
@@ -302,7 +304,8 @@ def test_episode_zeroed_status_mid_period(cuda):
         for k in range(case["steps"]):
             s = 5 + k
             if s % ep["auction_every"] == 0:
-                auc.auto(s, state, lambda seed: O.solve(qprev, vprev, p, adj, G, seed))
+                auc.auto(s, state, lambda P_in, rows: O.solve(qprev, vprev, p, adj, G, P_in,
+                                                              P_rows=rows))
             else:
                 auc.tick(s, state)
             assert (h["P"][k, b] == state.P).all(), (b, k)
