@@ -551,11 +551,19 @@ __device__ __forceinline__ void align_chunk(int n, const double* pq, const unsig
   const double scale = lazy ? oon : 1.0;  // 1.0 * x == x
   const double a0 = lazy ? -0.0 : 0.0;
   double a00 = a0, a01 = a0, a10 = a0, a11 = a0;  // a(di, sj)
-  for_members<NC>(n, pq, r, [&](unsigned long long mk, const double (&v)[4]) {
-    const double e0 = v[0] - sm0, e1 = v[1] - sm1;
-    const double d0 = scale * (v[2] - dm0), d1 = scale * (v[3] - dm1);
-    masked_add4(mk, a00, a01, a10, a11, d0 * e0, d0 * e1, d1 * e0, d1 * e1);
-  });
+  if (__any(act && lazy)) {
+    for_members<NC>(n, pq, r, [&](unsigned long long mk, const double (&v)[4]) {
+      const double e0 = v[0] - sm0, e1 = v[1] - sm1;
+      const double d0 = scale * (v[2] - dm0), d1 = scale * (v[3] - dm1);
+      masked_add4(mk, a00, a01, a10, a11, d0 * e0, d0 * e1, d1 * e0, d1 * e1);
+    });
+  } else {  // every item in the GEMM form: scale is 1.0 and 1.0 * x == x
+    for_members<NC>(n, pq, r, [&](unsigned long long mk, const double (&v)[4]) {
+      const double e0 = v[0] - sm0, e1 = v[1] - sm1;
+      const double d0 = v[2] - dm0, d1 = v[3] - dm1;
+      masked_add4(mk, a00, a01, a10, a11, d0 * e0, d0 * e1, d1 * e0, d1 * e1);
+    });
+  }
   if (act) {
     // column-major sigma S(di, sj)
     const double S[4] = {lazy ? a00 : a00 * oon, lazy ? a10 : a10 * oon,

@@ -234,13 +234,17 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
     for (int i0 = 0; i0 < R; i0 += 64) {
       const int i = i0 + lane;
       const int cnt = (i < R) ? __popcll(adjF[2 * i]) + __popcll(adjF[2 * i + 1]) : 0;
+      // inclusive prefix on DPP (row_shr 1, 2, 4, 8, then row_bcast 15 / 31):
+      // no ds_bpermute round trips while the other waves wait at the barrier
       int x = cnt;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-      }
+      x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);
+      x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);
+      x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);
+      x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);
+      x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);
+      x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);
       if (i < R) rowb[i] = base + x - cnt;
-      base += __shfl(x, 63, 64);
+      base += __builtin_amdgcn_readlane(x, 63);
     }
     if (lane == 0) rowb[R] = base;
   }
