@@ -383,13 +383,16 @@ __device__ __forceinline__ void wide_control(KCtlParams* Pp, int b, int f, unsig
       int cnt = 0;
       if (i < n)
         for (int w = 0; w < NW; ++w) cnt += __popcll(adjF[i * NW + w]);
+      // inclusive prefix on DPP (row_shr 1, 2, 4, 8, then row_bcast 15 / 31)
       int x = cnt;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-      }
+      x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);
+      x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);
+      x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);
+      x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);
+      x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);
+      x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);
       if (i < n) rowbase[i] = base + x - cnt;
-      base += __shfl(x, 63, 64);
+      base += __builtin_amdgcn_readlane(x, 63);
     }
     if (lane == 0) rowbase[n] = base;
   }
