@@ -87,7 +87,9 @@ if ok.any():
 # CBAA column-step sections (a -DACL_AUCTION_PROF=1 build): cycles summed
 # over a swarm's waves, and the counts of evaluated columns, walks and scans
 sec = st.cpu().numpy()[:, SEC:SEC + 9].astype(np.uint64)
-if args.n <= 128 and (not args.crowd or args.no_control) and sec[:, :8].any():
+# (n <= 128: ca_pair_kernel writes no stamps, so the slots are the CBAA's
+# with collision avoidance on as well)
+if args.n <= 128 and sec[:, :8].any():
     SN = ["level 0", "levels", "margin bound", "runner-up walk", "exact scan", "write-back",
           "selects+barrier", "column barrier"]
     tot8 = sec[:, :8].astype(np.float64).sum()
@@ -123,8 +125,9 @@ if args.n > 128 and sec[:, :4].any():
         g = lambda sh: ((spc >> np.uint64(sh)) & m21).astype(float).mean()
         print(f"  column updates per swarm: sparse {g(0):.1f}, dense {g(21):.1f}, "
               f"sparse -> dense {g(42):.1f}")
-# collision avoidance (a -DACL_CA_PROF=1 build, --crowd): ca_kernel wave-cycles
-if args.crowd and not args.no_control:
+# collision avoidance (a -DACL_CA_PROF=1 build, --crowd, n > 128): ca_kernel
+# wave-cycles (ca_pair_kernel, n <= 128, has no such counters)
+if args.crowd and not args.no_control and args.n > 128:
     x = st.cpu().numpy()[:, SEC + 8:SEC + 12].astype(np.float64)
     cnt = x[:, 3].sum()
     print(f"  ca close vehicles {cnt:.0f} ({cnt / args.B:.1f} per swarm)")
