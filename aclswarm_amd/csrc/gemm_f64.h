@@ -27,6 +27,8 @@
 // load/store is a contiguous 128-byte column segment.
 #pragma once
 
+#include <type_traits>
+
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
@@ -93,6 +95,9 @@ constexpr int kGemmKStep = 16;
 #endif
 #ifndef ACL_GEMM_DMA_WAVES
 #define ACL_GEMM_DMA_WAVES 3  // the 80-tile kernel's occupancy bound (waves per SIMD)
+#endif
+#ifndef ACL_GEMM_EDGE
+#define ACL_GEMM_EDGE 1  // an edge tile skips its 16-blocks outside the matrix
 #endif
 #ifndef ACL_GEMM_TILE_DEFAULT
 #define ACL_GEMM_TILE_DEFAULT 80  // the four-wave 80 tile
@@ -401,6 +406,12 @@ __global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
   // the block diagonal are computed (diag_blocks below), each one off the
   // diagonal stored twice
   const bool dtile = SYM && bi == bj;
+  // an edge tile (ACL_GEMM_EDGE): only its row / column blocks inside the
+  // matrix run their MFMAs (the others would multiply zero-filled operands
+  // into outputs that are never stored); workgroup-uniform, so the K loops
+  // are instantiated for edge and interior tiles apart
+  const int mbk = min(5, (J.m - m0 + 15) >> 4), nbk = min(5, (J.n - n0 + 15) >> 4);
+  const bool edge = ACL_GEMM_EDGE && (mbk < 5 || nbk < 5);
   if (flops && threadIdx.x == 0) {
     unsigned long long mn = 0;
     if (dtile) {
@@ -630,8 +641,9 @@ __global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
     // Diagonal tile: blocks (r, c), r <= c, dealt 4 / 4 / 4 / 3 over the
     // waves (diag_blocks), each block's full K on one wave; the blocks below
     // the diagonal are the mirrors of the ones above it
-    auto diag = [&](auto WC) {
+    auto diag = [&](auto WC, auto EC) {
       constexpr int W = decltype(WC)::value;
+      constexpr bool EDGE = decltype(EC)::value;
       constexpr int NQ = W == 3 ? 3 : 4;
       constexpr int RB[4][4] = {{0, 0, 0, 0}, {1, 1, 1, 1}, {2, 2, 2, 0}, {3, 3, 4, 4}};
       constexpr int CB[4][4] = {{0, 1, 2, 3}, {1, 2, 3, 4}, {2, 3, 4, 4}, {3, 4, 4, 4}};
@@ -644,9 +656,10 @@ __global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
           const int kr = k4 + (lane >> 4);
 #pragma unroll
           for (int q = 0; q < NQ; ++q)
-            dacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(b_at(cur, kr, CB[W][q] * 16 + (lane & 15)),
-                                                          a_at(cur, kr, RB[W][q] * 16 + (lane & 15)),
-                                                          dacc[q], 0, 0, 0);
+            if (!EDGE || (RB[W][q] < mbk && CB[W][q] < nbk))
+              dacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                  b_at(cur, kr, CB[W][q] * 16 + (lane & 15)),
+                  a_at(cur, kr, RB[W][q] * 16 + (lane & 15)), dacc[q], 0, 0, 0);
         }
       };
       if constexpr (DMA) {
@@ -683,12 +696,15 @@ __global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
           put_at(RB[W][q], CB[W][q], r, dacc[q][r], RB[W][q] != CB[W][q], alpha, beta, e2, tr);
       finish(e2, tr);
     };
+#define ACL_DIAG(W_) \
+  (edge ? diag(GemmWave<W_>{}, std::true_type{}) : diag(GemmWave<W_>{}, std::false_type{}))
     switch (__builtin_amdgcn_readfirstlane(wave)) {
-      case 0: diag(GemmWave<0>{}); break;
-      case 1: diag(GemmWave<1>{}); break;
-      case 2: diag(GemmWave<2>{}); break;
-      default: diag(GemmWave<3>{}); break;
+      case 0: ACL_DIAG(0); break;
+      case 1: ACL_DIAG(1); break;
+      case 2: ACL_DIAG(2); break;
+      default: ACL_DIAG(3); break;
     }
+#undef ACL_DIAG
     return;
   }
   f64x4 acc[NB], acc4w = f64x4{0.0, 0.0, 0.0, 0.0}, acc44 = f64x4{0.0, 0.0, 0.0, 0.0};
@@ -698,8 +714,9 @@ __global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
   // operand and the k4 step of block (4, 4) are then compile-time choices
   // (no selects, no exec-masked MFMA); ACL_GEMM_OPF: each k4 step's LDS
   // operands are read one step ahead, while the previous step's MFMAs run.
-  auto kloop = [&](auto WC) {
+  auto kloop = [&](auto WC, auto EC) {
     constexpr int WS = decltype(WC)::value;  // -1: the wave index at run time
+    constexpr bool EDGE = decltype(EC)::value;
     const int w = WS >= 0 ? WS : wave;
     struct Ops {
       double av, a4, bv[NB];
@@ -714,10 +731,12 @@ __global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
     auto mm = [&](int k4, const Ops& o) {
 #pragma unroll
       for (int b = 0; b < NB; ++b)
-        acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.bv[b], o.av, acc[b], 0, 0, 0);
+        if (!EDGE || (w < mbk && b < nbk))
+          acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.bv[b], o.av, acc[b], 0, 0, 0);
       if constexpr (WS >= 0) {
-        acc4w = __builtin_amdgcn_mfma_f64_16x16x4f64(o.bv[WS], o.a4, acc4w, 0, 0, 0);
-        if (k4 == 4 * WS)  // block (4, 4) on this wave's k4 step
+        if (!EDGE || (4 < mbk && WS < nbk))
+          acc4w = __builtin_amdgcn_mfma_f64_16x16x4f64(o.bv[WS], o.a4, acc4w, 0, 0, 0);
+        if (k4 == 4 * WS && (!EDGE || (4 < mbk && 4 < nbk)))  // block (4, 4) on this wave's k4 step
           acc44 = __builtin_amdgcn_mfma_f64_16x16x4f64(o.bv[4], o.a4, acc44, 0, 0, 0);
       } else {
         // block (4, w): B column block w (a wave-uniform index: select, no
@@ -792,16 +811,19 @@ __global__ void __launch_bounds__(256, ACL_GEMM_DMA_WAVES) gemm80w4_f64_kernel(
       __syncthreads();
     }
   };
+#define ACL_KLOOP(W_) \
+  (edge ? kloop(GemmWave<W_>{}, std::true_type{}) : kloop(GemmWave<W_>{}, std::false_type{}))
   if constexpr (ACL_GEMM_WSPEC) {
     switch (__builtin_amdgcn_readfirstlane(wave)) {
-      case 0: kloop(GemmWave<0>{}); break;
-      case 1: kloop(GemmWave<1>{}); break;
-      case 2: kloop(GemmWave<2>{}); break;
-      default: kloop(GemmWave<3>{}); break;
+      case 0: ACL_KLOOP(0); break;
+      case 1: ACL_KLOOP(1); break;
+      case 2: ACL_KLOOP(2); break;
+      default: ACL_KLOOP(3); break;
     }
   } else {
-    kloop(GemmWave<-1>{});
+    ACL_KLOOP(-1);
   }
+#undef ACL_KLOOP
   // (4, 4): the four partial sums through LDS (the A buffer is free), added in
   // wave order
   double* red = &Ash[0][0];
