@@ -31,9 +31,10 @@
 //   * the first collision test's candidate search from the pair loop's own q
 //     differences: a conservative test (the squared xy distance, contracted,
 //     against (thr (1 + 2^-40))^2) flags the formation rows that need the
-//     exact test, which the epilogue then runs as gain_epilogue does; a
-//     vehicle not flagged has no other vehicle within the threshold, so the
-//     outcome is the same, without an n^2 loop per swarm.
+//     exact test, which every thread of the workgroup then runs on a share
+//     of the rows (gain_epilogue's test); a vehicle not flagged has no other
+//     vehicle within the threshold, so the outcome is the same, without an
+//     n^2 loop per swarm.
 // Gates, gate margin and collision flags are decided by the same expressions
 // as in pair_gain_swarm (bit-identical); u / u_safe are tolerance parity.
 #pragma once
@@ -43,7 +44,7 @@
 namespace acl_amd {
 
 struct FusedLayout {
-  int pt, adj, etab, rowb, Pt, Pinv, acc, atab, cst, nearb, flags, gmw, caw, total;
+  int pt, adj, etab, rowb, Pt, Pinv, acc, atab, cst, nearb, clf, flags, gmw, caw, total;
 };
 
 // the pair loop's constants (FusedLayout::cst), read from LDS where they are
@@ -67,6 +68,7 @@ __host__ __device__ inline FusedLayout make_fused_layout(int n, int kW) {
   L.atab = o;  o = cal16(o + ACL_ATAB_N * 8);
   L.cst = o;   o = cal16(o + FC_N * 8);        // the pair loop's constants (FC_*)
   L.nearb = o; o = cal16(o + 4 * 4);           // [4] u32: rows flagged for the exact test
+  L.clf = o;   o = cal16(o + R * 4);           // [R] u32: vehicle close (the exact test's result)
   L.flags = o; o = cal16(o + 4);               // bit 0: a q coordinate is not finite
   L.gmw = o;   o = o + 8;                      // gate margin word
   L.caw = o;   o = cal16(o + 4);               // the swarm is on the collision list
@@ -168,6 +170,7 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
   double* atab = reinterpret_cast<double*>(smem + L.atab);
   double* cst = reinterpret_cast<double*>(smem + L.cst);
   unsigned* nearb = reinterpret_cast<unsigned*>(smem + L.nearb);
+  unsigned* clf = reinterpret_cast<unsigned*>(smem + L.clf);
   unsigned* flags = reinterpret_cast<unsigned*>(smem + L.flags);
   unsigned long long& gmw = *reinterpret_cast<unsigned long long*>(smem + L.gmw);
   unsigned* caw = reinterpret_cast<unsigned*>(smem + L.caw);
@@ -181,6 +184,7 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
     *flags = 0u;
   }
   if (tid < 4) nearb[tid] = 0u;
+  for (int k = tid; k < R; k += nthreads) clf[k] = 0u;
   if (tid < FC_N) {
     const double thr_hi = P.s.d_avoid_thresh * (1.0 + 0x1p-40);
     const double v[FC_N] = {P.g.K1_xy, P.g.K2_xy, P.g.K1_z, P.g.K2_z,
@@ -421,6 +425,34 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
   }
   __syncthreads();
   if (GM && tid == 0) P.gate_margin[b] = __longlong_as_double((long long)gmw);
+  // the first collision test's exact pass over the rows the pair loop
+  // flagged, on every thread: vehicle v = tid mod n against the rows
+  // tid / n, + per, ... (gain_epilogue's test; OR over the rows, any order)
+  // -- a crowded swarm's n x n tests on all of the workgroup's waves, not
+  // on the per-vehicle loop's first ones. A swarm without a flagged row (the
+  // usual case) skips the pass and its barrier (workgroup-uniform: nearb is
+  // complete after the pair loop's barrier).
+  if (nearb[0] | nearb[1] | nearb[2] | nearb[3]) {
+    const double thr = P.s.d_avoid_thresh;
+    const double thr_hi = thr * (1.0 + 0x1p-40);
+    const double thr2hi = thr_hi * thr_hi;
+    const int per = nthreads / n;  // >= 1: n <= nthreads
+    const int v = tid % n, j0 = tid / n;
+    if (j0 < per) {
+      const int i = Pinv[v];
+      if ((nearb[i >> 5] >> (i & 31)) & 1u) {
+        const double qv0 = pt[8 * i], qv1 = pt[8 * i + 1];
+        bool c = false;
+        for (int k = j0; k < n; k += per) {
+          const double dx = pt[8 * k] - qv0, dy = pt[8 * k + 1] - qv1;
+          const double d2 = dx * dx + dy * dy;
+          if (k != i && !(d2 > thr2hi)) c |= !(sqrt(d2) > thr);
+        }
+        if (c) clf[v] = 1u;
+      }
+    }
+    __syncthreads();
+  }
 
   // ---- per vehicle: u = kp (the kW waves' sums, in wave order) + kd (-vel)
   // once per edge of its row (distcntrl.cpp:85-95); saturation and the
@@ -428,8 +460,6 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
   {
     const acl_cntrl_gains_t g = kgains(P);
     const acl_safety_params_t sp = ksafety(P);
-    const double thr_hi = sp.d_avoid_thresh * (1.0 + 0x1p-40);
-    const double thr2hi = thr_hi * thr_hi;
     const int NW = (n + 63) >> 6;
     for (int v = tid; v < n; v += nthreads) {
       const int i = Pinv[v];
@@ -454,16 +484,7 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
       gu[1] = cmd1;
       gu[2] = cmd2;
       saturate(sp, cmd0, cmd1, cmd2);
-      bool close = false;
-      if ((nearb[i >> 5] >> (i & 31)) & 1u) {
-        // the exact test of gain_epilogue (vehicle order there; the same pairs)
-        const double qv0 = pt[8 * i], qv1 = pt[8 * i + 1];
-        for (int k = 0; k < n; ++k) {
-          const double dx = pt[8 * k] - qv0, dy = pt[8 * k + 1] - qv1;
-          const double d2 = dx * dx + dy * dy;
-          if (k != i && !(d2 > thr2hi)) close |= !(sqrt(d2) > sp.d_avoid_thresh);
-        }
-      }
+      const bool close = clf[v] != 0u;  // (the exact pass above)
       if (P.u_safe) {
         double* o = P.u_safe + ((size_t)b * n + v) * 3;
         o[0] = cmd0;
