@@ -44,7 +44,7 @@
 namespace acl_amd {
 
 struct FusedLayout {
-  int pt, adj, etab, rowb, Pt, Pinv, acc, atab, cst, nearb, clf, flags, gmw, caw, total;
+  int pt, adj, etab, rowb, Pt, Pinv, acc, atab, cst, nearb, clf, vel, flags, gmw, caw, total;
 };
 
 // the pair loop's constants (FusedLayout::cst), read from LDS where they are
@@ -69,6 +69,7 @@ __host__ __device__ inline FusedLayout make_fused_layout(int n, int kW) {
   L.cst = o;   o = cal16(o + FC_N * 8);        // the pair loop's constants (FC_*)
   L.nearb = o; o = cal16(o + 4 * 4);           // [4] u32: rows flagged for the exact test
   L.clf = o;   o = cal16(o + R * 4);           // [R] u32: vehicle close (the exact test's result)
+  L.vel = o;   o = cal16(o + n * 24);          // [n][3] f64 vel per vehicle (loaded with q)
   L.flags = o; o = cal16(o + 4);               // bit 0: a q coordinate is not finite
   L.gmw = o;   o = o + 8;                      // gate margin word
   L.caw = o;   o = cal16(o + 4);               // the swarm is on the collision list
@@ -171,6 +172,7 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
   double* cst = reinterpret_cast<double*>(smem + L.cst);
   unsigned* nearb = reinterpret_cast<unsigned*>(smem + L.nearb);
   unsigned* clf = reinterpret_cast<unsigned*>(smem + L.clf);
+  double* velv = reinterpret_cast<double*>(smem + L.vel);
   unsigned* flags = reinterpret_cast<unsigned*>(smem + L.flags);
   unsigned long long& gmw = *reinterpret_cast<unsigned long long*>(smem + L.gmw);
   unsigned* caw = reinterpret_cast<unsigned*>(smem + L.caw);
@@ -211,6 +213,12 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
         row[0] = gq[3 * v];
         row[1] = gq[3 * v + 1];
         row[2] = gq[3 * v + 2];
+        // the epilogue's damping term reads the vehicle's vel: loaded here,
+        // in the same round trip as q, instead of after the pair loop
+        const double* gvel = P.vel + ((size_t)b * n + v) * 3;
+        velv[3 * v] = gvel[0];
+        velv[3 * v + 1] = gvel[1];
+        velv[3 * v + 2] = gvel[2];
         const double x = gp[3 * i], y = gp[3 * i + 1], z = gp[3 * i + 2];
         row[3] = x;
         row[4] = y;
@@ -473,7 +481,7 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
       }
       double cmd0 = g.kp * s0, cmd1 = g.kp * s1, cmd2 = g.kp * s2;
       if (deg) {
-        const double* gv = P.vel + ((size_t)b * n + v) * 3;
+        const double* gv = velv + 3 * v;
         const double cn = (double)deg;
         cmd0 += cn * (g.kd * (-gv[0]));
         cmd1 += cn * (g.kd * (-gv[1]));
