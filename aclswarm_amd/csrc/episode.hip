@@ -112,7 +112,9 @@ __global__ void __launch_bounds__(64) latency_kernel(int n, const int32_t* fidx,
 // vehicle whose own final table is valid adopts it (its row of the auction's
 // per-vehicle hand-off, vvalid), the others keep their own, and the swarm
 // flies per-vehicle tables (control mode 1, est.per_vehicle) until an agreed
-// valid auction. The control hand-off (ctlPt / ctlMode / ctlRows, and the
+// valid auction; when any vehicle was left on an invalid table, the swarm's
+// next auto-auction is skipped too (that vehicle flushes instead of starting,
+// and the others' auction stalls on its START bid). The control hand-off (ctlPt / ctlMode / ctlRows, and the
 // control status cst) is written here, so no hand-off pass runs per step.
 struct AdoptArgs {
   int n, step, mode;
@@ -163,7 +165,14 @@ __global__ void __launch_bounds__(256) adopt_kernel(const AdoptArgs A) {
         ++e.n_invalid;
       } else {
         ++e.n_disagree;
-        if (s.n_invalid < n && !(s.flags & ACL_SWARM_BAD_INPUT)) take = 2;
+        const bool bad = (s.flags & ACL_SWARM_BAD_INPUT) != 0;
+        if (s.n_invalid < n && !bad) take = 2;
+        // a vehicle left on an invalid table sets invalid_assignment_
+        // (auctioneer.cpp:291) and skips its next start; its neighbours'
+        // auction then waits on its START bid (bidIterComplete,
+        // auctioneer.cpp:419-439) until they restart at the tick after: the
+        // swarm's next auction completes nowhere -- the flush rule
+        if (s.n_invalid > 0 && !bad) A.flush[b] = 1;
       }
     }
     A.est[b] = e;

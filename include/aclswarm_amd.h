@@ -451,14 +451,15 @@ acl_status_t acl_hungarian_batch(const acl_formations_t* formations,
  *      an agreed valid result is adopted by every vehicle; an agreed invalid
  *      one sets `flush`; on disagreement each vehicle whose own final table
  *      is valid adopts it and the others keep theirs -- the swarm then flies
- *      per-vehicle tables (est.per_vehicle) until an agreed valid auction
- *      (model limit: a vehicle whose own table is invalid after a disagreeing auction
- *      only keeps its old table, where the reference's vehicle also sets
- *      invalid_assignment_ (auctioneer.cpp:291) and flushes and skips its
- *      next auto-auction alone (coordination_ros.cpp:339-345) -- a per-vehicle
- *      skip the lockstep auction does not model, so episodes in which a
- *      vehicle ends a disagreeing auction on an invalid table have parity
- *      unpinned from that auction on);
+ *      per-vehicle tables (est.per_vehicle) until an agreed valid auction.
+ *      A vehicle whose own table is invalid after a disagreeing auction keeps
+ *      its old table and sets invalid_assignment_ (auctioneer.cpp:291): it
+ *      flushes instead of starting the next auto-auction (:339-345), the
+ *      others' auction stalls on its START bid (auctioneer.cpp:419-439) until
+ *      the tick after, so `flush` is set and the swarm skips that auction
+ *      (model limit: the stalled auction's stale START bids in the
+ *      reference's queues, and a formation graph with several components,
+ *      where only the flagged vehicle's component stalls, are not modelled);
  *   2. DistCntrl::compute with each vehicle's table and vel (controlCb,
  *      coordination_ros.cpp:365-378), Safety::cmdinCb saturation and collisionAvoidance
  *      (safety.cpp:172-197,412-541) -> the velocity goal;

@@ -184,13 +184,17 @@ def adopt(state, flush, res):
     auction, and each vehicle starts its next auction (alignment and
     neighbours) from its own table, as the reference's vehicles do.
 
-    Model limit: a vehicle whose own table is invalid after a disagreeing
-    auction keeps its old table here; the reference's vehicle also sets
-    invalid_assignment_ (auctioneer.cpp:291) and flushes and skips its next
-    auto-auction on its own (coordination_ros.cpp:339-345), a per-vehicle
-    skip the lockstep auction does not model. Parity is unpinned for the
-    auctions after such an event (the swarm-level skip is modelled only for
-    an agreed invalid result)."""
+    A vehicle whose own table is invalid after a disagreeing auction keeps
+    its old table and sets invalid_assignment_ (auctioneer.cpp:291): at the
+    next auto-auction it flushes instead of starting (coordination_ros.cpp:
+    339-345), so its neighbours wait on its START bid (bidIterComplete,
+    auctioneer.cpp:419-439) and, through them, the whole (connected) swarm's
+    auction completes nowhere until every vehicle restarts at the tick after
+    (:355-358). The lockstep model: the swarm skips its next auto-auction,
+    as after an agreed invalid result. Model limit: stale START bids the
+    stalled auction leaves in the reference's queues are not modelled, and a
+    formation graph with several components stalls only the flagged
+    vehicle's component there (here the whole swarm)."""
     if flush:
         return 0, "skipped"
     fl = res["status"]["flags"]
@@ -214,7 +218,8 @@ def adopt(state, flush, res):
                 P[v] = int(np.nonzero(who[v] == v)[0][0])
         state.tables = cur.astype(np.uint16)
         state.P = P
-    return 0, "disagree"
+    bad = bool(fl & 0x10)  # ACL_SWARM_BAD_INPUT
+    return (0 if all(vv) or bad else 1), "disagree"
 
 
 AUCTIONEER_DT = 0.001  # coordination.launch:23: one bid processed per tick

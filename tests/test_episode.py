@@ -124,7 +124,9 @@ def test_adopt_rule():
     who = np.array([[1, 0, 3, 2], [0, 1, 2, 3], [1, 0, 4, 4], [4, 4, 4, 4]], np.uint16)
     dis = {"P_out": np.array([1, 1, 2, 3], np.uint16), "status": {"flags": 0x00}, "who": who}
     st = E.SwarmState(P)
-    assert E.adopt(st, 0, dis) == (0, "disagree")
+    # vehicles 2 and 3 set invalid_assignment_ (auctioneer.cpp:291): the
+    # swarm's next auto-auction stalls on them and is skipped (flush = 1)
+    assert E.adopt(st, 0, dis) == (1, "disagree")
     assert st.P.tolist() == [1, 1, 2, 3]          # own points: 0 and 1 adopted, 2, 3 kept
     assert st.tables[0].tolist() == [1, 0, 3, 2] and st.tables[1].tolist() == [0, 1, 2, 3]
     assert st.tables[2].tolist() == [0, 1, 2, 3] and st.tables[3].tolist() == [0, 1, 2, 3]
@@ -134,9 +136,12 @@ def test_adopt_rule():
         assert rows[v][P_in[v]] == v              # acl_solve_args_t::P_rows' contract
     # a second disagreement: the invalid vehicle keeps its own previous row
     who2 = np.array([[4, 4, 4, 4], [2, 3, 0, 1], [3, 2, 1, 0], [0, 1, 2, 3]], np.uint16)
-    E.adopt(st, 0, {"P_out": None, "status": {"flags": 0x00}, "who": who2})
+    assert E.adopt(st, 0, {"P_out": None, "status": {"flags": 0x00}, "who": who2}) == (1, "disagree")
     assert st.tables[0].tolist() == [1, 0, 3, 2] and st.P[0] == 1
     assert st.tables[1].tolist() == [2, 3, 0, 1] and st.P[1] == 3
+    # a disagreement with every table valid sets no flush
+    who3 = np.stack([E.inverse(newP), E.inverse(P), E.inverse(P), E.inverse(newP)])
+    assert E.adopt(st, 0, {"P_out": None, "status": {"flags": 0x00}, "who": who3}) == (0, "disagree")
     # agreement clears the per-vehicle state
     assert E.adopt(st, 0, ok) == (0, "adopted") and st.tables is None
 

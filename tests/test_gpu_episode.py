@@ -130,7 +130,7 @@ def test_episode_teacher_forced_parity(cuda, ci):
     est = e.status()
     ep = E.params_from_struct(eps)
     B, n = case["q"].shape[:2]
-    n_adopt = n_ca = n_dis = 0
+    n_adopt = n_ca = n_dis = n_skip = 0
     for b in range(B):
         f = case["fidx"][b]
         p, adj, G = case["pts"][f], case["adj"][f], case["gains"][f]
@@ -170,8 +170,10 @@ def test_episode_teacher_forced_parity(cuda, ci):
         assert st["per_vehicle"] == int(state.tables is not None)
         n_adopt += counts["adopted"]
         n_dis += counts["disagree"]
+        n_skip += counts["skipped"]
     if case.get("disagree"):
         assert n_dis > 0         # the chain formations end auctions on different tables
+        assert n_skip > 0        # ... with vehicles on invalid ones: the next auction stalls
     else:
         assert n_adopt > 0
     if ci == 1:
