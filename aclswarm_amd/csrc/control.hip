@@ -740,7 +740,13 @@ __device__ __forceinline__ bool ca_resolve_serial(int nslot, double* caA, signed
 }
 
 #ifndef ACL_CA_GRID
-#define ACL_CA_GRID 2048
+#define ACL_CA_GRID 2048  // ca_kernel's workgroups at most (a grid-stride loop over the list)
+#endif
+// ca_pair_kernel's: more workgroups than the CU can hold, so the dispatcher
+// evens out swarms of unequal work (crowded C3 15.60 -> 15.43 ms, the
+// uncrowded launch unchanged; profiles/r5_ab_cagrid/)
+#ifndef ACL_CA_PAIR_GRID
+#define ACL_CA_PAIR_GRID 8192
 #endif
 // diagnostic build (-DACL_CA_PROF=1, scripts/phase_profile.py --crowd): wave
 // cycles of the sector build, the resolution and the rest into
@@ -1579,7 +1585,7 @@ hipError_t launch_control(const CtlParams& P, int nb, int which, hipStream_t str
 #endif
     if (P.n <= kMaxN && P.n >= ACL_CA_PAIR_MIN_N) {
       const int lp = ca_pair_layout(P.n).total;
-      hipLaunchKernelGGL(ca_pair_kernel, dim3(nb < ACL_CA_GRID ? nb : ACL_CA_GRID), dim3(kCaPT), lp,
+      hipLaunchKernelGGL(ca_pair_kernel, dim3(nb < ACL_CA_PAIR_GRID ? nb : ACL_CA_PAIR_GRID), dim3(kCaPT), lp,
                          stream, P);
       return hipGetLastError();
     }
