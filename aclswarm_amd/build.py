@@ -19,7 +19,13 @@ DRIVER = os.path.join(HERE, "lib", "libfacade_driver.so")
 CG_DRIVER_SRC = os.path.join(ROOT, "tests", "codegen_driver.cpp")
 CG_DRIVER = os.path.join(HERE, "lib", "libcodegen_driver.so")
 SOURCES = ["solve.hip", "auction.hip", "solve_wide.hip", "control.hip", "admm.hip", "hungarian.hip", "episode.hip",
-           "formation_gen.hip", "api.cpp", "codegen_api.cpp"]
+           "formation_gen.hip", "api.cpp"]
+# The generated ADMM library's C++ entry points (ADMMGainDesign3D and the
+# generic MATLAB-Coder emx utilities) live in their own shim library linked to
+# the core, so a process that loads libaclswarm_amd.so next to another
+# Coder-generated library does not get these common names interposed.
+CODEGEN_SRC = os.path.join(CSRC, "codegen_api.cpp")
+CODEGEN_OUT = os.path.join(HERE, "lib", "libaclswarm_amd_codegen.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
          "-fPIC", "-shared", "-Wall", "-Wno-unused-function"]
@@ -71,14 +77,13 @@ def _compile_objects(force, verbose, extra=()):
     return objs
 
 
-def _gxx_driver(src, out, incs, deps, force, verbose):
+def _gxx_driver(src, out, incs, deps, force, verbose, libs=("aclswarm_amd",)):
     if not force and os.path.exists(out) and all(
             os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
         return out
     cmd = (["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fPIC", "-shared"] +
-           ["-I" + i for i in incs] +
-           [src, "-L" + os.path.dirname(OUT), "-laclswarm_amd", "-Wl,-rpath,$ORIGIN",
-            "-o", out + ".tmp"])
+           ["-I" + i for i in incs] + [src, "-L" + os.path.dirname(OUT)] +
+           ["-l" + x for x in libs] + ["-Wl,-rpath,$ORIGIN", "-o", out + ".tmp"])
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
@@ -90,10 +95,30 @@ def build_driver(force=False, verbose=False):
     """g++ against the library, found next to the binary ($ORIGIN): the C++
     facade exerciser and the codegen-entry-point driver."""
     inc = os.path.join(ROOT, "include")
+    build_codegen(force, verbose)
     _gxx_driver(CG_DRIVER_SRC, CG_DRIVER, [os.path.join(inc, "codegen_admm")],
-                [CG_DRIVER_SRC, OUT, os.path.join(inc, "aclswarm_amd_codegen.h")], force, verbose)
+                [CG_DRIVER_SRC, OUT, CODEGEN_OUT, os.path.join(inc, "aclswarm_amd_codegen.h")],
+                force, verbose, libs=("aclswarm_amd_codegen", "aclswarm_amd"))
     return _gxx_driver(DRIVER_SRC, DRIVER, [inc],
                        [DRIVER_SRC, OUT, os.path.join(inc, "aclswarm_amd.hpp")], force, verbose)
+
+
+def build_codegen(force=False, verbose=False):
+    """libaclswarm_amd_codegen.so: the codegen entry points over the core's C
+    ABI (host code only), found next to the core ($ORIGIN)."""
+    deps = [CODEGEN_SRC, OUT, os.path.join(ROOT, "include", "aclswarm_amd.h"),
+            os.path.join(ROOT, "include", "aclswarm_amd_codegen.h")]
+    if not force and os.path.exists(CODEGEN_OUT) and all(
+            os.path.getmtime(d) <= os.path.getmtime(CODEGEN_OUT) for d in deps):
+        return CODEGEN_OUT
+    cmd = (["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fPIC", "-shared",
+            CODEGEN_SRC, "-L" + os.path.dirname(OUT), "-laclswarm_amd", "-Wl,-rpath,$ORIGIN",
+            "-o", CODEGEN_OUT + ".tmp"])
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(CODEGEN_OUT + ".tmp", CODEGEN_OUT)
+    return CODEGEN_OUT
 
 
 def build(force=False, verbose=False):

@@ -768,6 +768,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     }
   }
   __syncthreads();
+  // (M_BAD is final here: the own-row checks below report into M_ROWBAD, so
+  // no wave's entry test sees another wave's write and the barrier inside
+  // stays workgroup-uniform)
   if (rowsm && !misc[M_BAD]) {
     // each vehicle's own row: checked, its neighbourhood mask and its
     // alignment (thread v; align_own_row), the alignment at out[Pin[v]] with
@@ -784,7 +787,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
             y = qf[3 * Pin[u] + 1];
           },
           nbm, out + 6 * i, galign);
-      if (!ok) misc[M_BAD] = 1;
+      if (!ok) misc[M_ROWBAD] = 1;
       vadj[2 * v] = nbm[0];
       vadj[2 * v + 1] = nbm[1];
     }
@@ -792,7 +795,7 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     block_min_gap(margw, galign);
     __syncthreads();
   }
-  if (misc[M_BAD]) {
+  if (misc[M_BAD] | misc[M_ROWBAD]) {
     // P_in is not a permutation (or fidx is out of range): nothing is solved
     for (int v = tid; v < n; v += kAB) {
       P.P_out[(size_t)b * n + v] = P.P_in[(size_t)b * n + v];

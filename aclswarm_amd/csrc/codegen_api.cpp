@@ -7,9 +7,9 @@
 // inputs, ADMMGainDesign3D, emxFree_real_T. These are the same functions with
 // C++ linkage; the design itself is one formation of the batched solver
 // (default parameters, LINPACK basis: the codegen's gains), synchronous on
-// the default stream of the current device.
-#include <hip/hip_runtime.h>
-
+// the default stream of the current device. Host code only, built into its
+// own library (libaclswarm_amd_codegen.so, linked to libaclswarm_amd.so): the
+// generic emx utility names stay out of the core library's exports.
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -137,21 +137,33 @@ void ADMMGainDesign3D(const emxArray_real_T* Qs, const emxArray_real_T* adj, emx
   // column-major, the GainMat Aopt holds
   const size_t bp = (size_t)3 * n * sizeof(double), ba = (size_t)n * n * sizeof(double),
                bg = (size_t)N3 * N3 * sizeof(double);
-  void *dp = nullptr, *da = nullptr, *dg = nullptr;
+  void *dp = nullptr, *da = nullptr, *dg = nullptr, *di = nullptr;
+  int32_t it[2] = {0, 0};
   acl_admm_params_t prm;
   acl_default_admm_params(&prm);
   prm.basis = ACL_ADMM_BASIS_LINPACK;
   const bool ok = acl_malloc(&dp, bp) == ACL_OK && acl_malloc(&da, ba) == ACL_OK &&
-                  acl_malloc(&dg, bg) == ACL_OK &&
+                  acl_malloc(&dg, bg) == ACL_OK && acl_malloc(&di, sizeof(it)) == ACL_OK &&
                   acl_memcpy_h2d(dp, Qs->data, bp, nullptr) == ACL_OK &&
                   acl_memcpy_h2d(da, adj->data, ba, nullptr) == ACL_OK &&
                   acl_admm_solve_batch(1, n, static_cast<const double*>(dp),
                                        static_cast<const double*>(da), static_cast<double*>(dg),
-                                       nullptr, &prm, nullptr) == ACL_OK &&
+                                       static_cast<int32_t*>(di), &prm, nullptr) == ACL_OK &&
                   acl_memcpy_d2h(Aopt->data, dg, bg, nullptr) == ACL_OK &&
+                  acl_memcpy_d2h(it, di, sizeof(it), nullptr) == ACL_OK &&
                   acl_stream_synchronize(nullptr) == ACL_OK;
   if (dp) acl_free(dp);
   if (da) acl_free(da);
   if (dg) acl_free(dg);
-  if (!ok) emx_empty(Aopt);  // acl_last_error() holds the failing call's message
+  if (di) acl_free(di);
+  if (!ok) {
+    emx_empty(Aopt);  // acl_last_error() holds the failing call's message
+  } else if (it[0] < 0 || it[1] < 0) {
+    // a PSD projection left unconverged (include/aclswarm_amd.h: negative
+    // iters): the generated library has no error channel, so the design is
+    // withheld (Aopt empty, as for the other failures) and the reason kept
+    acl__set_error("ADMMGainDesign3D: a PSD projection did not converge (Jacobi fallback "
+                   "exhausted); the gains are not reliable");
+    emx_empty(Aopt);
+  }
 }

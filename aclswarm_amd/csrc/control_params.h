@@ -173,7 +173,8 @@ struct SolveParams {
 // misc int slots of the auction kernels' LDS
 enum { M_BAD = 0, M_NONFIN = 1, M_NINV = 5, M_AGREE = 6, M_CHANGED = 7, M_NCA = 8,
        M_PINF = 9 /* a formation coordinate is not finite */,
-       M_MARG = 10 /* u64: bits of the swarm's minimum decision gap (misc[10..11]) */ };
+       M_MARG = 10 /* u64: bits of the swarm's minimum decision gap (misc[10..11]) */,
+       M_ROWBAD = 12 /* a vehicle's own row (P_rows) failed its check */ };
 
 // Control stage: which = 0 launches the gain kernel for swarms
 // [P.b0, P.b0 + nb) (DistCntrl::compute, saturation, the collision test),

@@ -183,6 +183,14 @@ def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
     if P_rows is not None:
         if P_rows_on is None or P_rows.shape != (B, n, n) or P_rows_on.shape != (B,):
             raise ValueError("P_rows [B][n][n] needs P_rows_on [B]")
+        # the kernels read raw row-major u16 / u8 memory on q's device
+        if P_rows.dtype not in (torch.int16, torch.uint16) or \
+                P_rows_on.dtype not in (torch.uint8, torch.bool):
+            raise ValueError("P_rows must be int16 (u16 bits) and P_rows_on uint8/bool")
+        if not (P_rows.is_contiguous() and P_rows_on.is_contiguous()):
+            raise ValueError("P_rows and P_rows_on must be contiguous")
+        if P_rows.device != q.device or P_rows_on.device != q.device:
+            raise ValueError("P_rows and P_rows_on must be on q's device")
         a.P_rows = P_rows.data_ptr()
         a.P_rows_on = P_rows_on.data_ptr()
     F = table.struct()

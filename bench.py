@@ -595,7 +595,7 @@ def main():
                        f"acl_amd::auction_kernel<1, 256, true, false, {mg}>" if n <= 64 else
                        f"acl_amd::auction_kernel<2, 512, true, false, {mg}>" if n <= 128 else
                        f"acl_amd::solve_wide_kernel<true, false, {mg}>")
-        gain_sym = (f"acl_amd::gain_kernel<{w['planes']}, false>" if n <= 128 else
+        gain_sym = (f"acl_amd::gain_kernel<{w['planes']}, false, 256>" if n <= 128 else
                     f"acl_amd::gain_kernel<{w['planes']}, false, 1024>")
         align_sym = "acl_amd::align_kernel<2>" if n <= 128 else "acl_amd::align_wide_kernel"
     else:
@@ -607,7 +607,7 @@ def main():
         # n > 128: the control law is the directed walk on 1 024-thread workgroups
         gain_sym = ("acl_amd::gain_pair_kernel<false, false>" if w["planes"] == 5 and n <= 128
                     else f"acl_amd::gain_kernel<{w['planes']}, false, 1024>" if n > 128
-                    else f"acl_amd::gain_kernel<{w['planes']}, false>")
+                    else f"acl_amd::gain_kernel<{w['planes']}, false, 256>")
     kern = {}
     for k, (name, sym) in enumerate((("auction", auction_sym), ("gain", gain_sym),
                                      ("ca", "acl_amd::ca_pair_kernel" if n <= 128

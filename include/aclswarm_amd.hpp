@@ -403,15 +403,25 @@ class Auctioneer {
       last_error_ = "Auctioneer::start before setFormation";
       return;
     }
+    AuctionOut r;
     try {
-      run_auction(q_colmajor);
+      r = run_auction(q_colmajor);
       last_status_ = ACL_OK;
       last_error_.clear();
     } catch (const std::exception& e) {
       last_status_ = ACL_ERR_HIP;
       last_error_ = e.what();
+      auction_open_ = false;
+      return;
     }
     auction_open_ = false;
+    // The user's handlers run outside the GPU error channel: the vehicle
+    // adopts its result first (auctioneer.cpp:250-295, which notifies the
+    // new-assignment handler), then the final bid is published; an exception
+    // either handler throws reaches the caller, as it would out of the
+    // reference's processBid, and is not reported as a GPU failure.
+    finish(r.who);
+    if (send_bid_) send_bid_((uint32_t)auctionid_, (uint32_t)(2 * n_), finalBid(r.q, r.who, r.Rt));
   }
   /* the outcome of the last start(): ACL_OK, or why no auction ran
    * (lastError() says what) */
@@ -419,7 +429,12 @@ class Auctioneer {
   const std::string& lastError() const { return last_error_; }
 
  private:
-  void run_auction(const double* q_colmajor) {
+  struct AuctionOut {
+    std::vector<double> q;     // the snapshot, xyz rows
+    std::vector<uint16_t> who; // this vehicle's final table: task -> vehicle
+    std::vector<double> Rt;    // every vehicle's alignment (R, t)
+  };
+  AuctionOut run_auction(const double* q_colmajor) {
     auction_open_ = true;
     auctionid_++;
     if (verbose_)  // auctioneer.cpp:110-115
@@ -462,8 +477,7 @@ class Auctioneer {
                                  (size_t)n * 2, nullptr));
     detail::check(acl_memcpy_d2h(Rt.data(), d_rt_.get(), Rt.size() * 8, nullptr));
     detail::check(acl_stream_synchronize(nullptr));
-    if (send_bid_) send_bid_((uint32_t)auctionid_, (uint32_t)(2 * n), finalBid(q, who, Rt));
-    finish(who);
+    return AuctionOut{q, std::move(who), std::move(Rt)};
   }
 
   /* The final bid of this vehicle: who[j] (-1 = none) and price[j] = the

@@ -248,7 +248,9 @@ int orc_umeyama2_gap(int k, const double* src, const double* dst, double R[4],
   }
   double s1 = 1.0;
   if (variant == 1) {
-    /* Eigen 3.4: S(m-1) = -1 iff det(U) det(V) < 0 */
+    /* Eigen 3.4: S(m-1) = -1 iff det(U) det(V) < 0 (orthogonal factors,
+     * determinants +-1: no near-tie to track, the gap is 1) */
+    if (gap) *gap = 1.0;
     if (det2_lu(U) * det2_lu(V) < 0.0) s1 = -1.0;
   } else {
     /* Eigen 3.3.x: S from det(sigma); rank-deficient branch */
@@ -299,6 +301,14 @@ void orc_align(int n, int v, const double* q, const double* p,
   orc_align_gap(n, v, q, p, adj, P, R, t, NULL);
 }
 
+/* The Eigen version whose umeyama rule the vehicle alignments follow (SURVEY
+ * App. B; the reference pins none): 0 = 3.3.x (the default, the GPU's rule),
+ * 1 = 3.4. A process-wide switch for the version-risk measurement
+ * (scripts/eigen_variant_risk.py); set it before any solve runs. */
+static int g_umeyama_variant = 0;
+void orc_set_umeyama_variant(int variant) { g_umeyama_variant = variant ? 1 : 0; }
+int orc_get_umeyama_variant(void) { return g_umeyama_variant; }
+
 void orc_align_gap(int n, int v, const double* q, const double* p,
                    const uint8_t* adj, const uint16_t* P, double R[4],
                    double t[2], double* gap) {
@@ -319,7 +329,7 @@ void orc_align_gap(int n, int v, const double* q, const double* p,
       ++k;
     }
   }
-  orc_umeyama2_gap(k, src, dst, R, t, 0, gap);
+  orc_umeyama2_gap(k, src, dst, R, t, g_umeyama_variant, gap);
   free(src);
   free(dst);
   free(Pt);

@@ -65,6 +65,11 @@ int orc_umeyama2_gap(int k, const double* src, const double* dst, double R[4],
                      double t[2], int variant, double* gap);
 
 /* Auctioneer::alignFormation for vehicle v: R (row-major 2x2), t (2). */
+/* The umeyama rule of every vehicle alignment below (orc_align*, the solve
+ * entry points): 0 = Eigen 3.3.x (default), 1 = Eigen 3.4. Process-wide. */
+void orc_set_umeyama_variant(int variant);
+int orc_get_umeyama_variant(void);
+
 void orc_align(int n, int v, const double* q, const double* p,
                const uint8_t* adj, const uint16_t* P, double R[4],
                double t[2]);

@@ -122,6 +122,17 @@ def umeyama2(src, dst, variant=0):
     return R.reshape(2, 2), t
 
 
+def align(n, v, q, p, adj, P):
+    """orc_align: vehicle v's alignment (auctioneer.cpp:347-415) under the
+    current umeyama rule. Returns (R 2x2, t 2)."""
+    q = _c(q, np.float64); p = _c(p, np.float64); adj = _c(adj, np.uint8)
+    P = _c(P, np.uint16)
+    R = np.zeros(4); t = np.zeros(2)
+    lib().orc_align(n, v, _p(q, ct.c_double), _p(p, ct.c_double), _p(adj, ct.c_uint8),
+                    _p(P, ct.c_uint16), _p(R, ct.c_double), _p(t, ct.c_double))
+    return R.reshape(2, 2), t
+
+
 def prices(q, p, adj, P):
     n = q.shape[0]
     q = _c(q, np.float64); p = _c(p, np.float64); adj = _c(adj, np.uint8)

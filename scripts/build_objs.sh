@@ -15,8 +15,7 @@ for s in solve solve_wide control admm hungarian episode formation_gen; do
   fi
 done
 { [ build/obj/api.o -nt $C/api.cpp ] && [ build/obj/api.o -nt include/aclswarm_amd.h ]; } || /opt/rocm/bin/hipcc $F -c $C/api.cpp -o build/obj/api.o
-[ build/obj/codegen_api.o -nt $C/codegen_api.cpp ] || /opt/rocm/bin/hipcc $F -c $C/codegen_api.cpp -o build/obj/codegen_api.o
 name=$1; shift
 /opt/rocm/bin/hipcc $F "$@" -c $C/auction.hip -o build/obj/auction_$name.o
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 build/obj/{solve,solve_wide,control,admm,hungarian,episode,formation_gen,api,codegen_api}.o build/obj/auction_$name.o -o aclswarm_amd/lib/exp/$name.so
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 build/obj/{solve,solve_wide,control,admm,hungarian,episode,formation_gen,api}.o build/obj/auction_$name.o -o aclswarm_amd/lib/exp/$name.so
 echo aclswarm_amd/lib/exp/$name.so

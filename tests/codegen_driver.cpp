@@ -3,7 +3,7 @@
 // initialize, an emxInit'd 2-D result, wrappers around the caller's points
 // and adjacency, the design, frees), built against include/codegen_admm/ --
 // the header names admm.h includes (admm.h:16-20) -- and linked to
-// libaclswarm_amd.so. tests/test_gpu_codegen.py calls codegen_run through
+// libaclswarm_amd_codegen.so (over libaclswarm_amd.so). tests/test_gpu_codegen.py calls codegen_run through
 // ctypes; tests/test_abi.py compiles it and checks the exported names.
 #include <ADMMGainDesign3D.h>
 #include <ADMMGainDesign3D_emxAPI.h>

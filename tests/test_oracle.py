@@ -346,3 +346,49 @@ def test_oracle_batch_threads_match_serial():
         np.testing.assert_array_equal(out["P_out"][b], r["P_out"])
         np.testing.assert_array_equal(out["u_safe"][b], r["u_safe"])
         assert out["status"][b]["eff_rounds"] == r["status"]["eff_rounds"]
+
+
+def test_umeyama_rule_switch_reaches_the_solve():
+    """orc_set_umeyama_variant (the Eigen 3.3 / 3.4 umeyama rule, SURVEY
+    App. B) applies to every vehicle alignment of the solve: the aligned
+    (R, t) equal orc_umeyama2 under that rule, and on the reference
+    generator's N = 100 formations both rules give the same assignments,
+    flags and rounds (the rules differ only where det(sigma) and
+    det(U) det(V) disagree in sign by rounding: the C3 count over the bench
+    workload is scripts/eigen_variant_risk.py's)."""
+    P, A = H.simform("simform100_nc")
+    rng = np.random.RandomState(11)
+    F = 3
+    pts = np.stack([P[s, 0] for s in range(F)])
+    adjs = np.stack([A[s] for s in range(F)])
+    gains = np.stack([H.synth_gains(rng, a) for a in adjs])
+    B = 6
+    fidx = np.arange(B, dtype=np.int32) % F
+    q = np.stack([H.random_positions(rng, 100, 45.0) for _ in range(B)])
+    vel = rng.normal(0, 0.1, (B, 100, 3))
+    Pin = np.stack([H.random_perm(rng, 100) for _ in range(B)])
+    L = O.lib()
+    outs = []
+    try:
+        for var in (0, 1):
+            L.orc_set_umeyama_variant(var)
+            assert L.orc_get_umeyama_variant() == var
+            outs.append(O.solve_batch(fidx, q, vel, pts, adjs, gains, Pin, nthreads=4)[0])
+            # one vehicle's alignment against the plain entry point
+            b, v = 1, 17
+            f = fidx[b]
+            i = Pin[b][v]
+            Pt = np.argsort(Pin[b])
+            nb = [j for j in range(100) if adjs[f][i, j] or j == i]
+            src = pts[f][nb, :2]
+            dst = q[b][Pt[nb], :2]
+            R, t = O.umeyama2(src, dst, var)
+            Ra, ta = O.align(100, v, q[b], pts[f], adjs[f], Pin[b])
+            np.testing.assert_array_equal(R, Ra)
+            np.testing.assert_array_equal(t, ta)
+    finally:
+        L.orc_set_umeyama_variant(0)
+    for k in ("P_out", "u_safe"):
+        np.testing.assert_array_equal(outs[0][k], outs[1][k])
+    np.testing.assert_array_equal(outs[0]["status"]["flags"], outs[1]["status"]["flags"])
+    np.testing.assert_array_equal(outs[0]["status"]["eff_rounds"], outs[1]["status"]["eff_rounds"])
