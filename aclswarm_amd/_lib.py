@@ -22,7 +22,7 @@ FLAG_CHANGED = 0x04
 FLAG_NONFINITE = 0x08
 FLAG_BAD_INPUT = 0x10
 FLAG_CA_ACTIVE = 0x20
-ABI_VERSION = 8  # include/aclswarm_amd.h ACL_ABI_VERSION
+ABI_VERSION = 9  # include/aclswarm_amd.h ACL_ABI_VERSION
 FLAG_FRAGILE = 0x40
 FRAGILE_MARGIN = 1e-6
 
@@ -38,6 +38,7 @@ EXPORTS = (
     "acl_control_batch", "acl_write_assignment_log", "acl_read_assignment_log",
     "acl_hungarian_batch",
     "acl_default_episode_params", "acl_episode_workspace_bytes", "acl_episode_batch",
+    "acl_default_trial_params", "acl_trial_workspace_bytes", "acl_trial_init", "acl_trial_batch",
     "acl_generate_formation_groups",
     "acl_malloc", "acl_free", "acl_memcpy_h2d", "acl_memcpy_d2h", "acl_memset",
     "acl_stream_synchronize", "acl_last_error",
@@ -108,7 +109,11 @@ class EpisodeParams(ct.Structure):
                 ("auction_latency", ct.c_int32), ("max_accel_xy", ct.c_double),
                 ("max_accel_z", ct.c_double), ("bounds_min", ct.c_double * 3),
                 ("bounds_max", ct.c_double * 3), ("orig_zero_vel_thr", ct.c_double),
-                ("avg_active_ca_thr", ct.c_double)]
+                ("avg_active_ca_thr", ct.c_double), ("assignment", ct.c_int32)]
+
+
+ASSIGN_CBAA = 0     # acl_episode_params_t::assignment (ABI 9)
+ASSIGN_CENTRAL = 1
 
 
 EPISODE_STATUS_DTYPE = np.dtype([("converged_step", "<i4"), ("gridlock_step", "<i4"),
@@ -129,6 +134,39 @@ class EpisodeArgs(ct.Structure):
                 ("vel_hist", ct.c_void_p), ("u_hist", ct.c_void_p), ("ca_hist", ct.c_void_p), ("P_hist", ct.c_void_p),
                 ("workspace", ct.c_void_p), ("cntrl", CntrlGains), ("safety", SafetyParams),
                 ("ep", EpisodeParams)]
+
+
+class TrialParams(ct.Structure):
+    """acl_trial_params_t (supervisor.py:47-62,88,121; coordination.launch:5)."""
+    _fields_ = [("ep", EpisodeParams), ("tick_rate", ct.c_int32), ("settle_steps", ct.c_int32),
+                ("hover_wait", ct.c_double), ("assignment_timeout", ct.c_double),
+                ("formation_received_wait", ct.c_double), ("converged_wait", ct.c_double),
+                ("gridlock_timeout", ct.c_double), ("trial_timeout", ct.c_double),
+                ("alpha", ct.c_double)]
+
+
+# supervisor.py State values (ACL_TRIAL_*)
+TRIAL_HOVERING, TRIAL_WAITING, TRIAL_FLYING, TRIAL_IN_FORMATION = 3, 4, 5, 6
+TRIAL_GRIDLOCK, TRIAL_COMPLETE, TRIAL_TERMINATE = 7, 8, 9
+
+TRIAL_STATUS_DTYPE = np.dtype([(k, "<i4") for k in (
+    "state", "last_state", "timer_ticks", "formation", "ticks", "received", "logging",
+    "commit", "next_auction", "conv_len", "conv_head", "grid_len", "grid_head", "log_init",
+    "t_start", "t_grid", "done_step")] + [("n_auctions", "<u2"), ("n_invalid", "<u2"),
+                                          ("n_skipped", "<u2"), ("n_disagree", "<u2"),
+                                          ("per_vehicle", "<i4")])
+
+
+class TrialArgs(ct.Structure):
+    """acl_trial_args_t (batched Monte-Carlo trials)."""
+    _fields_ = [("B", ct.c_int32), ("K", ct.c_int32)] + [
+        (k, ct.c_void_p) for k in ("fseq", "fidx", "q", "vel", "P", "flush", "ts", "ctl_on",
+                                   "ring_u", "ring_ca", "posf", "dist", "t_conv", "t_avoid",
+                                   "n_assign")] + [
+        ("step0", ct.c_int32), ("steps", ct.c_int32)] + [
+        (k, ct.c_void_p) for k in ("q_hist", "vel_hist", "u_hist", "ca_hist", "ctl_hist",
+                                   "P_hist", "state_hist", "workspace")] + [
+        ("cntrl", CntrlGains), ("safety", SafetyParams), ("tp", TrialParams)]
 
 
 HUNG_BAD_INPUT = 0x01
@@ -187,6 +225,14 @@ def lib():
     L.acl_episode_workspace_bytes.restype = SZ
     L.acl_episode_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(EpisodeArgs), VP]
     L.acl_episode_batch.restype = ct.c_int
+    L.acl_default_trial_params.argtypes = [ct.POINTER(TrialParams)]
+    L.acl_default_trial_params.restype = None
+    L.acl_trial_workspace_bytes.argtypes = [I32, I32]
+    L.acl_trial_workspace_bytes.restype = SZ
+    L.acl_trial_init.argtypes = [ct.POINTER(TrialArgs), I32, VP]
+    L.acl_trial_init.restype = ct.c_int
+    L.acl_trial_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(TrialArgs), VP]
+    L.acl_trial_batch.restype = ct.c_int
     L.acl_generate_formation_groups.argtypes = [I32, I32, VP, I32, ct.c_double, ct.c_double,
                                                 ct.c_double, ct.c_double, I64, VP, VP, VP,
                                                 VP, VP]
@@ -242,6 +288,12 @@ def default_episode_params():
     e = EpisodeParams()
     lib().acl_default_episode_params(ct.byref(e))
     return e
+
+
+def default_trial_params():
+    t = TrialParams()
+    lib().acl_default_trial_params(ct.byref(t))
+    return t
 
 
 def default_gains():

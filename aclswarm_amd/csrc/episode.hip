@@ -2,12 +2,16 @@
 //
 // acl_episode_batch flies B swarms for a number of control periods in
 // lockstep, reusing the decision-loop kernels of acl_solve_batch /
-// acl_control_batch and adding two small kernels:
+// acl_control_batch (and acl_hungarian_batch in the centralized mode) and
+// adding small kernels:
 //
 //   adopt_kernel   after an auto-auction: the flush/skip rule of
 //                  CoordinationROS::autoauctionCb (coordination_ros.cpp:339-
 //                  345) and adoption of a valid, agreed assignment
 //                  (auctioneer.cpp:283-292, newAssignmentCb :284-303)
+//   central_kernel ACL_ASSIGN_CENTRAL: the operator's Hungarian assignment as
+//                  every vehicle's setAssignment + newAssignmentCb
+//                  (coordination_ros.cpp:330-343)
 //   traj_kernel    Safety::makeSafeTraj (safety.cpp:330-408) with the
 //                  utils::rateLimit / clamp helpers (utils.h:213-264), the
 //                  perfectly tracking vehicle (q <- goal.pos, vel <-
@@ -25,38 +29,11 @@
 
 #include "../../include/aclswarm_amd.h"
 #include "control_params.h"
+#include "episode_dev.h"
 
 extern "C" acl_status_t acl__set_error(const char* msg);
 
 namespace acl_amd {
-
-constexpr int kEpBlock = 128;  // traj_kernel threads (64 for n <= 64: fewer waves per step)
-
-// Episode workspace: the auction's solve workspace, the control stage's own
-// hand-off region (the head of a WsLayout: pt, mode, rows, ...; kept apart
-// so that an auction still pending does not overwrite the tables the
-// vehicles fly meanwhile -- and the next auction's own rows, P_rows), the
-// auction's output and the control stage's output of the current step.
-struct EpLayout {
-  size_t solve, ctl, Pnew, st, cst, u, us, ca, lat, total;
-};
-
-inline EpLayout ep_layout(int n, int B) {
-  EpLayout L;
-  const size_t nb = (size_t)n, bb = (size_t)B;
-  size_t o = 0;
-  L.solve = o; o = ws_al(o + ws_layout(n, B).total);
-  L.ctl = o;   o = ws_al(o + ws_layout(n, B).wide);  // pt .. camask: what run_control uses
-  L.Pnew = o;  o = ws_al(o + bb * nb * 2);
-  L.st = o;    o = ws_al(o + bb * sizeof(acl_swarm_status_t));
-  L.cst = o;   o = ws_al(o + bb * sizeof(acl_swarm_status_t));
-  L.u = o;     o = ws_al(o + bb * nb * 3 * 8);
-  L.us = o;    o = ws_al(o + bb * nb * 3 * 8);
-  L.ca = o;    o = ws_al(o + bb * nb);
-  L.lat = o;   o = ws_al(o + bb * 4);  // per-swarm auction latency (control steps)
-  L.total = o;
-  return L;
-}
 
 // An auction's latency in control steps, per swarm (acl_episode_params_t::
 // auction_latency): fixed, or the reference's timing -- one bid processed per
@@ -215,6 +192,49 @@ __global__ void __launch_bounds__(256) adopt_kernel(const AdoptArgs A) {
   }
 }
 
+// ACL_ASSIGN_CENTRAL: CoordinationROS::autoauctionCb in the centralized
+// comparison mode (coordination_ros.cpp:330-343). The operator's assignment
+// -- acl_hungarian_batch's P_opt from the current q with last = the swarm's
+// P (operator.py:219-240) -- becomes every vehicle's assignment
+// (Auctioneer::setAssignment + newAssignmentCb): one table, control mode 0.
+// A swarm whose Hungarian problem was BAD_INPUT / NONFINITE keeps its P.
+struct CentralArgs {
+  int n;
+  uint16_t* P;
+  const uint16_t* Popt;
+  const int32_t* hst;
+  acl_episode_status_t* est;
+  uint16_t* ctlPt;
+  uint8_t* ctlMode;
+  acl_swarm_status_t* cst;
+};
+
+__global__ void __launch_bounds__(256) central_kernel(const CentralArgs A) {
+  const int b = blockIdx.x, tid = threadIdx.x, n = A.n;
+  const bool ok = A.hst[b] == 0;  // workgroup-uniform
+  if (tid == 0) {
+    acl_episode_status_t e = A.est[b];
+    if (ok) {
+      ++e.n_auctions;
+      e.per_vehicle = 0;
+    } else {
+      ++e.n_invalid;
+    }
+    A.est[b] = e;
+  }
+  if (!ok) return;
+  const size_t bn = (size_t)b * n;
+  for (int v = tid; v < n; v += 256) {
+    const uint16_t pv = A.Popt[bn + v];
+    A.P[bn + v] = pv;
+    A.ctlPt[bn + pv] = (uint16_t)v;  // a permutation (status 0)
+  }
+  if (tid == 0) {
+    A.ctlMode[b] = 0;
+    A.cst[b] = acl_swarm_status_t{};
+  }
+}
+
 struct TrajParams {
   int n, B, step, k, tick;
   double* q;
@@ -235,22 +255,6 @@ struct TrajParams {
   acl_episode_params_t ep;
 };
 
-// utils::rateLimit (utils.h:254-264)
-__device__ __forceinline__ void rate_limit(double dt, double lo, double hi, double v0, double& v1) {
-  const double upper = v0 + hi * dt;
-  const double lower = v0 + lo * dt;
-  if (v1 > upper) v1 = upper;
-  if (v1 < lower) v1 = lower;
-}
-
-// utils::clamp (utils.h:213-227)
-__device__ __forceinline__ double clamp_ind(double val, double lower, double upper, bool& clamped) {
-  if (val < lower) { clamped = true; return lower; }
-  if (val > upper) { clamped = true; return upper; }
-  clamped = false;
-  return val;
-}
-
 __global__ void __launch_bounds__(kEpBlock) traj_kernel(const TrajParams T) {
   __shared__ int s_all_conv, s_any_grid, s_nca;
   const int n = T.n, b = blockIdx.x, tid = threadIdx.x;
@@ -265,31 +269,13 @@ __global__ void __launch_bounds__(kEpBlock) traj_kernel(const TrajParams T) {
   __syncthreads();
   const uint32_t m0 = T.est[b].n_samples;  // ticks before this one
   const int L = ep.bufflen;
-  const double dt = ep.control_dt;
   int nca = 0;
   for (int v = tid; v < n; v += (int)blockDim.x) {
     const size_t iv = (size_t)b * n + v;
     double gp[3] = {T.q[3 * iv], T.q[3 * iv + 1], T.q[3 * iv + 2]};
     double gv[3] = {T.vel[3 * iv], T.vel[3 * iv + 1], T.vel[3 * iv + 2]};
     double c[3] = {T.us[3 * iv], T.us[3 * iv + 1], T.us[3 * iv + 2]};
-    // Safety::makeSafeTraj (safety.cpp:330-408)
-    const double amax[3] = {ep.max_accel_xy, ep.max_accel_xy, ep.max_accel_z};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) rate_limit(dt, -amax[a], amax[a], gv[a], c[a]);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const double next = gp[a] + c[a] * dt;
-      bool clamped = false;
-      // std::min / std::max (b < a ? b : a, a < b ? b : a)
-      const double lo = gp[a] < ep.bounds_min[a] ? gp[a] : ep.bounds_min[a];
-      const double hi = ep.bounds_max[a] < gp[a] ? gp[a] : ep.bounds_max[a];
-      gp[a] = clamp_ind(next, lo, hi, clamped);
-      if (clamped) {
-        c[a] = 0.0;
-        rate_limit(dt, -amax[a], amax[a], gv[a], c[a]);
-      }
-      gv[a] = c[a];
-    }
+    make_safe_traj(ep, gp, gv, c);
     // the vehicle tracks its goal exactly
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -362,6 +348,7 @@ extern "C" void acl_default_episode_params(acl_episode_params_t* e) {
   e->bounds_max[0] = 100.0;  e->bounds_max[1] = 100.0;  e->bounds_max[2] = 30.0;
   e->orig_zero_vel_thr = 1.0;
   e->avg_active_ca_thr = 0.95;
+  e->assignment = ACL_ASSIGN_CBAA;
 }
 
 extern "C" size_t acl_episode_workspace_bytes(int32_t n, int32_t B) {
@@ -385,6 +372,10 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
   if (ep.auction_every < 1 || ep.sample_every < 1 || ep.bufflen < 1 || !(ep.control_dt > 0.0))
     return acl__set_error("acl_episode_batch: auction_every, sample_every, bufflen must be "
                           ">= 1 and control_dt > 0");
+  if (ep.assignment != ACL_ASSIGN_CBAA && ep.assignment != ACL_ASSIGN_CENTRAL)
+    return acl__set_error("acl_episode_batch: assignment must be ACL_ASSIGN_CBAA or "
+                          "ACL_ASSIGN_CENTRAL");
+  const bool central = ep.assignment == ACL_ASSIGN_CENTRAL;
   const EpLayout W = ep_layout(n, B);
   unsigned char* ws = (unsigned char*)a->workspace;
   hipStream_t s = (hipStream_t)stream;
@@ -447,8 +438,17 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
   A.ctlMode = wc + WS.mode;
   A.ctlRows = reinterpret_cast<uint16_t*>(wc + WS.rows);
   A.cst = cs.status;
+  // ACL_ASSIGN_CENTRAL: the operator's Hungarian from the swarm's current P
+  acl_hungarian_args_t ha = {};
+  ha.B = B; ha.fidx = a->fidx; ha.q = a->q; ha.P_last = a->P; ha.P_opt = Pnew;
+  ha.cost = reinterpret_cast<double*>(ws + W.hcost);
+  ha.status = reinterpret_cast<int32_t*>(ws + W.hst);
+  CentralArgs CA;
+  CA.n = n; CA.P = a->P; CA.Popt = Pnew; CA.hst = ha.status; CA.est = a->est;
+  CA.ctlPt = A.ctlPt; CA.ctlMode = A.ctlMode; CA.cst = A.cst;
   // auctions that take time: each swarm's latency in control steps
-  const bool timed = ep.auction_latency != 0;
+  // (the centralized mode applies its assignment at the auto-auction itself)
+  const bool timed = !central && ep.auction_latency != 0;
   int32_t* lat = reinterpret_cast<int32_t*>(ws + W.lat);
   if (timed) {
     hipLaunchKernelGGL(latency_kernel, dim3(B), dim3(64), 0, s, n, a->fidx, F->n_formations,
@@ -460,7 +460,12 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
   for (int k = 0; k < a->steps; ++k) {
     const int step = a->step0 + k;
     A.step = step;
-    if (step % ep.auction_every == 0) {
+    if (step % ep.auction_every == 0 && central) {
+      const acl_status_t r = acl_hungarian_batch(F, &ha, stream);
+      if (r != ACL_OK) return r;
+      hipLaunchKernelGGL(central_kernel, dim3(B), dim3(256), 0, s, CA);
+      if (hipGetLastError() != hipSuccess) return acl__set_error("central_kernel launch failed");
+    } else if (step % ep.auction_every == 0) {
       const acl_status_t r = acl_solve_batch(F, &sa, stream);
       if (r != ACL_OK) return r;
       A.mode = 0;

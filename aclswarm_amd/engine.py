@@ -415,6 +415,105 @@ class Episode:
         return arr.view(L.EPISODE_STATUS_DTYPE).reshape(-1)
 
 
+class Trial:
+    """Batched Monte-Carlo trials (acl_trial_batch; supervisor.py over the
+    closed loop): each swarm flies its formation sequence fseq[b] through the
+    supervisor's state machine and keeps its per-trial record. State persists
+    across calls (a trial can be run in chunks of steps).
+
+    fseq [B][K] int32, q/vel [B][n][3] f64 on the device (copied). The
+    assignment starts at identity (no formation yet)."""
+
+    def __init__(self, table, fseq, q, vel, params=None, cntrl=None, safety=None):
+        dev = q.device
+        self.table = table
+        self.B, self.n = int(q.shape[0]), table.n
+        self.K = int(fseq.shape[1])
+        self.tp = params or L.default_trial_params()
+        self.cntrl = cntrl or L.default_gains()
+        self.safety = safety or L.default_safety()
+        B, n, K = self.B, self.n, self.K
+        Lb = int(self.tp.ep.bufflen)
+        self.fseq = fseq.to(torch.int32).contiguous()
+        self.fidx = torch.empty(B, dtype=torch.int32, device=dev)
+        self.q = q.clone().contiguous()
+        self.vel = vel.clone().contiguous()
+        self.P = torch.empty((B, n), dtype=torch.int16, device=dev)
+        self.flush = torch.empty(B, dtype=torch.uint8, device=dev)
+        self.ts = torch.empty((B, L.TRIAL_STATUS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        self.ctl_on = torch.empty((B, n), dtype=torch.uint8, device=dev)
+        self.ring_u = torch.empty((B, Lb, n), dtype=torch.float64, device=dev)
+        self.ring_ca = torch.empty((B, Lb, n), dtype=torch.uint8, device=dev)
+        self.posf = torch.empty((B, 2, n), dtype=torch.float64, device=dev)
+        self.dist = torch.empty((B, n), dtype=torch.float64, device=dev)
+        self.t_conv = torch.empty((B, K), dtype=torch.float64, device=dev)
+        self.t_avoid = torch.empty((B, K), dtype=torch.float64, device=dev)
+        self.n_assign = torch.empty((B, K), dtype=torch.int32, device=dev)
+        need = int(L.lib().acl_trial_workspace_bytes(n, B))
+        self.ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        self.step = 0
+        a = self._args(0)
+        L.check(L.lib().acl_trial_init(ct.byref(a), n, ct.c_void_p(
+            torch.cuda.current_stream(dev).cuda_stream)), "acl_trial_init")
+
+    def _args(self, steps, hist=None):
+        a = L.TrialArgs()
+        a.B, a.K = self.B, self.K
+        for k in ("fseq", "fidx", "q", "vel", "P", "flush", "ts", "ctl_on", "ring_u", "ring_ca",
+                  "posf", "dist", "t_conv", "t_avoid", "n_assign"):
+            setattr(a, k, getattr(self, k).data_ptr())
+        a.step0, a.steps = self.step, steps
+        if hist is not None:
+            for k, f in (("q", "q_hist"), ("vel", "vel_hist"), ("u", "u_hist"), ("ca", "ca_hist"),
+                         ("ctl", "ctl_hist"), ("P", "P_hist"), ("state", "state_hist")):
+                setattr(a, f, hist[k].data_ptr())
+        a.workspace = self.ws.data_ptr()
+        a.cntrl, a.safety, a.tp = self.cntrl, self.safety, self.tp
+        return a
+
+    def run(self, steps, history=False, stream=None):
+        """Advance every trial `steps` control periods. With history=True
+        returns per-step device tensors q/vel/u [steps][B][n][3] (u: 0 for
+        stopped controllers), ca/ctl [steps][B][n], P [steps][B][n] (int16),
+        state [steps][B]; else None."""
+        dev = self.q.device
+        B, n = self.B, self.n
+        hist = None
+        if history:
+            f64 = dict(dtype=torch.float64, device=dev)
+            hist = {"q": torch.empty((steps, B, n, 3), **f64),
+                    "vel": torch.empty((steps, B, n, 3), **f64),
+                    "u": torch.empty((steps, B, n, 3), **f64),
+                    "ca": torch.empty((steps, B, n), dtype=torch.uint8, device=dev),
+                    "ctl": torch.empty((steps, B, n), dtype=torch.uint8, device=dev),
+                    "P": torch.empty((steps, B, n), dtype=torch.int16, device=dev),
+                    "state": torch.empty((steps, B), dtype=torch.int32, device=dev)}
+        a = self._args(steps, hist)
+        F = self.table.struct()
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+        L.check(L.lib().acl_trial_batch(ct.byref(F), ct.byref(a), ct.c_void_p(stream)),
+                "acl_trial_batch")
+        self.step += steps
+        return hist
+
+    def status(self):
+        """Per-trial supervisor state and counters, structured numpy [B]."""
+        arr = np.ascontiguousarray(self.ts.cpu().numpy())
+        return arr.view(L.TRIAL_STATUS_DTYPE).reshape(-1)
+
+    def records(self):
+        """The supervisor's per-trial record (the CSV row of complete(),
+        supervisor.py:404-415) as numpy arrays: dist [B][n], time [B][K],
+        time_avoidance [B][K], assignments [B][K], plus state / done_step."""
+        st = self.status()
+        return {"dist": self.dist.cpu().numpy(), "time": self.t_conv.cpu().numpy(),
+                "time_avoidance": self.t_avoid.cpu().numpy(),
+                "assignments": self.n_assign.cpu().numpy(),
+                "state": st["state"].copy(), "last_state": st["last_state"].copy(),
+                "done_step": st["done_step"].copy()}
+
+
 def generate_formation_groups(seeds, n, fc, l, w, h, min_dist=2.0, max_candidates=0,
                               stream=None):
     """acl_generate_formation_groups: the reference's

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define ACL_ABI_VERSION 8
+#define ACL_ABI_VERSION 9
 
 typedef enum {
   ACL_OK = 0,
@@ -516,7 +516,26 @@ typedef struct {
   double bounds_max[3];    /*              {100, 100, 30} */
   double orig_zero_vel_thr;  /* 1.00 m/s (supervisor.py:61) */
   double avg_active_ca_thr;  /* 0.95 (supervisor.py:62) */
+  int32_t assignment;      /* ABI 9. ACL_ASSIGN_CBAA (0, default): the auction
+                              above. ACL_ASSIGN_CENTRAL: the reference's
+                              centralized comparison mode
+                              (/operator/central_assignment,
+                              coordination_ros.cpp:330-343): at each
+                              auto-auction the operator's
+                              find_optimal_assignment(q, p, last)
+                              (operator.py:219-240, assignment.py:94-137,
+                              acl_hungarian_batch with P_last = the swarm's
+                              current P) is applied as every vehicle's
+                              setAssignment + newAssignmentCb -- no CBAA, no
+                              flush rule, no auction latency; a swarm whose
+                              Hungarian problem is BAD_INPUT / NONFINITE (the
+                              operator's scipy call would raise) keeps its P
+                              and counts n_invalid. n_auctions counts the
+                              central assignments applied. */
 } acl_episode_params_t;
+
+#define ACL_ASSIGN_CBAA    0
+#define ACL_ASSIGN_CENTRAL 1
 
 void acl_default_episode_params(acl_episode_params_t* e);
 
@@ -569,6 +588,156 @@ typedef struct {
 size_t acl_episode_workspace_bytes(int32_t n, int32_t B);
 acl_status_t acl_episode_batch(const acl_formations_t* formations,
                                const acl_episode_args_t* args, void* stream);
+
+/* ---- batched Monte-Carlo trials (ABI 9; SURVEY §8f widening of row f1) ---
+ * B independent trials of aclswarm_sim's supervisor (aclswarm_sim/nodes/
+ * supervisor.py:160-236) over the closed loop of acl_episode_batch: each
+ * swarm flies a sequence of K formations (its formation group, fseq[b][k])
+ * through the supervisor's state machine
+ *   HOVERING --HOVER_WAIT--> next_formation --> WAITING_ON_ASSIGNMENT
+ *   --assignment--> FLYING (logging) --converged--> IN_FORMATION
+ *   --CONVERGED_WAIT--> HOVERING ... --all K done--> COMPLETE
+ *   FLYING --gridlocked--> GRIDLOCK --has_left_gridlock--> FLYING
+ *   with the ASSIGNMENT (20 s), GRIDLOCK (90 s) and trial watchdog (600 s)
+ *   timeouts --> TERMINATE,
+ * its windowed predicates over their own sample buffers (a predicate appends
+ * a sample only when the state machine calls it; next_state clears both
+ * buffers except FLYING -> IN_FORMATION, supervisor.py:238-265,297-337), and
+ * its per-trial record (the CSV row of complete(), :404-415): the smoothed
+ * planar distance flown per vehicle (log_signals, :452-487), the time to
+ * converge per formation, the (last) gridlock duration per formation and the
+ * assignments received per formation.
+ * Per control step s (control_dt), per swarm not yet COMPLETE / TERMINATE:
+ *   1. a formation requested by the last supervisor tick is committed
+ *      (CoordinationROS::spin, coordination_ros.cpp:95-153): the vehicles'
+ *      controllers stop and send one zero command (makeSafeTraj of a zero
+ *      velocity goal), the assignment resets to identity (Auctioneer::
+ *      setFormation, auctioneer.cpp:42-62), flush clears, and the first
+ *      auto-auction is due form_settle_time later, then one every
+ *      auction_every steps (autoauctionCb, :322-359);
+ *   2. a due auto-auction: CBAA with the episode's adoption and flush rules
+ *      (acl_episode_batch step 1, auction_latency must be 0), or the
+ *      operator's Hungarian (ep.assignment = ACL_ASSIGN_CENTRAL); a vehicle
+ *      that adopts an assignment starts its controller (first_assignment_,
+ *      newAssignmentCb :284-303); vehicle 0's assignment message is the
+ *      supervisor's (assignmentCb, supervisor.py:147-150; in the centralized
+ *      mode a message only when the assignment changed or is the first,
+ *      centralAssignmentCb :271-280);
+ *   3. DistCntrl + Safety for every vehicle whose controller runs, and
+ *      makeSafeTraj of its safe command; a vehicle whose controller is
+ *      stopped holds its last goal (Safety::controlCb keeps sending the last
+ *      goal message, safety.cpp:268-290; perfectly tracked);
+ *   4. every sample_every steps, one supervisor tick (tick_rate Hz): its
+ *      voriggoal / CA samples are |u| and the CA flag of running
+ *      controllers, 0 for stopped ones.
+ * Model limits: the trial starts in HOVERING with the swarm in
+ * the air (IDLE / TAKING_OFF are the simulator's); a formation commits at the
+ * step after the tick that requested it (the 5 Hz spin loop's delay is not
+ * modelled); the zero command's collision-avoidance flag is taken as 0; the
+ * watchdog counts from the first tick.
+ * Device pointers, updated in place (a trial continues across calls):
+ *   fseq [B][K] formation indices; fidx [B] out: the formation of each
+ *   swarm's controllers; q, vel [B][n][3]; P [B][n] (identity at the start);
+ *   flush [B]; ts [B] acl_trial_status_t (zeroed before the first call, then
+ *   acl_trial_init); ctl_on [B][n] u8; ring_u [B][bufflen][n] f64,
+ *   ring_ca [B][bufflen][n] u8 (the converged / gridlocked sample buffers);
+ *   posf [B][2][n] f64 (the smoothed x / y of log_signals); dist [B][n];
+ *   t_conv, t_avoid [B][K] f64 s; n_assign [B][K] i32.
+ * Optional histories (NULL = not stored), k = local step: q_hist, vel_hist,
+ *   u_hist [steps][B][n][3]; ca_hist, ctl_hist [steps][B][n] u8; P_hist
+ *   [steps][B][n]; state_hist [steps][B] i32 (supervisor state after the
+ *   step). workspace: acl_trial_workspace_bytes(n, B). */
+enum {
+  ACL_TRIAL_HOVERING = 3,             /* supervisor.py State values */
+  ACL_TRIAL_WAITING_ON_ASSIGNMENT = 4,
+  ACL_TRIAL_FLYING = 5,
+  ACL_TRIAL_IN_FORMATION = 6,
+  ACL_TRIAL_GRIDLOCK = 7,
+  ACL_TRIAL_COMPLETE = 8,
+  ACL_TRIAL_TERMINATE = 9
+};
+
+typedef struct {
+  acl_episode_params_t ep;        /* control_dt, auction_every, sample_every
+                                     (control steps per tick), bufflen
+                                     (BUFFLEN), accelerations, bounds, the two
+                                     thresholds, assignment; auction_latency
+                                     must be 0 */
+  int32_t tick_rate;              /* 50 Hz (supervisor.py:121) */
+  int32_t settle_steps;           /* form_settle_time / control_dt = 150
+                                     (coordination.launch:5) */
+  double hover_wait;              /* 5 s (supervisor.py:52) */
+  double assignment_timeout;      /* 20 s (:53) */
+  double formation_received_wait; /* 1 s (:54) */
+  double converged_wait;          /* 1 s (:55) */
+  double gridlock_timeout;        /* 90 s (:56) */
+  double trial_timeout;           /* 600 s (:57) */
+  double alpha;                   /* 0.98 (:88, log_signals' smoothing) */
+} acl_trial_params_t;
+
+void acl_default_trial_params(acl_trial_params_t* t);
+
+typedef struct {
+  int32_t state;          /* ACL_TRIAL_* */
+  int32_t last_state;
+  int32_t timer_ticks;    /* supervisor timer (-1 on entering a state) */
+  int32_t formation;      /* curr_formation_idx (-1 before the first) */
+  int32_t ticks;          /* supervisor ticks since the trial started */
+  int32_t received;       /* received_assignment */
+  int32_t logging;        /* is_logging */
+  int32_t commit;         /* 1: a formation waits to be committed */
+  int32_t next_auction;   /* steps to the next auto-auction (0: none) */
+  int32_t conv_len, conv_head;  /* 'converged_orig_vel' deque: size, next slot */
+  int32_t grid_len, grid_head;  /* 'gridlocked_active_ca' deque */
+  int32_t log_init;       /* log_signals' filters initialised */
+  int32_t t_start;        /* step at which the formation's logging started */
+  int32_t t_grid;         /* step at which GRIDLOCK was entered */
+  int32_t done_step;      /* step of complete() / terminate(), -1 running */
+  uint16_t n_auctions, n_invalid, n_skipped, n_disagree;
+  int32_t per_vehicle;    /* the swarm's vehicles fly different tables */
+} acl_trial_status_t; /* 80 bytes */
+
+typedef struct {
+  int32_t B;
+  int32_t K;
+  const int32_t* fseq;
+  int32_t* fidx;
+  double* q;
+  double* vel;
+  uint16_t* P;
+  uint8_t* flush;
+  acl_trial_status_t* ts;
+  uint8_t* ctl_on;
+  double* ring_u;
+  uint8_t* ring_ca;
+  double* posf;
+  double* dist;
+  double* t_conv;
+  double* t_avoid;
+  int32_t* n_assign;
+  int32_t step0;
+  int32_t steps;
+  double* q_hist;
+  double* vel_hist;
+  double* u_hist;
+  uint8_t* ca_hist;
+  uint8_t* ctl_hist;
+  uint16_t* P_hist;
+  int32_t* state_hist;
+  void* workspace;
+  acl_cntrl_gains_t cntrl;
+  acl_safety_params_t safety;
+  acl_trial_params_t tp;
+} acl_trial_args_t;
+
+size_t acl_trial_workspace_bytes(int32_t n, int32_t B);
+/* the start of a trial: ts zeroed except state HOVERING, timer_ticks -1,
+   formation -1, done_step -1; P identity; ctl_on, rings, posf, dist, t_conv,
+   t_avoid, n_assign, flush zeroed; fidx = fseq[b][0] (device pointers of
+   acl_trial_args_t; q and vel are the caller's) */
+acl_status_t acl_trial_init(const acl_trial_args_t* args, int32_t n, void* stream);
+acl_status_t acl_trial_batch(const acl_formations_t* formations,
+                             const acl_trial_args_t* args, void* stream);
 
 /* ---- random formation groups on the device -----------
  * Replaces aclswarm_sim/nodes/generate_random_formation.py:59-80

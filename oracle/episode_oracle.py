@@ -10,6 +10,11 @@ What it restates, in the order one lockstep control period applies it:
     current q (pyoracle.solve, the restatement of auctioneer.cpp) and each
     vehicle's adoption of its own final table when it is valid
     (auctioneer.cpp:250-295; `adopt`, `SwarmState`);
+    In the centralized comparison mode (acl_episode_params_t::assignment =
+    ACL_ASSIGN_CENTRAL, coordination_ros.cpp:330-343) the auto-auction
+    applies the operator's Hungarian assignment instead (`central_assign`:
+    pyoracle.hungarian, the restatement of assignment.py:94-137, with last =
+    the swarm's current P, operator.py:219-240);
   * DistCntrl::compute + Safety::cmdinCb + collisionAvoidance for every
     vehicle (pyoracle.control / saturate / collision_avoidance, i.e.
     distcntrl.cpp:46-102, safety.cpp:172-197,412-541);
@@ -40,7 +45,7 @@ def default_params():
     return dict(control_dt=0.01, auction_every=120, sample_every=2, bufflen=50,
                 auction_latency=0, max_accel_xy=0.5, max_accel_z=0.8,
                 bounds_min=(-100.0, -100.0, 0.0), bounds_max=(100.0, 100.0, 30.0),
-                orig_zero_vel_thr=1.0, avg_active_ca_thr=0.95)
+                orig_zero_vel_thr=1.0, avg_active_ca_thr=0.95, assignment=0)
 
 
 def params_from_struct(e):
@@ -49,7 +54,8 @@ def params_from_struct(e):
                 auction_latency=e.auction_latency,
                 max_accel_xy=e.max_accel_xy, max_accel_z=e.max_accel_z,
                 bounds_min=tuple(e.bounds_min), bounds_max=tuple(e.bounds_max),
-                orig_zero_vel_thr=e.orig_zero_vel_thr, avg_active_ca_thr=e.avg_active_ca_thr)
+                orig_zero_vel_thr=e.orig_zero_vel_thr, avg_active_ca_thr=e.avg_active_ca_thr,
+                assignment=int(getattr(e, "assignment", 0)))
 
 
 def _rate_limit(dt, lo, hi, v0, v1):
@@ -222,6 +228,22 @@ def adopt(state, flush, res):
     return (0 if all(vv) or bad else 1), "disagree"
 
 
+def central_assign(state, q, p):
+    """ACL_ASSIGN_CENTRAL's auto-auction (coordination_ros.cpp:330-343): the
+    operator's find_optimal_assignment(q, p, last) (operator.py:219-240,
+    assignment.py:94-137; pyoracle.hungarian) with last = the swarm's current
+    P becomes every vehicle's assignment (Auctioneer::setAssignment +
+    newAssignmentCb): one table. A BAD_INPUT / NONFINITE problem (scipy
+    would raise in the operator) leaves the swarm on its P. Mutates `state`;
+    returns 'central' or 'invalid'."""
+    P, _, _, st = O.hungarian(q, p, P_last=state.P)
+    if st != 0:
+        return "invalid"
+    state.P = P.astype(np.uint16).copy()
+    state.tables = None
+    return "central"
+
+
 AUCTIONEER_DT = 0.001  # coordination.launch:23: one bid processed per tick
 
 
@@ -246,17 +268,26 @@ class Auctions:
     their own step). An auto-auction that finds one pending restarts it
     (coordination_ros.cpp:355-358); the flush rule (:339-345) skips one."""
 
-    def __init__(self, latency, flush=0):
-        self.latency = latency
+    def __init__(self, latency, flush=0, central=False):
+        self.latency = 0 if central else latency
         self.flush = flush
+        self.central = central
         self.pending = -1
         self.res = None
-        self.counts = dict(skipped=0, auctions=0, adopted=0, invalid=0, disagree=0, restarted=0)
+        self.counts = dict(skipped=0, auctions=0, adopted=0, invalid=0, disagree=0, restarted=0,
+                           central=0)
 
-    def auto(self, step, state, solve):
+    def auto(self, step, state, solve, central=None):
         """An auto-auction step; solve(P_in, P_rows) runs CBAA from the
         current q with the vehicles' own assignments (state.solve_args()).
-        Mutates `state`."""
+        In the centralized mode central() applies the operator's assignment
+        instead (`central_assign`). Mutates `state`."""
+        if self.central:
+            ev = central()
+            self.counts[ev] += 1
+            if ev == "central":
+                self.counts["auctions"] += 1
+            return state
         if self.flush:
             self.flush = 0
             self.counts["skipped"] += 1
@@ -290,14 +321,15 @@ def run_episode(q, vel, P, p, adj, gains, steps, ep, step0=0, g=None, s=None):
     vel = np.array(vel, np.float64)
     st = SwarmState(P)
     sup = Supervisor(q.shape[0], ep)
-    auc = Auctions(auction_latency_steps(q.shape[0], adj, ep))
+    auc = Auctions(auction_latency_steps(q.shape[0], adj, ep), central=ep.get("assignment", 0) == 1)
     conv_step = grid_step = -1
     qs = []
     for k in range(steps):
         step = step0 + k
         if step % ep["auction_every"] == 0:
             auc.auto(step, st, lambda P_in, rows: O.solve(q, vel, p, adj, gains, P_in, g, s,
-                                                          P_rows=rows))
+                                                          P_rows=rows),
+                     central=lambda: central_assign(st, q, p))
         else:
             auc.tick(step, st)
         u, us, ca = control_step(q, vel, p, adj, gains, st.P, g, s, st.tables)

@@ -65,7 +65,8 @@ def main():
     r0, r1 = res[0], res[1]
     dP = (r0["P_out"] != r1["P_out"]).any(axis=1)
     # (FRAGILE masked: the margin tracks the 3.3 rule's determinant test)
-    dF = (r0["status"]["flags"] & ~0x40) != (r1["status"]["flags"] & ~0x40)
+    keep = np.uint32(0xFFFFFFFF ^ 0x40)
+    dF = (r0["status"]["flags"] & keep) != (r1["status"]["flags"] & keep)
     dR = r0["status"]["eff_rounds"] != r1["status"]["eff_rounds"]
     changed = dP | dF | dR
     fragile = (r0["status"]["flags"] & 0x40) != 0  # ACL_SWARM_FRAGILE

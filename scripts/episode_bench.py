@@ -9,6 +9,13 @@ swarm-steps/s (one swarm advanced one control period) with the state
 resident in HBM, per-kernel times from HIP events are not used here (the
 step is a sequence of small launches; rocprofv3 --stats gives the split).
 The CPU baseline runs oracle/episode_oracle.py's loop on a bounded sample.
+
+--assignment both: the reference's CBAA-vs-centralized comparison
+(coordination_ros.cpp:330-343, /operator/central_assignment): the same swarms
+flown once with the distributed auction and once with the operator's
+Hungarian assignment at every auto-auction (acl_episode_params_t::assignment),
+and the episode outcomes of each (converged / gridlocked swarms and their
+steps, collision-avoidance vehicle-steps, auction events) in one line.
 """
 import argparse
 import json
@@ -38,7 +45,10 @@ def main():
                     help="also time the chunk of `steps` captured once as a HIP graph and "
                          "replayed (the per-step launches without host launch overhead)")
     ap.add_argument("--reps", type=int, default=3, help="graph replays timed")
+    ap.add_argument("--assignment", choices=("cbaa", "central", "both"), default="cbaa")
     args = ap.parse_args()
+    if args.assignment == "both":
+        return compare(args)
     dev = torch.device("cuda:0")
     gen = torch.Generator(device=dev)
     gen.manual_seed(99)
@@ -47,10 +57,12 @@ def main():
     if not args.no_tile_gains:
         T.tile_gains()  # formation setup: tile-ordered gain records (acl_tile_gains)
     # warm-up: a short episode (first launches, workspace)
-    e0 = engine.Episode(T, w["fidx"], w["q"], w["vel"], w["P_in"])
+    ep_run = L.default_episode_params()
+    ep_run.assignment = L.ASSIGN_CENTRAL if args.assignment == "central" else L.ASSIGN_CBAA
+    e0 = engine.Episode(T, w["fidx"], w["q"], w["vel"], w["P_in"], params=ep_run)
     e0.run(2)
     torch.cuda.synchronize()
-    e = engine.Episode(T, w["fidx"], w["q"], w["vel"], w["P_in"])
+    e = engine.Episode(T, w["fidx"], w["q"], w["vel"], w["P_in"], params=ep_run)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e.run(args.steps)
@@ -138,6 +150,56 @@ def main():
                                 "sample": f"{k} control steps of one n={args.n} swarm through "
                                           "oracle/episode_oracle.py (C restatement of "
                                           "DistCntrl/Safety/CBAA per vehicle), 1 thread"}
+    print(json.dumps(line), flush=True)
+
+
+def outcomes(st, steps):
+    conv = st["converged_step"]
+    grid = st["gridlock_step"]
+    c = conv >= 0
+    return {"converged": int(c.sum()),
+            "converged_step_mean": float(conv[c].mean()) if c.any() else None,
+            "converged_step_median": float(np.median(conv[c])) if c.any() else None,
+            "gridlocked": int((grid >= 0).sum()),
+            "ca_vehicle_steps": int(st["n_ca_steps"].sum()),
+            "assignments_applied": int(st["n_auctions"].sum()),
+            "invalid": int(st["n_invalid"].sum()), "skipped": int(st["n_skipped"].sum()),
+            "disagree": int(st["n_disagree"].sum()), "steps": steps}
+
+
+def compare(args):
+    """CBAA vs the centralized Hungarian on the same swarms (same workload,
+    same start): one JSON line with both modes' episode outcomes and rates."""
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(99)
+    w = workload.simform_workload(args.B, args.n, gen, dev, F=None, complete=False, planes=5)
+    T = engine.FormationTable(w["n"], w["p"], w["bits"], w["gains"], w["gain_off"], w["planes"])
+    if not args.no_tile_gains:
+        T.tile_gains()
+    res = {}
+    for name, mode in (("cbaa", L.ASSIGN_CBAA), ("central", L.ASSIGN_CENTRAL)):
+        ep = L.default_episode_params()
+        ep.assignment = mode
+        e0 = engine.Episode(T, w["fidx"], w["q"], w["vel"], w["P_in"], params=ep)
+        e0.run(2)
+        torch.cuda.synchronize()
+        e = engine.Episode(T, w["fidx"], w["q"], w["vel"], w["P_in"], params=ep)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e.run(args.steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        r = outcomes(e.status(), args.steps)
+        r["swarm_steps_per_s"] = args.B * args.steps / dt
+        r["ms_per_step"] = dt / args.steps * 1e3
+        res[name] = r
+    line = {"metric": f"closed-loop episodes, CBAA vs centralized Hungarian (N={args.n})",
+            "B": args.B, "n": args.n, "steps": args.steps, "control_dt": 0.01,
+            "auction_every": 120, "dtype": "f64",
+            "data": "synthetic (simform_workload, C3 shape: noncomplete generator formations, "
+                    "a unique formation per swarm), same swarms and starts in both modes",
+            "cbaa": res["cbaa"], "central": res["central"]}
     print(json.dumps(line), flush=True)
 
 

@@ -316,3 +316,76 @@ def test_episode_zeroed_status_mid_period(cuda):
         assert st["n_restarted"] == c["restarted"] == 0
         assert (st["n_auctions"], st["n_skipped"]) == (c["auctions"], c["skipped"])
         assert st["pending_step"] == (auc.pending + 1 if auc.pending >= 0 else 0)
+
+
+@pytest.mark.parametrize("ci", [0, 1, 3, 5])
+def test_episode_central_teacher_forced(cuda, ci):
+    """ACL_ASSIGN_CENTRAL (coordination_ros.cpp:330-343): every auto-auction
+    applies the operator's Hungarian assignment (assignment.py:94-137 with
+    last = the swarm's current P) instead of CBAA. Teacher-forced: at each
+    auto-auction the CPU's Hungarian (oracle/hungarian_oracle.c) from the
+    GPU's own q and P must give the assignment the GPU's controller used
+    (bit-exact), and every step's commands, flags and state as in the CBAA
+    test; counters (assignments applied) equal."""
+    import torch
+    case = dict(_case(ci))
+    case["ep"] = dict(case["ep"], assignment=1, auction_latency=7)  # (latency: ignored)
+    e, eps = _episode(case, cuda)
+    hist = e.run(case["steps"], history=True)
+    torch.cuda.synchronize()
+    h = {k: v.cpu().numpy() for k, v in hist.items()}
+    h["P"] = h["P"].view(np.uint16)
+    est = e.status()
+    ep = E.params_from_struct(eps)
+    assert ep["assignment"] == 1
+    B, n = case["q"].shape[:2]
+    changed = 0
+    for b in range(B):
+        f = case["fidx"][b]
+        p, adj, G = case["pts"][f], case["adj"][f], case["gains"][f]
+        auc = E.Auctions(7, central=True)
+        state = E.SwarmState(case["P"][b])
+        qprev, vprev = case["q"][b], case["vel"][b]
+        for k in range(case["steps"]):
+            P0 = state.P.copy()
+            if k % ep["auction_every"] == 0:
+                auc.auto(k, state, None, central=lambda: E.central_assign(state, qprev, p))
+            else:
+                auc.tick(k, state)
+            changed += int((P0 != state.P).any())
+            assert (h["P"][k, b] == state.P).all(), (b, k)
+            assert state.tables is None
+            u, us, ca = E.control_step(qprev, vprev, p, adj, G, state.P)
+            np.testing.assert_allclose(h["u"][k, b], u, rtol=U_RTOL, atol=U_RTOL)
+            assert (h["ca"][k, b] == ca).all(), (b, k)
+            qn, vn = E.make_safe_traj(qprev, vprev, us, ep)
+            np.testing.assert_allclose(h["q"][k, b], qn, rtol=0, atol=Q_ATOL)
+            qprev, vprev = h["q"][k, b], h["vel"][k, b]
+        st, c = est[b], auc.counts
+        assert (st["n_auctions"], st["n_invalid"]) == (c["auctions"], c["invalid"]), (st, c)
+        assert (st["n_skipped"], st["n_disagree"], st["n_restarted"]) == (0, 0, 0)
+        assert st["pending_step"] == 0 and st["per_vehicle"] == 0
+    assert changed > 0  # the operator's assignment replaced the starting ones
+
+
+def test_episode_central_bad_problem_keeps_P(cuda):
+    """A swarm whose Hungarian problem is NONFINITE (a vehicle position is
+    NaN: scipy's linear_sum_assignment would raise in the operator) keeps its
+    assignment and counts n_invalid; the others get theirs."""
+    import torch
+    case = dict(_cases()[0], steps=3, ep=dict(auction_every=2, assignment=1))
+    q = case["q"].copy()
+    q[2, 3, 0] = np.nan
+    case["q"] = q
+    e, _ = _episode(case, cuda)
+    hist = e.run(case["steps"], history=True)
+    torch.cuda.synchronize()
+    Ph = hist["P"].cpu().numpy().view(np.uint16)
+    est = e.status()
+    assert (Ph[:, 2] == case["P"][2]).all()
+    assert est[2]["n_invalid"] == 2 and est[2]["n_auctions"] == 0
+    for b in (0, 1, 3):
+        P, _, _, st = O.hungarian(case["q"][b], case["pts"][case["fidx"][b]],
+                                  P_last=case["P"][b])
+        assert st == 0 and (Ph[0, b] == P).all()
+        assert est[b]["n_auctions"] == 2 and est[b]["n_invalid"] == 0
