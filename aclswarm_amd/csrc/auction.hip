@@ -742,6 +742,21 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     }
     if (tid < n) W1[tid] = 0ull;
   }
+  // the alignment launch's results (align_kernel: every work item's (R, t),
+  // the item of every formation row, the swarm's smallest alignment gap) in
+  // the same round trip: all 6n doubles of the item region are read (items
+  // past the count are never used), so no read waits for the item count
+  unsigned long long agap = 0ull;
+#ifndef ACL_ALIGN_PREFETCH
+#define ACL_ALIGN_PREFETCH 1
+#endif
+  if (ACL_ALIGN_PREFETCH && !kInlineAlign && !rowsm) {
+    const unsigned char* wsa = P.ws + P.W.align + (size_t)b * P.W.align_stride;
+    const double* gout = reinterpret_cast<const double*>(wsa);
+    for (int k = tid; k < 6 * n; k += kAB) out[k] = gout[k];
+    for (int i = tid; i < n; i += kAB) itm[i] = wsa[(size_t)n * 48 + i];
+    if (tid == 0) agap = *reinterpret_cast<const unsigned long long*>(wsa + (size_t)n * 48 + a16(n));
+  }
   __syncthreads();
   if (tid == 0) {
     misc[M_AGREE] = 1;
@@ -858,6 +873,9 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
     // the alignments' gaps go into the swarm margin now: the CBAA rounds
     // prune their margin work against it (below)
     block_min_gap(margw, galign);
+  } else if (ACL_ALIGN_PREFETCH) {
+    // (out and itm were filled in phase 0)
+    if (tid == 0) atomicMin(margw, agap);
   } else {
     const unsigned char* wsa = P.ws + P.W.align + (size_t)b * P.W.align_stride;
     const int nitems = *reinterpret_cast<const int*>(wsa + (size_t)n * 48 + a16(n) + 8);
@@ -1343,6 +1361,21 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
   sp.flush(P, b, lane);
   stamp_phase(P, b, tid, 4);
   ACL_AUCTION_STOP_AT(5);
+  // FUSE: the control phase's global reads now, so that adoption and the
+  // hand-off hide their latency (pair_fused.h, fused_prefetch). P.ctl through
+  // the kernel-argument segment, loaded where it is used (pair_fused.h): P is
+  // this kernel's only argument, at offset 0
+  FusedPre fpre;
+#ifndef ACL_FUSED_PREFETCH
+#define ACL_FUSED_PREFETCH 0
+#endif
+  if constexpr (FUSE && ACL_FUSED_PREFETCH) {
+    KCtlParams* pc = (KCtlParams*)((const __attribute__((address_space(4))) char*)
+                                       __builtin_amdgcn_kernarg_segment_ptr() +
+                                   offsetof(SolveParams, ctl));
+    asm volatile("" : "+s"(pc));
+    fused_prefetch(*pc, b, f, tid, fpre);
+  }
   if (MG) {  // swarm margin: every lane's pair and the wave's level pair (the
              // alignments' gaps are in already)
     margin_track(mp, uhi, ulo);
@@ -1496,7 +1529,8 @@ __global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
                                        __builtin_amdgcn_kernarg_segment_ptr() +
                                    offsetof(SolveParams, ctl));
     asm volatile("" : "+s"(pc));
-    pair_gain_fused<kAW, GM>(pc, b, f, smem, tid, kAB);
+    if (!ACL_FUSED_PREFETCH) fused_prefetch(*pc, b, f, tid, fpre);
+    pair_gain_fused<kAW, GM>(pc, b, f, smem, tid, kAB, fpre);
     stamp_phase(P, b, tid, 7);  // diagnostic: end of the control phase
   }
   stamp_rt(P, b, tid, kStampRt1);

@@ -151,9 +151,40 @@ __device__ __forceinline__ acl_safety_params_t ksafety(KCtlParams& P) {
   return s;
 }
 
+// The control phase's global reads, issued by the caller right after its
+// CBAA rounds (before adoption and the hand-off, whose work then hides their
+// latency): thread tid < n holds vehicle tid's q and vel and formation row
+// tid's point and adjacency words. None of it depends on the assignment.
+struct FusedPre {
+  double q0, q1, q2, v0, v1, v2, px, py, pz;
+  unsigned long long a0, a1;
+};
+
+__device__ __forceinline__ void fused_prefetch(KCtlParams& P, int b, int f, int tid,
+                                               FusedPre& X) {
+  const int n = P.n;
+  X.q0 = X.q1 = X.q2 = X.v0 = X.v1 = X.v2 = X.px = X.py = X.pz = 0.0;
+  X.a0 = X.a1 = 0ull;
+  if (tid < n) {
+    const int NWg = (n + 63) >> 6;
+    const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+    const double* gq = P.q + ((size_t)b * n + tid) * 3;
+    const double* gv = P.vel + ((size_t)b * n + tid) * 3;
+    const double* gp = P.p + ((size_t)f * n + tid) * 3;
+    const uint64_t* ga = P.adj + ((size_t)f * n + tid) * NWg;
+    X.q0 = gq[0]; X.q1 = gq[1]; X.q2 = gq[2];
+    X.v0 = gv[0]; X.v1 = gv[1]; X.v2 = gv[2];
+    X.px = gp[0]; X.py = gp[1]; X.pz = gp[2];
+    X.a0 = ga[0];
+    if (NWg > 1) X.a1 = ga[1] & lastmask;
+    else X.a0 &= lastmask;
+  }
+}
+
 template <int kW, bool GM>
 __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
-                                                unsigned char* smem, int tid, int nthreads) {
+                                                unsigned char* smem, int tid, int nthreads,
+                                                const FusedPre& X) {
   KCtlParams& P = *Pp;
   const int n = P.n;  // n <= 128 <= nthreads
   const int nb = (n + 7) >> 3, R = 8 * nb;
@@ -176,6 +207,9 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
   unsigned* flags = reinterpret_cast<unsigned*>(smem + L.flags);
   unsigned long long& gmw = *reinterpret_cast<unsigned long long*>(smem + L.gmw);
   unsigned* caw = reinterpret_cast<unsigned*>(smem + L.caw);
+  // [n][3] q by vehicle: the prefetched values' way to their formation rows
+  // (in the per-wave sums' region, zeroed only after the rows are built)
+  double* qs = acc;
 
   // ---- setup: the caller has written Pt[tid] (thread tid reads it back
   // here, so no barrier is needed first); every other table is built here
@@ -196,51 +230,53 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
     for (int k = 1; k < FC_N; ++k) x = tid == k ? v[k] : x;
     cst[tid] = x;
   }
-  const int NWg = (n + 63) >> 6;  // words per row of the global adjacency
   {
-    const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
-    const double* gp = P.p + (size_t)f * n * 3;
-    const double* gq = P.q + (size_t)b * n * 3;
-    const uint64_t* ga = P.adj + (size_t)f * n * NWg;
     bool qbad = false;
-    if (tid < R) {
-      const int i = tid;
-      double row[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-      unsigned long long a0 = 0ull, a1 = 0ull;
-      if (i < n) {
-        const int v = Pt[i];
-        Pinv[v] = (uint16_t)i;
-        row[0] = gq[3 * v];
-        row[1] = gq[3 * v + 1];
-        row[2] = gq[3 * v + 2];
-        // the epilogue's damping term reads the vehicle's vel: loaded here,
-        // in the same round trip as q, instead of after the pair loop
-        const double* gvel = P.vel + ((size_t)b * n + v) * 3;
-        velv[3 * v] = gvel[0];
-        velv[3 * v + 1] = gvel[1];
-        velv[3 * v + 2] = gvel[2];
-        const double x = gp[3 * i], y = gp[3 * i + 1], z = gp[3 * i + 2];
-        row[3] = x;
-        row[4] = y;
-        row[5] = z;
-        row[6] = x * x + y * y;
-        row[7] = z * z;
-        qbad = !(__builtin_isfinite(row[0]) && __builtin_isfinite(row[1]) &&
-                 __builtin_isfinite(row[2]));
-        a0 = ga[(size_t)i * NWg];
-        if (NWg > 1) a1 = ga[(size_t)i * NWg + 1] & lastmask;
-        else a0 &= lastmask;
-      }
-      double4* d = reinterpret_cast<double4*>(pt + 8 * i);
-      d[0] = make_double4(row[0], row[1], row[2], row[3]);
-      d[1] = make_double4(row[4], row[5], row[6], row[7]);
-      adjF[2 * i] = a0;
-      adjF[2 * i + 1] = a1;
+    if (tid < n) {
+      // vehicle tid: q into the scratch, vel (the epilogue's damping term)
+      const int v = tid;
+      qs[3 * v] = X.q0;
+      qs[3 * v + 1] = X.q1;
+      qs[3 * v + 2] = X.q2;
+      velv[3 * v] = X.v0;
+      velv[3 * v + 1] = X.v1;
+      velv[3 * v + 2] = X.v2;
+      qbad = !(__builtin_isfinite(X.q0) && __builtin_isfinite(X.q1) && __builtin_isfinite(X.q2));
     }
-    for (int k = tid; k < kW * R * 3; k += nthreads) acc[k] = 0.0;
+    if (tid < R) {
+      // formation row tid: its point and adjacency (zeros past n)
+      const int i = tid;
+      double row[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+      if (i < n) {
+        Pinv[Pt[i]] = (uint16_t)i;
+        const double x = X.px, y = X.py, z = X.pz;
+        row[0] = x;
+        row[1] = y;
+        row[2] = z;
+        row[3] = x * x + y * y;
+        row[4] = z * z;
+      }
+      pt[8 * i + 3] = row[0];
+      reinterpret_cast<double4*>(pt + 8 * i)[1] = make_double4(row[1], row[2], row[3], row[4]);
+      adjF[2 * i] = X.a0;
+      adjF[2 * i + 1] = X.a1;
+    }
     if (__any(qbad) && lane == 0) atomicOr(flags, 1u);
   }
   __syncthreads();
+  if (tid < R) {  // row i's q: vehicle Pt[i]'s (zeros past n)
+    const int i = tid;
+    double q0 = 0.0, q1 = 0.0, q2 = 0.0;
+    if (i < n) {
+      const int v = Pt[i];
+      q0 = qs[3 * v];
+      q1 = qs[3 * v + 1];
+      q2 = qs[3 * v + 2];
+    }
+    pt[8 * i] = q0;
+    pt[8 * i + 1] = q1;
+    pt[8 * i + 2] = q2;
+  }
   if (wave == 0) {  // record base of every row: a scan of the row popcounts
     int base = 0;
     for (int i0 = 0; i0 < R; i0 += 64) {
@@ -269,6 +305,7 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
                            (w ? (unsigned)__popcll(adjF[2 * i]) : 0u);
     etab[k] = ((unsigned)rowb[i] + below) << 8 | (unsigned)((word >> sh) & 0xFFull);
   }
+  for (int k = tid; k < kW * R * 3; k += nthreads) acc[k] = 0.0;  // (the q scratch is dead)
   const bool qfin = (*flags & 1u) == 0u;  // workgroup-uniform (set before the barriers)
   __syncthreads();
 
