@@ -94,22 +94,36 @@ extern "C" int acl_internal_kernel_times(double* ms, int* count) {
 }
 
 namespace acl_amd {
-// acl_swarm_stats: up to kStatsGrid workgroups stride over the 16-byte
-// records (B = 65 536: 64 per thread with one workgroup was ~0.1 ms of
-// serial loads), LDS accumulators, then integer atomics into the output
-// words (exact, order-free); extrema as u32 bit patterns (emax, and the
-// complement of the smallest margin: non-negative floats order like their
-// bits), converted by the last workgroup to finish (a done counter).
+// acl_swarm_stats: workgroups stride over the 16-byte records. Every count is
+// reduced in the wave first (DPP / shuffle sums; the histogram bins by
+// wave-aggregated atomics: one per distinct bin of the wave), so the LDS
+// accumulators take one atomic per wave and key instead of one per record
+// (a 1 024-record workgroup's same-address LDS atomics had serialised: 27 us
+// at C2). Up to kStatsSmall records run on one workgroup, which writes the
+// output words itself (no zeroing memsets before it); larger batches use up
+// to kStatsGrid workgroups and integer atomics into the zeroed output words
+// (exact, order-free), extrema as u32 bit patterns (emax, and the complement
+// of the smallest margin: non-negative floats order like their bits),
+// converted by the last workgroup to finish (a done counter).
 constexpr int kStatsThreads = 1024, kStatsHist = 64, kStatsKeys = 11, kStatsGrid = 64;
+constexpr int kStatsSmall = 16384;
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
 __global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_status_t* st, int B,
                                                               long long* counters, double* ext) {
-  // the 16 bytes of ext serve as scratch until the last workgroup writes
-  // them: [0] emax, [1] ~(smallest margin bits) (0 = +inf), [2] workgroups done
+  // (grid > 1) the 16 bytes of ext serve as scratch until the last workgroup
+  // writes them: [0] emax, [1] ~(smallest margin bits) (0 = +inf), [2]
+  // workgroups done
   unsigned* scratch = reinterpret_cast<unsigned*>(ext);
   __shared__ unsigned long long cnt[kStatsKeys + kStatsHist];
   __shared__ unsigned emax, mmin;
   __shared__ bool last;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
   for (int k = tid; k < kStatsKeys + kStatsHist; k += kStatsThreads) cnt[k] = 0ull;
   if (tid == 0) {
     emax = 0u;
@@ -118,9 +132,14 @@ __global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_st
   __syncthreads();
   unsigned long long c[kStatsKeys] = {};
   unsigned em = 0u, mm = 0x7F800000u;
-  for (int b = blockIdx.x * kStatsThreads + tid; b < B; b += gridDim.x * kStatsThreads) {
-    const acl_swarm_status_t s = st[b];
-    c[0] += 1;
+  const int stride = gridDim.x * kStatsThreads;
+  // (the loop bound is wave-uniform: every lane of a wave iterates together)
+  for (int b0 = blockIdx.x * kStatsThreads + (tid & ~63); b0 < B; b0 += stride) {
+    const int b = b0 + lane;
+    const bool ok = b < B;
+    acl_swarm_status_t s = {};
+    if (ok) s = st[b];
+    c[0] += ok ? 1 : 0;
     const uint32_t bits[7] = {ACL_SWARM_VALID, ACL_SWARM_AGREE, ACL_SWARM_CHANGED,
                               ACL_SWARM_NONFINITE, ACL_SWARM_BAD_INPUT, ACL_SWARM_CA_ACTIVE,
                               ACL_SWARM_FRAGILE};
@@ -129,18 +148,48 @@ __global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_st
     c[8] += s.n_invalid;
     c[9] += s.n_ca;
     c[10] += s.eff_rounds;
-    atomicAdd(&cnt[kStatsKeys + (s.eff_rounds < kStatsHist - 1 ? s.eff_rounds : kStatsHist - 1)],
-              1ull);
-    em = s.eff_rounds > em ? s.eff_rounds : em;
-    const unsigned mb = __float_as_uint(s.margin);
-    mm = mb < mm ? mb : mm;
+    // the histogram: one LDS atomic per distinct bin of the wave
+    const unsigned bin = s.eff_rounds < kStatsHist - 1 ? s.eff_rounds : kStatsHist - 1;
+    unsigned long long todo = __ballot(ok);
+    while (todo) {
+      const int leader = __ffsll((long long)todo) - 1;
+      const unsigned lb = (unsigned)__shfl((int)bin, leader, 64);
+      const unsigned long long m = __ballot(bin == lb) & todo;
+      if (lane == leader) atomicAdd(&cnt[kStatsKeys + lb], (unsigned long long)__popcll(m));
+      todo &= ~m;
+    }
+    if (ok) {
+      em = s.eff_rounds > em ? s.eff_rounds : em;
+      const unsigned mb = __float_as_uint(s.margin);
+      mm = mb < mm ? mb : mm;
+    }
   }
 #pragma unroll
-  for (int k = 0; k < kStatsKeys; ++k)
-    if (c[k]) atomicAdd(&cnt[k], c[k]);
-  atomicMax(&emax, em);
-  atomicMin(&mmin, mm);
+  for (int k = 0; k < kStatsKeys; ++k) {
+    const unsigned long long w = wave_sum_u64(c[k]);
+    if (lane == 0 && w) atomicAdd(&cnt[k], w);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned e2 = (unsigned)__shfl_xor((int)em, o, 64);
+    const unsigned m2 = (unsigned)__shfl_xor((int)mm, o, 64);
+    em = e2 > em ? e2 : em;
+    mm = m2 < mm ? m2 : mm;
+  }
+  if (lane == 0) {
+    atomicMax(&emax, em);
+    atomicMin(&mmin, mm);
+  }
   __syncthreads();
+  if (gridDim.x == 1) {  // the whole batch: write the outputs (no memsets)
+    for (int k = tid; k < kStatsKeys + kStatsHist; k += kStatsThreads)
+      counters[k] = (long long)cnt[k];
+    if (tid == 0) {
+      ext[0] = B > 0 ? (double)emax : 0.0;
+      ext[1] = B > 0 ? -(double)__uint_as_float(mmin) : -1.0;
+    }
+    return;
+  }
   for (int k = tid; k < kStatsKeys + kStatsHist; k += kStatsThreads)
     if (cnt[k]) atomicAdd(reinterpret_cast<unsigned long long*>(counters + k), cnt[k]);
   if (tid == 0) {
@@ -167,10 +216,12 @@ extern "C" acl_status_t acl_swarm_stats(const acl_swarm_status_t* status, int32_
   if (!counters || !extrema || (B > 0 && !status))
     return acl__set_error("acl_swarm_stats: null argument");
   const hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(counters, 0, ACL_STATS_COUNTERS * sizeof(int64_t), s) != hipSuccess ||
-      hipMemsetAsync(extrema, 0, 2 * sizeof(double), s) != hipSuccess)
+  const int grid =
+      B > kStatsSmall ? std::min(kStatsGrid, (B + kStatsThreads - 1) / kStatsThreads) : 1;
+  if (grid > 1 &&
+      (hipMemsetAsync(counters, 0, ACL_STATS_COUNTERS * sizeof(int64_t), s) != hipSuccess ||
+       hipMemsetAsync(extrema, 0, 2 * sizeof(double), s) != hipSuccess))
     return acl__set_error("acl_swarm_stats: hipMemsetAsync failed");
-  const int grid = B > 0 ? std::min(kStatsGrid, (B + kStatsThreads - 1) / kStatsThreads) : 1;
   hipLaunchKernelGGL(stats_kernel, dim3(grid), dim3(kStatsThreads), 0, s, status, B,
                      (long long*)counters, extrema);
   const hipError_t e = hipGetLastError();

@@ -1,5 +1,7 @@
 """acl_swarm_stats (the per-solve convergence counters of SURVEY §8e) on the
-GPU against its torch statement in aclswarm_amd/dist.py, bit for bit."""
+GPU against its torch statement in aclswarm_amd/dist.py, bit for bit: one
+workgroup writing the outputs itself (B <= 16 384) and the multi-workgroup
+atomics (B > 16 384)."""
 import numpy as np
 import pytest
 import torch
@@ -24,7 +26,7 @@ def _records(rng, B):
     return st
 
 
-@pytest.mark.parametrize("B", [0, 1, 1000, 70001])
+@pytest.mark.parametrize("B", [0, 1, 1000, 4096, 16384, 16385, 70001])
 def test_stats_native_matches_torch(B):
     rng = np.random.RandomState(B)
     st = torch.from_numpy(_records(rng, B))
