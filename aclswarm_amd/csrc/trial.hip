@@ -74,6 +74,7 @@ inline TrLayout tr_layout(int n, int B) {
 
 struct TrialDev {
   int n, B, K, step, k;
+  int F;  // formations in the table (acl_trial_init: 0, no range to check yet)
   int central;
   const int32_t* fseq;
   int32_t* fidx;
@@ -150,7 +151,7 @@ __global__ void __launch_bounds__(kTrBlock) trial_init_kernel(const TrialDev D) 
     t.done_step = -1;
     D.ts[b] = t;
     D.flush[b] = 0;
-    D.fidx[b] = D.fseq[(size_t)b * K];
+    D.fidx[b] = D.fseq[(size_t)b * K];  // (range-checked at every step: trial_pre_kernel)
     D.ctlMode[b] = 0;
     D.cst[b] = acl_swarm_status_t{};
   }
@@ -162,6 +163,19 @@ __global__ void __launch_bounds__(64) trial_pre_kernel(const TrialDev D) {
   const size_t bn = (size_t)b * n;
   acl_trial_status_t t = D.ts[b];  // (every thread: uniform decisions)
   int due = 0, zs = 0, f = D.fidx[b];
+  // a formation index outside the table ends the trial before anything of
+  // the table is read (the control stage reads fidx[b] every step)
+  bool fbad = false;
+  for (int k = 0; k < D.K; ++k) {
+    const int x = D.fseq[(size_t)b * D.K + k];
+    fbad |= x < 0 || x >= D.F;
+  }
+  if (fbad && t.done_step < 0) {
+    t.last_state = t.state;
+    t.state = ACL_TRIAL_TERMINATE;
+    t.done_step = D.step;
+  }
+  if (fbad) f = 0;
   if (t.done_step < 0) {
     bool now = false;
     if (t.commit) {
@@ -198,6 +212,7 @@ __global__ void __launch_bounds__(64) trial_pre_kernel(const TrialDev D) {
     }
   }
   if (tid == 0) {
+    if (fbad) D.fidx[b] = 0;
     if (zs) {
       D.fidx[b] = f;
       D.ctlMode[b] = 0;
@@ -631,7 +646,7 @@ acl_amd::TrialDev trial_dev(const acl_trial_args_t* a, int n) {
   unsigned char* ws = (unsigned char*)a->workspace;
   unsigned char* wc = ws + W.E.ctl;
   TrialDev D;
-  D.n = n; D.B = a->B; D.K = a->K; D.step = 0; D.k = 0;
+  D.n = n; D.B = a->B; D.K = a->K; D.step = 0; D.k = 0; D.F = 0;
   D.central = a->tp.ep.assignment == ACL_ASSIGN_CENTRAL;
   D.fseq = a->fseq; D.fidx = a->fidx; D.q = a->q; D.vel = a->vel; D.P = a->P;
   D.flush = a->flush; D.ts = a->ts; D.ctl_on = a->ctl_on; D.ring_u = a->ring_u;
@@ -685,6 +700,8 @@ extern "C" acl_status_t acl_trial_batch(const acl_formations_t* F, const acl_tri
   const int B = a->B;
   if (B == 0 || a->steps == 0) return ACL_OK;
   TrialDev D = trial_dev(a, n);
+  D.F = F->n_formations;
+  if (D.F < 1) return acl__set_error("acl_trial_batch: n_formations < 1");
   const TrLayout W = tr_layout(n, B);
   unsigned char* ws = (unsigned char*)a->workspace;
   unsigned char* wc = ws + W.E.ctl;

@@ -435,6 +435,8 @@ class Trial:
         B, n, K = self.B, self.n, self.K
         Lb = int(self.tp.ep.bufflen)
         self.fseq = fseq.to(torch.int32).contiguous()
+        if tuple(self.fseq.shape) != (B, K):
+            raise ValueError("Trial: fseq must be [B][K]")
         self.fidx = torch.empty(B, dtype=torch.int32, device=dev)
         self.q = q.clone().contiguous()
         self.vel = vel.clone().contiguous()

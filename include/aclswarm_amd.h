@@ -636,7 +636,9 @@ acl_status_t acl_episode_batch(const acl_formations_t* formations,
  * modelled); the zero command's collision-avoidance flag is taken as 0; the
  * watchdog counts from the first tick.
  * Device pointers, updated in place (a trial continues across calls):
- *   fseq [B][K] formation indices; fidx [B] out: the formation of each
+ *   fseq [B][K] formation indices (a trial with an index outside [0,
+ *   n_formations) ends at once: TERMINATE, nothing of the table read, its
+ *   fidx 0); fidx [B] out: the formation of each
  *   swarm's controllers; q, vel [B][n][3]; P [B][n] (identity at the start);
  *   flush [B]; ts [B] acl_trial_status_t (zeroed before the first call, then
  *   acl_trial_init); ctl_on [B][n] u8; ring_u [B][bufflen][n] f64,

@@ -188,3 +188,20 @@ def test_trial_chunks_equal_one_call(cuda):
     for k in ("q", "vel", "P", "flush", "ts", "ctl_on", "ring_u", "ring_ca", "posf", "dist",
               "t_conv", "t_avoid", "n_assign", "fidx"):
         assert torch.equal(getattr(tr1, k), getattr(tr2, k)), k
+
+
+def test_trial_formation_index_out_of_range(cuda):
+    """A trial whose formation sequence names a formation outside the table
+    ends at its first step (TERMINATE, nothing of the table read); the other
+    trials of the batch run as they do alone."""
+    case = _swarm6_case(B=3)
+    bad = case["fseq"].copy()
+    bad[1, 2] = 7  # three formations in the table
+    case_bad = dict(case, fseq=bad)
+    tr_bad, h_bad, _ = _run(case_bad, cuda, 200)
+    tr_ok, h_ok, _ = _run(case, cuda, 200)
+    st = tr_bad.status()
+    assert st[1]["state"] == T.TERMINATE and st[1]["done_step"] == 0
+    for b in (0, 2):
+        assert np.array_equal(h_bad["q"][:, b], h_ok["q"][:, b])
+        assert np.array_equal(h_bad["state"][:, b], h_ok["state"][:, b])
