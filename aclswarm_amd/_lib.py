@@ -22,7 +22,7 @@ FLAG_CHANGED = 0x04
 FLAG_NONFINITE = 0x08
 FLAG_BAD_INPUT = 0x10
 FLAG_CA_ACTIVE = 0x20
-ABI_VERSION = 9  # include/aclswarm_amd.h ACL_ABI_VERSION
+ABI_VERSION = 10  # include/aclswarm_amd.h ACL_ABI_VERSION
 FLAG_FRAGILE = 0x40
 FRAGILE_MARGIN = 1e-6
 
@@ -82,7 +82,8 @@ class SolveArgs(ct.Structure):
                 ("early_exit", ct.c_int32), ("do_control", ct.c_int32),
                 ("align_Rt", ct.c_void_p), ("gate_margin", ct.c_void_p),
                 ("skip_margin", ct.c_int32),
-                ("P_rows", ct.c_void_p), ("P_rows_on", ct.c_void_p)]
+                ("P_rows", ct.c_void_p), ("P_rows_on", ct.c_void_p),
+                ("ws_persistent", ct.c_int32)]
 
 
 class ControlArgs(ct.Structure):

@@ -107,7 +107,7 @@ __device__ void gain_swarm(const CtlParams& P, int b) {
   double* red = reinterpret_cast<double*>(smem + L.red) + wave * 64 * 3;
   double* atab = reinterpret_cast<double*>(smem + L.atab);
 #if ACL_GAIN_FASTMATH
-  for (int k = tid; k < ACL_ATAB_N; k += kB) atab[k] = ACL_ATAB[k / 5][k % 5];
+  for (int k = tid; k < ACL_ATAB_N; k += kB) atab[k] = ACL_ATAB_AT(k);
 #else
   for (int k = tid; k < ACL_ATAB_N; k += kB) atab[k] = kAtanTab[k / 6][k % 6];
 #endif
@@ -761,6 +761,31 @@ __device__ __forceinline__ bool ca_resolve_serial(int nslot, double* caA, signed
 #define CPROF_T(v)
 #define CPROF_ADD(acc, x)
 #endif
+// The collision list's counters (WsLayout::cacount: [0] entries, [1]
+// workgroups done) are zero between calls, so a persistent workspace needs no
+// memset per solve (acl_solve_args_t::ws_persistent): the launch's first
+// max(count, 1) workgroups each add one to [1] when they are done (every one
+// of them read the count at its start, before its own increment, so all read
+// the same count), and the last of them zeroes both. A workgroup past them
+// reads either that count or 0 and takes no part either way -- so an
+// uncrowded launch costs one atomic, not one per workgroup (8 192 same-address
+// returning atomics had made the C3 launch 6 -> 97 us). The count is clamped
+// to the batch: a list is never longer than B.
+__device__ __forceinline__ unsigned ca_list_count(const CtlParams& P) {
+  const unsigned c = *P.ca_count;
+  return c < (unsigned)P.B ? c : (unsigned)P.B;
+}
+
+__device__ __forceinline__ void ca_list_release(const CtlParams& P, unsigned count) {
+  const unsigned g = gridDim.x, parts = count == 0u ? 1u : (count < g ? count : g);
+  if (blockIdx.x >= parts) return;  // workgroup-uniform
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(P.ca_count + 1, 1u) == parts - 1u) {
+    atomicExch(P.ca_count, 0u);
+    atomicExch(P.ca_count + 1, 0u);
+  }
+}
+
 __global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
@@ -777,7 +802,7 @@ __global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
   signed char* tS = reinterpret_cast<signed char*>(wb + L.ts);
   unsigned* nca = reinterpret_cast<unsigned*>(smem + L.nca);
   const acl_safety_params_t sp = P.s;
-  const unsigned count = *P.ca_count;
+  const unsigned count = ca_list_count(P);
   for (unsigned it = blockIdx.x; it < count; it += gridDim.x) {
     const int b = (int)P.ca_list[it];
     const double* gq = P.q + (size_t)b * n * 3;
@@ -900,6 +925,7 @@ __global__ void __launch_bounds__(64 * kCaWaves) ca_kernel(const CtlParams P) {
       P.status[b].flags |= (uint32_t)ACL_SWARM_CA_ACTIVE;
     }
   }
+  ca_list_release(P, count);
 }
 
 // ---- collisionAvoidance by pairs (n <= 128) ----------------------------------
@@ -1150,7 +1176,7 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
   // [0] nc, [5] modified, [6] pairs handed out, [8..12] class counts
   int* misc = reinterpret_cast<int*>(smem + L.misc);
   const acl_safety_params_t sp = P.s;
-  const unsigned count = *P.ca_count;
+  const unsigned count = ca_list_count(P);
   for (unsigned itb = blockIdx.x; itb < (ACL_CA_STOP < 1 ? 0u : count); itb += gridDim.x) {
     const int b = (int)P.ca_list[itb];
     const double* gq = P.q + (size_t)b * n * 3;
@@ -1432,6 +1458,7 @@ __global__ void __launch_bounds__(kCaPT, ACL_CA_OCC) ca_pair_kernel(const CtlPar
     }
     __syncthreads();  // q, cl and misc are rewritten for the next listed swarm
   }
+  ca_list_release(P, count);
 }
 
 // acl_control_batch's hand-off: P must be a permutation (else BAD_INPUT and

@@ -24,13 +24,13 @@ constexpr int kCtlBlock = 256;
 #if ACL_GAIN_FASTMATH
 #define ACL_GAIN_SQRT sqrt_nr1
 #define ACL_GAIN_ATAN acl_atan_b
-#define ACL_ATAB_N 170
-#define ACL_ATAB kAtanBTab
+#define ACL_ATAB_N 68  // {c_k, a_k} of kAtanBTab's 34 rows
+#define ACL_ATAB_AT(k) kAtanBTab[(k) >> 1][((k) & 1) ? 4 : 2]
 #else
 #define ACL_GAIN_SQRT sqrt_nr
 #define ACL_GAIN_ATAN acl_atan_tab
 #define ACL_ATAB_N 30
-#define ACL_ATAB kAtanTab
+#define ACL_ATAB_AT(k) kAtanTab[(k) / 6][(k) % 6]
 #endif
 constexpr int kCtlWaves = kCtlBlock / 64;
 
@@ -385,7 +385,7 @@ __device__ __forceinline__ void pair_gain_swarm(const CtlParams& P, int b, int f
   double* uo = reinterpret_cast<double*>(smem + L.out);
   double* atab = reinterpret_cast<double*>(smem + L.atab);
 #if ACL_GAIN_FASTMATH
-  for (int k = tid; k < ACL_ATAB_N; k += nthreads) atab[k] = ACL_ATAB[k / 5][k % 5];
+  for (int k = tid; k < ACL_ATAB_N; k += nthreads) atab[k] = ACL_ATAB_AT(k);
 #else
   for (int k = tid; k < ACL_ATAB_N; k += nthreads) atab[k] = kAtanTab[k / 6][k % 6];
 #endif

@@ -213,7 +213,7 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
 
   // ---- setup: the caller has written Pt[tid] (thread tid reads it back
   // here, so no barrier is needed first); every other table is built here
-  for (int k = tid; k < ACL_ATAB_N; k += nthreads) atab[k] = ACL_ATAB[k / 5][k % 5];
+  for (int k = tid; k < ACL_ATAB_N; k += nthreads) atab[k] = ACL_ATAB_AT(k);
   if (GM && tid == 0) gmw = (unsigned long long)__double_as_longlong(__builtin_inf());
   if (tid == 0) {
     *caw = 0u;
@@ -402,8 +402,13 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
         gate_decide_t<GM>(fcst(cst, FC_TXY), fcst(cst, FC_TZ), fcst(cst, FC_WIN), e_xy, e_z, q0,
                           q1, q2, bi.z, bj.z, bi.w, bj.w, pix, piy, piz, pjx, pjy, pjz, gxy, gz,
                           gmxy, gmz);
+#if ACL_DIAG_NOATAN  // diagnostic bound (wrong results): linear scale terms
+        if (gxy) Fxy = fcst(cst, FC_K1XY) * (fcst(cst, FC_K2XY) * e_xy);
+        if (gz) Fz = fcst(cst, FC_K1Z) * (fcst(cst, FC_K2Z) * e_z);
+#else
         if (gxy) Fxy = fcst(cst, FC_K1XY) * ACL_GAIN_ATAN(fcst(cst, FC_K2XY) * e_xy, atab);
         if (gz) Fz = fcst(cst, FC_K1Z) * ACL_GAIN_ATAN(fcst(cst, FC_K2Z) * e_z, atab);
+#endif
       }
       const double f0 = Fxy * q0, f1 = Fxy * q1, f2 = Fz * q2;
       // row i: up_ij = A_ij q + F q (kp is applied per vehicle)

@@ -95,8 +95,8 @@ extern "C" int acl_internal_kernel_times(double* ms, int* count) {
 
 namespace acl_amd {
 // acl_swarm_stats: workgroups stride over the 16-byte records. Every count is
-// reduced in the wave first (DPP / shuffle sums; the histogram bins by
-// wave-aggregated atomics: one per distinct bin of the wave), so the LDS
+// reduced in the wave first (DPP / shuffle sums; the histogram by one ballot
+// per distinct bin of the wave into lane `bin`'s register), so the LDS
 // accumulators take one atomic per wave and key instead of one per record
 // (a 1 024-record workgroup's same-address LDS atomics had serialised: 27 us
 // at C2). Up to kStatsSmall records run on one workgroup, which writes the
@@ -106,7 +106,7 @@ namespace acl_amd {
 // of the smallest margin: non-negative floats order like their bits),
 // converted by the last workgroup to finish (a done counter).
 constexpr int kStatsThreads = 1024, kStatsHist = 64, kStatsKeys = 11, kStatsGrid = 64;
-constexpr int kStatsSmall = 16384;
+constexpr int kStatsSmall = 16384, kStatsPre = 4;
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x) {
 #pragma unroll
@@ -130,32 +130,31 @@ __global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_st
     mmin = 0x7F800000u;  // +inf
   }
   __syncthreads();
+  static_assert(kStatsHist == 64, "one histogram bin per lane");
   unsigned long long c[kStatsKeys] = {};
+  unsigned hist = 0u;  // this lane's bin of the wave's histogram
   unsigned em = 0u, mm = 0x7F800000u;
   const int stride = gridDim.x * kStatsThreads;
-  // (the loop bound is wave-uniform: every lane of a wave iterates together)
-  for (int b0 = blockIdx.x * kStatsThreads + (tid & ~63); b0 < B; b0 += stride) {
-    const int b = b0 + lane;
-    const bool ok = b < B;
-    acl_swarm_status_t s = {};
-    if (ok) s = st[b];
+  const uint32_t bits[7] = {ACL_SWARM_VALID, ACL_SWARM_AGREE, ACL_SWARM_CHANGED,
+                            ACL_SWARM_NONFINITE, ACL_SWARM_BAD_INPUT, ACL_SWARM_CA_ACTIVE,
+                            ACL_SWARM_FRAGILE};
+  // one record per lane (ok: the lane has one); wave-uniform control
+  auto take = [&](const acl_swarm_status_t& s, bool ok) {
     c[0] += ok ? 1 : 0;
-    const uint32_t bits[7] = {ACL_SWARM_VALID, ACL_SWARM_AGREE, ACL_SWARM_CHANGED,
-                              ACL_SWARM_NONFINITE, ACL_SWARM_BAD_INPUT, ACL_SWARM_CA_ACTIVE,
-                              ACL_SWARM_FRAGILE};
 #pragma unroll
     for (int k = 0; k < 7; ++k) c[1 + k] += (s.flags & bits[k]) ? 1 : 0;
     c[8] += s.n_invalid;
     c[9] += s.n_ca;
     c[10] += s.eff_rounds;
-    // the histogram: one LDS atomic per distinct bin of the wave
+    // the histogram: lane h of the wave counts bin h (kStatsHist == 64), one
+    // ballot per distinct bin of the wave; added to LDS once per wave below
     const unsigned bin = s.eff_rounds < kStatsHist - 1 ? s.eff_rounds : kStatsHist - 1;
     unsigned long long todo = __ballot(ok);
     while (todo) {
       const int leader = __ffsll((long long)todo) - 1;
       const unsigned lb = (unsigned)__shfl((int)bin, leader, 64);
       const unsigned long long m = __ballot(bin == lb) & todo;
-      if (lane == leader) atomicAdd(&cnt[kStatsKeys + lb], (unsigned long long)__popcll(m));
+      hist += (unsigned)lane == lb ? (unsigned)__popcll(m) : 0u;
       todo &= ~m;
     }
     if (ok) {
@@ -163,12 +162,28 @@ __global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_st
       const unsigned mb = __float_as_uint(s.margin);
       mm = mb < mm ? mb : mm;
     }
+  };
+  // kStatsPre records per lane are loaded before any is reduced (their HBM
+  // latencies overlap: one round trip per kStatsPre strides, not per stride);
+  // the loop bounds are wave-uniform: every lane of a wave iterates together
+  for (int b1 = blockIdx.x * kStatsThreads + (tid & ~63); b1 < B; b1 += kStatsPre * stride) {
+    acl_swarm_status_t sp[kStatsPre];
+#pragma unroll
+    for (int u = 0; u < kStatsPre; ++u) {
+      const int b = b1 + u * stride + lane;
+      sp[u] = acl_swarm_status_t{};
+      if (b < B) sp[u] = st[b];
+    }
+#pragma unroll
+    for (int u = 0; u < kStatsPre; ++u)
+      if (b1 + u * stride < B) take(sp[u], b1 + u * stride + lane < B);
   }
 #pragma unroll
   for (int k = 0; k < kStatsKeys; ++k) {
     const unsigned long long w = wave_sum_u64(c[k]);
     if (lane == 0 && w) atomicAdd(&cnt[k], w);
   }
+  if (hist) atomicAdd(&cnt[kStatsKeys + lane], (unsigned long long)hist);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const unsigned e2 = (unsigned)__shfl_xor((int)em, o, 64);
@@ -286,7 +301,9 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
     C.all_uniform = 0;
     C.F = F->n_formations;
     C.gate_margin = a->gate_margin;
-    if (hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
+    // the list counters ([0] entries, [1] workgroups done): zero unless the
+    // caller keeps them zero between calls (ws_persistent)
+    if (!a->ws_persistent && hipMemsetAsync(C.ca_count, 0, 2 * sizeof(unsigned), s) != hipSuccess)
       return acl__set_error("hipMemsetAsync failed");
   }
   // The control phase runs inside the auction's workgroups (one launch, the
@@ -359,7 +376,7 @@ acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_a
   const acl_status_t st = ctl_params(F, a, C);
   if (st != ACL_OK || a->B == 0) return st;
   if (flags & CTL_MIXED) C.all_uniform = 0;
-  if ((flags & CTL_RESET) && hipMemsetAsync(C.ca_count, 0, sizeof(unsigned), s) != hipSuccess)
+  if ((flags & CTL_RESET) && hipMemsetAsync(C.ca_count, 0, 2 * sizeof(unsigned), s) != hipSuccess)
     return acl__set_error("hipMemsetAsync failed");
   hipError_t e = hipSuccess;
   if (flags & CTL_PREP) {

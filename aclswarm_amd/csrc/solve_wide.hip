@@ -345,7 +345,7 @@ __device__ __forceinline__ void wide_control(KCtlParams* Pp, int b, int f, unsig
   unsigned* caw = reinterpret_cast<unsigned*>(smem + L.caw);
   const unsigned long long lastmask = (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
 
-  for (int k = tid; k < ACL_ATAB_N; k += kWBlock) atab[k] = ACL_ATAB[k / 5][k % 5];
+  for (int k = tid; k < ACL_ATAB_N; k += kWBlock) atab[k] = ACL_ATAB_AT(k);
   if (tid == 0) {
     *flags = 0u;
     *caw = 0u;

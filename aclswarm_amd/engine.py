@@ -114,26 +114,41 @@ class FormationTable:
 
 
 _WS = {}
+# per device: the (n, B) whose collision-list counters the cached workspace
+# holds at zero ("all": freshly zero-filled). The counters' offset depends on
+# n and B, so a call of another shape reuses their bytes for other data.
+_WS_CLEAN = {}
 
 
 def workspace(n, B, device):
-    """Device workspace for acl_solve_batch (cached per device, grown on demand)."""
+    """Device workspace for acl_solve_batch / acl_control_batch (cached per
+    device, grown on demand, zero-filled when allocated)."""
     need = int(L.lib().acl_solve_workspace_bytes(n, B))
     key = str(device)
     ws = _WS.get(key)
     if ws is None or ws.numel() < need:
-        ws = torch.empty(max(need, 1), dtype=torch.uint8, device=device)
+        ws = torch.zeros(max(need, 1), dtype=torch.uint8, device=device)
         _WS[key] = ws
+        _WS_CLEAN[key] = "all"
     return ws
+
+
+def _counters_zero(device, n, B):
+    """acl_solve_args_t::ws_persistent applies: the cached workspace holds this
+    shape's collision-list counters at zero (the last call that could touch
+    them had this shape and left them zero, or the buffer is fresh)."""
+    return _WS_CLEAN.get(str(device)) in ("all", (n, B))
 
 
 def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
           do_control=True, want_who=False, want_align=False, want_gate_margin=False, out=None,
-          stream=None, margin=True, P_rows=None, P_rows_on=None):
+          stream=None, margin=True, P_rows=None, P_rows_on=None, persistent=True):
     """Run acl_solve_batch for B = q.shape[0] swarms. All tensors on device.
 
     margin=False sets acl_solve_args_t::skip_margin: the status margin is -1
-    and FRAGILE is never set; everything else is unchanged.
+    and FRAGILE is never set; everything else is unchanged. persistent=False
+    clears acl_solve_args_t::ws_persistent (the call memsets the collision-
+    list counters itself; the outputs are the same).
 
     P_rows [B][n][n] int16 (uint16 bits) and P_rows_on [B] uint8
     (acl_solve_args_t::P_rows): a swarm with P_rows_on[b] != 0 runs its
@@ -180,6 +195,10 @@ def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
     a.early_exit = int(bool(early_exit))
     a.do_control = int(bool(do_control))
     a.skip_margin = 0 if margin else 1
+    # the call's memset of the collision-list counters only when the cached
+    # workspace does not hold them at zero for this shape (ABI 10)
+    clean = _counters_zero(dev, n, B)
+    a.ws_persistent = 1 if (persistent and clean) else 0
     if P_rows is not None:
         if P_rows_on is None or P_rows.shape != (B, n, n) or P_rows_on.shape != (B,):
             raise ValueError("P_rows [B][n][n] needs P_rows_on [B]")
@@ -196,7 +215,12 @@ def solve(table, fidx, q, vel, P_in, cntrl=None, safety=None, early_exit=True,
     F = table.struct()
     if stream is None:
         stream = torch.cuda.current_stream(dev).cuda_stream
+    _WS_CLEAN[str(dev)] = None  # (until the call has been enqueued)
     L.check(lib.acl_solve_batch(ct.byref(F), ct.byref(a), ct.c_void_p(stream)), "acl_solve_batch")
+    # with control the collision-avoidance launch left this shape's counters
+    # zero; an auction-only call leaves them as they were (other shapes' bytes
+    # may now hold its data)
+    _WS_CLEAN[str(dev)] = (n, B) if (do_control or clean) else None
     return out
 
 
@@ -269,8 +293,10 @@ def control(table, fidx, q, vel, P, cntrl=None, safety=None, want_gate_margin=Fa
     F = table.struct()
     if stream is None:
         stream = torch.cuda.current_stream(dev).cuda_stream
+    _WS_CLEAN[str(dev)] = None
     L.check(lib.acl_control_batch(ct.byref(F), ct.byref(a), ct.c_void_p(stream)),
             "acl_control_batch")
+    _WS_CLEAN[str(dev)] = (n, B)  # (it zeroes the counters first; its CA launch leaves them zero)
     return out
 
 

@@ -385,8 +385,15 @@ def main():
                     help="5: ADMM-structured gain blocks (the reference's gains); "
                          "9: general 3x3 blocks")
     ap.add_argument("--graph", action="store_true",
-                    help="time the step (solve + device-side stats) as one captured HIP graph "
-                         "replayed per step (launch-bound configurations such as C2; one GPU)")
+                    help="time the step (solve + device-side stats) as a captured HIP graph "
+                         "(launch-bound configurations such as C2; one GPU)")
+    ap.add_argument("--graph-steps", type=int, default=10,
+                    help="with --graph: steps captured per graph (the largest divisor of --steps "
+                         "not above it); the K timed steps are K / G replays, with one event "
+                         "pair around them all (per-step events add a gap at every replay)")
+    ap.add_argument("--no-persistent", action="store_true",
+                    help="solve with acl_solve_args_t::ws_persistent = 0 (a memset of the "
+                         "collision-list counters per call; A/B of ABI 10's persistent workspace)")
     ap.add_argument("--margin", action="store_true",
                     help="time the headline with the decision margin tracked (default: the "
                          "reference's work only, acl_solve_args_t::skip_margin; the margin-on "
@@ -447,9 +454,12 @@ def main():
 
     def solve(margin):
         engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"], early_exit=not args.full_rounds,
-                     out=out, stream=stream.cuda_stream, margin=margin)
+                     out=out, stream=stream.cuda_stream, margin=margin,
+                     persistent=not args.no_persistent)
 
     lib = L.lib()
+
+    graph_steps = [0]  # steps per captured graph (0: eager launches)
 
     def timed(margin, ktimes):
         """W warmup + K timed steps (barrier + synchronize on both sides),
@@ -493,27 +503,33 @@ def main():
             with torch.cuda.stream(gs):  # one eager step on the capture stream first
                 engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"],
                              early_exit=not args.full_rounds, out=out, stream=gs.cuda_stream,
-                             margin=margin)
+                             margin=margin, persistent=not args.no_persistent)
                 D.gather_results(out["P_out"], out["status"])
             torch.cuda.synchronize()
+            # G steps per graph (G divides K: exactly K steps are timed)
+            G = max(g for g in range(1, max(1, min(args.graph_steps, args.steps)) + 1)
+                    if args.steps % g == 0)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=gs):
-                engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"],
-                             early_exit=not args.full_rounds, out=out, stream=gs.cuda_stream,
-                             margin=margin)
-                gres = D.gather_results(out["P_out"], out["status"])
+                for _ in range(G):
+                    engine.solve(T, w["fidx"], w["q"], w["vel"], w["P_in"],
+                                 early_exit=not args.full_rounds, out=out, stream=gs.cuda_stream,
+                                 margin=margin, persistent=not args.no_persistent)
+                    gres = D.gather_results(out["P_out"], out["status"])
             with torch.cuda.stream(gs):
                 graph.replay()
             torch.cuda.synchronize()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0 = time.perf_counter()
             with torch.cuda.stream(gs):
-                for k in range(args.steps):
-                    evs[k][0].record(gs)
+                ev0.record(gs)
+                for k in range(args.steps // G):
                     graph.replay()
-                    evs[k][1].record(gs)
+                ev1.record(gs)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / args.steps
-            call_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+            call_ms = ev0.elapsed_time(ev1) / args.steps
+            graph_steps[0] = G
             res = gres
         dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
         if world > 1:
@@ -689,7 +705,8 @@ def main():
             "decision_margin": ("tracked" if args.margin else
                                 "not tracked in the timed steps (skip_margin); see `margin`"),
             "parallelism": f"swarm-sharded x{world}",
-            "launch": ("one captured HIP graph per step (solve + device-side stats), replayed"
+            "launch": (f"captured HIP graph of {graph_steps[0]} step(s) (solve + device-side "
+                       "stats per step), replayed; one event pair around the timed replays"
                        if args.graph and world == 1 else "eager launches on one stream"),
             "gains": ("synthetic ADMM-structured blocks [a b 0; c d 0; 0 0 e] "
                       "(solver.cpp:49-77), 5-entry records = 40 B/edge" if w["planes"] == 5 else

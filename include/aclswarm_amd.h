@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define ACL_ABI_VERSION 9
+#define ACL_ABI_VERSION 10
 
 typedef enum {
   ACL_OK = 0,
@@ -260,9 +260,12 @@ acl_status_t acl_swarm_stats(const acl_swarm_status_t* status, int32_t B, int64_
  *                      bytes (required): the auction kernel hands each
  *                      vehicle's adopted assignment to the control kernels
  *                      through it; for n > 128 it also holds the CBAA tables.
- * The call enqueues three kernels on `stream`: the auction over all B swarms,
- * the gain kernel (DistCntrl, saturation, the collision test) and the
- * collision-avoidance kernel for the vehicles the gain kernel listed.
+ * The call enqueues three kernels on `stream` (n > 64: four, the alignment
+ * first): the auction over all B swarms (with 5-entry gain records it also
+ * runs DistCntrl, saturation and the collision test for every swarm whose
+ * vehicles agree), the gain kernel (the other swarms) and the collision-
+ * avoidance kernel for the vehicles they listed; and, unless ws_persistent,
+ * a memset of the list counters before them.
  */
 typedef struct {
   int32_t B;
@@ -311,6 +314,16 @@ typedef struct {
                           the vehicles hold different assignments. A row that
                           is not such a permutation: BAD_INPUT. */
   const uint8_t* P_rows_on; /* [B] (with P_rows) */
+  int32_t ws_persistent; /* ABI 10. 0 (default): the call zeroes the workspace's
+                          collision-list counters first (one memset on the
+                          stream). 1: the caller zero-filled the workspace
+                          when it allocated it and has used it since only for
+                          acl_solve_batch / acl_control_batch calls with the
+                          same n and B (the counters' offset depends on both),
+                          one stream at a time: every such call with control
+                          leaves the counters zero (its collision-avoidance
+                          launch resets them), so the call enqueues no memset
+                          (a launch fewer per solve). */
 } acl_solve_args_t;
 
 /* Largest n acl_solve_batch accepts (512). */

@@ -138,3 +138,50 @@ def test_skip_margin_same_outcome(cuda, n):
         assert (b["status"]["margin"] == -1.0).all()
     ref = _oracle(pts, adjs, gains, fidx[:6], q[:6], vel[:6], P_in[:6])
     _compare({k: v[:6] for k, v in a.items()}, ref)
+
+
+@pytest.mark.parametrize("n", [20, 100, 200])
+def test_persistent_workspace_same_as_memset(cuda, n):
+    """acl_solve_args_t::ws_persistent (ABI 10): the collision-avoidance
+    launch leaves the list counters zero, so solves without the per-call
+    memset -- crowded swarms listed every call, an acl_control_batch call on
+    the same workspace in between -- give the outputs (n_ca counts and CA
+    flags included) of a solve that zeroes them first; a call of another
+    shape in between makes the next one zero them again (their offset moves)."""
+    import torch
+    from aclswarm_amd import engine
+    rng = np.random.RandomState(5300 + n)
+    F, B = 3, 40
+    pts, adjs, gains = _case(rng, n, F, disconnected=True)
+    dev = torch.device("cuda:0")
+    T = engine.FormationTable.from_host(pts, adjs, gains, device=dev, planes=5)
+    fidx = torch.from_numpy((np.arange(B) % F).astype(np.int32)).to(dev)
+    q = np.stack([H.random_positions(rng, n, 2.0 * n) for _ in range(B)])
+    q[::3, :, :2] *= 0.05  # crowded: listed for collision avoidance
+    qd = torch.from_numpy(q).to(dev)
+    vel = torch.from_numpy(rng.normal(0, 0.3, (B, n, 3))).to(dev)
+    P_in = torch.from_numpy(np.stack([H.random_perm(rng, n) for _ in range(B)]).view(np.int16)).to(dev)
+
+    def run(persistent, b=B):
+        o = engine.solve(T, fidx[:b], qd[:b], vel[:b], P_in[:b], persistent=persistent)
+        torch.cuda.synchronize()
+        return {k: v.cpu().numpy() for k, v in o.items()}
+
+    def same(got, ref, what):
+        for k in ("P_out", "status", "u", "u_safe", "ca_flag"):
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{k} ({what})")
+
+    ref = run(False)
+    st = engine.status_to_numpy(torch.from_numpy(ref["status"]))
+    assert (st["n_ca"] > 0).sum() >= B // 4  # many swarms listed
+    for it in range(3):
+        assert engine._counters_zero(dev, n, B)  # this call runs without the memset
+        same(run(True), ref, f"call {it}")
+        # a control call of the same shape on the same workspace between solves
+        engine.control(T, fidx, qd, vel, torch.from_numpy(ref["P_out"]).to(dev))
+    small = run(True, 9)  # another shape: its counters are zeroed by that call
+    same(small, {k: v[:9] for k, v in ref.items()}, "small")
+    assert not engine._counters_zero(dev, n, B)
+    same(run(True), ref, "after the small batch")
+    assert engine._counters_zero(dev, n, B)
+    same(run(True), ref, "persistent again")
