@@ -1129,8 +1129,16 @@ __global__ void __launch_bounds__(kJT) psd_jacobi_kernel(const Part* parts, doub
 // X_old: the block is read (Sr's mirror block too, through LDS, where it
 // meets a diagonal tile) and S, X are written to both, the mirror through the
 // LDS tile (coalesced); sum |dX| counts an off-diagonal pair twice.
+// pmf: the block's elements of the X22 quadrant also give the next
+// iteration's Pm = P_struct(M22), M22 = -S22 - mu X22 (pm_kernel's expression
+// on the S, X just written, the same bits), so no pm launch re-reads S and X.
+// A structured part's 2 x 2 groups (s even, the host checks) never straddle a
+// 32-aligned block, and P_struct of the symmetric M22 is symmetric bit for bit
+// (0.5 (x + y) of a mirrored pair; the odd terms negate as x - y = -(y - x)),
+// so the mirror block gets the same values.
 constexpr int kPB = 32;
-__global__ void __launch_bounds__(256) post_ut_kernel(const Part* parts, double mu, int tile) {
+__global__ void __launch_bounds__(256) post_ut_kernel(const Part* parts, double mu, int tile,
+                                                      int pmf) {
   const Part& P = parts[blockIdx.y];
   if (!P.sc->active) return;
   const int s = P.s, n2 = 2 * s;
@@ -1179,8 +1187,10 @@ __global__ void __launch_bounds__(256) post_ut_kernel(const Part* parts, double 
       tx[c][li] = Xn;
     }
   }
+  // the block meets the X22 quadrant (workgroup-uniform)
+  const bool pmb = pmf && i0 + kPB > s && j0 + kPB > s;
+  if (!dgb || pmb) __syncthreads();
   if (!dgb) {  // workgroup-uniform: the mirror block, rows j coalesced
-    __syncthreads();
 #pragma unroll
     for (int m = 0; m < kPB / 8; ++m) {
       const int c = lg + 8 * m, j = j0 + li, i = i0 + c;
@@ -1188,6 +1198,41 @@ __global__ void __launch_bounds__(256) post_ut_kernel(const Part* parts, double 
         const size_t et = j + (size_t)i * n2;
         P.S[et] = ts[li][c];
         P.X[et] = tx[li][c];
+      }
+    }
+  }
+  if (pmb) {
+    __shared__ double tp[kPB][kPB + 1];  // Pm of the block
+    // M22 at block-local (row r, column c): pm_kernel's (-1 S) + (-mu X)
+    auto Mv = [&](int r, int c) { return (-1.0 * ts[c][r]) + (-mu * tx[c][r]); };
+#pragma unroll
+    for (int m = 0; m < kPB / 8; ++m) {
+      const int c = lg + 8 * m, i = i0 + li, j = j0 + c;
+      if (i < n2 && j < n2 && i >= s && j >= s) {
+        const int a = i - s, b = j - s;
+        double v;
+        if (!P.st) {
+          v = Mv(li, c);
+        } else {  // pstruct_at: the group's rows li - (a & 1) + {0, 1}, columns likewise
+          const int r0 = li - (a & 1), c0 = c - (b & 1);
+          if ((a & 1) == (b & 1)) {
+            v = 0.5 * (Mv(r0, c0) + Mv(r0 + 1, c0 + 1));
+          } else {
+            const double bb = 0.5 * (Mv(r0, c0 + 1) - Mv(r0 + 1, c0));
+            v = (a & 1) ? -bb : bb;
+          }
+        }
+        P.Pm[a + (size_t)b * s] = v;
+        tp[c][li] = v;
+      }
+    }
+    if (!dgb) {
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < kPB / 8; ++m) {
+        const int c = lg + 8 * m, j = j0 + li, i = i0 + c;
+        if (j < n2 && i < n2 && i >= s && j >= s)
+          P.Pm[(j - s) + (size_t)(i - s) * s] = tp[li][c];
       }
     }
   }
@@ -1668,8 +1713,13 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
     ACL_HIP(hipGetLastError(), "setup kernels");
     // ---- ADMM iterations
     const double mu = prm.mu, eps = prm.epsEig;
+    // the iterations after the first take Pm from the previous post-process
+    // (post_ut_kernel's pmf: every structured part's s even)
+    bool pm_fused = true;
+    for (int p = 0; p < NP; ++p)
+      if (info[p].st && (info[p].s & 1)) pm_fused = false;
     for (int itr = 0; itr < prm.maxItr; ++itr) {
-      hipLaunchKernelGGL(pm_kernel, gS, dim3(kT), 0, st, dp, -1.0, -mu, 1);
+      if (itr == 0 || !pm_fused) hipLaunchKernelGGL(pm_kernel, gS, dim3(kT), 0, st, dp, -1.0, -mu, 1);
       ACL_HIP(gemm(J_YK, false, false), "gemm Yk");
       hipLaunchKernelGGL(rc_kernel, dim3(NP), dim3(kT), 0, st, dp, 1, mu);
       ACL_HIP(gemm(J_T, true, false), "gemm T");
@@ -1682,7 +1732,7 @@ extern "C" acl_status_t acl_admm_solve_batch(int32_t F, int32_t n, const double*
       {
         const int nbp = (n2max + kPB - 1) / kPB;
         hipLaunchKernelGGL(post_ut_kernel, dim3(nbp * (nbp + 1) / 2, NP), dim3(256), 0, st, dp, mu,
-                           JobLists::sym(J_S) ? gemm_tile_size() : (1 << 30));
+                           JobLists::sym(J_S) ? gemm_tile_size() : (1 << 30), pm_fused ? 1 : 0);
       }
       hipLaunchKernelGGL(check_kernel, dim3(1), dim3(1024), 0, st, dp, NP, prm.thresh,
                          prm.threshTr, X.d_cnt + 1);
