@@ -95,7 +95,7 @@ extern "C" int acl_internal_kernel_times(double* ms, int* count) {
 
 namespace acl_amd {
 // acl_swarm_stats: workgroups stride over the 16-byte records. Every count is
-// reduced in the wave first (DPP / shuffle sums; the histogram by one ballot
+// reduced in the wave first (DPP sums; the histogram by one ballot
 // per distinct bin of the wave into lane `bin`'s register), so the LDS
 // accumulators take one atomic per wave and key instead of one per record
 // (a 1 024-record workgroup's same-address LDS atomics had serialised: 27 us
@@ -108,10 +108,12 @@ namespace acl_amd {
 constexpr int kStatsThreads = 1024, kStatsHist = 64, kStatsKeys = 11, kStatsGrid = 64;
 constexpr int kStatsSmall = 16384, kStatsPre = 4;
 
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
+// (wave sums on DPP: common.h's ACL_WAVE_REDUCE, no LDS round trips)
+__device__ __forceinline__ unsigned op_uadd(unsigned a, unsigned b) { return a + b; }
+
+__device__ __forceinline__ unsigned wave_sum_u32(unsigned x) {
+  ACL_WAVE_REDUCE(x, op_uadd);
+  return (unsigned)__builtin_amdgcn_readlane((int)x, 63);
 }
 
 __global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_status_t* st, int B,
@@ -131,7 +133,9 @@ __global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_st
   }
   __syncthreads();
   static_assert(kStatsHist == 64, "one histogram bin per lane");
-  unsigned long long c[kStatsKeys] = {};
+  // per-lane counts in 32 bits: a lane takes at most B / (grid 1 024) records
+  // (eff_rounds <= 1 024 each), a wave's sums stay below 2^32 for B < 2^31
+  unsigned c[kStatsKeys] = {};
   unsigned hist = 0u;  // this lane's bin of the wave's histogram
   unsigned em = 0u, mm = 0x7F800000u;
   const int stride = gridDim.x * kStatsThreads;
@@ -140,19 +144,20 @@ __global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_st
                             ACL_SWARM_FRAGILE};
   // one record per lane (ok: the lane has one); wave-uniform control
   auto take = [&](const acl_swarm_status_t& s, bool ok) {
-    c[0] += ok ? 1 : 0;
+    c[0] += ok ? 1u : 0u;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) c[1 + k] += (s.flags & bits[k]) ? 1 : 0;
+    for (int k = 0; k < 7; ++k) c[1 + k] += (s.flags & bits[k]) ? 1u : 0u;
     c[8] += s.n_invalid;
     c[9] += s.n_ca;
     c[10] += s.eff_rounds;
     // the histogram: lane h of the wave counts bin h (kStatsHist == 64), one
-    // ballot per distinct bin of the wave; added to LDS once per wave below
+    // ballot per distinct bin of the wave (the bin read by readlane: no LDS
+    // round trip); added to LDS once per wave below
     const unsigned bin = s.eff_rounds < kStatsHist - 1 ? s.eff_rounds : kStatsHist - 1;
     unsigned long long todo = __ballot(ok);
     while (todo) {
       const int leader = __ffsll((long long)todo) - 1;
-      const unsigned lb = (unsigned)__shfl((int)bin, leader, 64);
+      const unsigned lb = (unsigned)__builtin_amdgcn_readlane((int)bin, leader);
       const unsigned long long m = __ballot(bin == lb) & todo;
       hist += (unsigned)lane == lb ? (unsigned)__popcll(m) : 0u;
       todo &= ~m;
@@ -178,19 +183,17 @@ __global__ void __launch_bounds__(kStatsThreads) stats_kernel(const acl_swarm_st
     for (int u = 0; u < kStatsPre; ++u)
       if (b1 + u * stride < B) take(sp[u], b1 + u * stride + lane < B);
   }
+  unsigned w[kStatsKeys];
 #pragma unroll
-  for (int k = 0; k < kStatsKeys; ++k) {
-    const unsigned long long w = wave_sum_u64(c[k]);
-    if (lane == 0 && w) atomicAdd(&cnt[k], w);
-  }
+  for (int k = 0; k < kStatsKeys; ++k) w[k] = wave_sum_u32(c[k]);
+  // lane k < kStatsKeys adds key k (one LDS atomic instruction per wave)
+  unsigned mine = 0u;
+#pragma unroll
+  for (int k = 0; k < kStatsKeys; ++k) mine = lane == k ? w[k] : mine;
+  if (lane < kStatsKeys && mine) atomicAdd(&cnt[lane], (unsigned long long)mine);
   if (hist) atomicAdd(&cnt[kStatsKeys + lane], (unsigned long long)hist);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned e2 = (unsigned)__shfl_xor((int)em, o, 64);
-    const unsigned m2 = (unsigned)__shfl_xor((int)mm, o, 64);
-    em = e2 > em ? e2 : em;
-    mm = m2 < mm ? m2 : mm;
-  }
+  em = wave_max_u32(em);
+  mm = ~wave_max_u32(~mm);
   if (lane == 0) {
     atomicMax(&emax, em);
     atomicMin(&mmin, mm);

@@ -18,7 +18,7 @@ for p in ${PART:-tests bench}; do
       timeout -k 10 600 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
       timeout -k 10 300 python bench.py --config c4 --no-cpu > $O/bench_c4.json 2> $O/bench_c4.err || { tail -20 $O/bench_c4.err; exit 1; }
       timeout -k 10 300 python bench.py --config c5 > $O/bench_c5.json 2> $O/bench_c5.err || { tail -20 $O/bench_c5.err; exit 1; }
-      timeout -k 10 300 python bench.py --config c2 --graph --no-cpu > $O/bench_c2.json 2> $O/bench_c2.err || { tail -20 $O/bench_c2.err; exit 1; }
+      timeout -k 10 300 python bench.py --config c2 --graph --graph-steps 10 --no-cpu > $O/bench_c2.json 2> $O/bench_c2.err || { tail -20 $O/bench_c2.err; exit 1; }
       for f in default c4 c5 c2; do python -c "
 import json; d=json.load(open('$O/bench_$f.json'))
 print('$f', round(d['value'],1), d['unit'], round(d['ms_per_step'],3), 'frac', round(d['roofline']['frac'],4), 'margin', d.get('margin',{}).get('value_margin_on'), 'crowded', d.get('ca_probe',{}).get('call_ms'))"; done ;;
