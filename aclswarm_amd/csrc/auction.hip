@@ -651,8 +651,12 @@ __global__ void __launch_bounds__(64) align_kernel(const SolveParams P) {
 // FUSE: phase 5, the control law of a swarm whose vehicles all adopted one
 // assignment, runs in this workgroup right after its auction (see below);
 // GM: the fused phase also reports the gate margin.
+#ifndef ACL_AUCTION_OCC_SMALL
+#define ACL_AUCTION_OCC_SMALL 6  // waves per SIMD the 128-thread (n <= 32) instantiation is built for
+#endif
 template <int NC, int kAB, bool FUSE, bool GM, bool MG>
-__global__ void __launch_bounds__(kAB, 6) auction_kernel(const SolveParams P) {
+__global__ void __launch_bounds__(kAB, kAB == 128 ? ACL_AUCTION_OCC_SMALL : 6)
+    auction_kernel(const SolveParams P) {
   constexpr int kAW = kAB / 64;  // waves per swarm
   constexpr int kCW = kAW < ACL_CBAA_WAVES ? kAW : ACL_CBAA_WAVES;  // CBAA round waves
   static_assert((kCW & (kCW - 1)) == 0, "ACL_CBAA_WAVES: a power of two");
