@@ -344,19 +344,17 @@ __device__ constexpr double kAtanBTab[34][5] = {
 // mantissa bits, (bits >> 21) - (123 << 2) + 1 clamped to [0, 33], four
 // integer instructions -- and atan(t) = t + t z (-1/3 + z/5 - z^2/7 + z^3/9
 // - z^4/11), z = t^2, is within 4e-16 relative on |t| <= 0.0625
-// (tests/test_fastmath.py). One reciprocal with one Newton step.
-// The LDS table holds {c_k, a_k} per row (kAtanBTab's columns 2 and 4, one
-// 16-byte read): rows 0..32 have na = db = 1 and nb = -c, so fma(na, |x|, nb)
-// = |x| - c and fma(da, |x|, db) = fma(c, |x|, 1) bit for bit; row 33 is
-// num = -1, den = |x| (selected).
+// (tests/test_fastmath.py). One reciprocal with one Newton step. The row's
+// five coefficients are five LDS reads: a 16-byte {c, a} row with the last
+// row selected measured no faster and cost the vector ALU -- which bounds the
+// fused kernel -- four selects per call (profiles/r6_ab_atan/).
 __device__ __forceinline__ double acl_atan_b(double x, const double* tab) {
   const double ax = fabs(x);
   int k = (int)(__float_as_uint((float)ax) >> 21) - (123 << 2) + 1;
   k = k < 0 ? 0 : (k > 33 ? 33 : k);
-  const double2 rw = *reinterpret_cast<const double2*>(tab + 2 * k);
-  const bool big = k == 33;
-  const double num = big ? -1.0 : ax - rw.x;
-  const double den = big ? ax : __builtin_fma(rw.x, ax, 1.0);
+  const double* rw = tab + 5 * k;
+  const double num = __builtin_fma(rw[0], ax, rw[1]);
+  const double den = __builtin_fma(rw[2], ax, rw[3]);
   double r = __builtin_amdgcn_rcp(den);
   r = __builtin_fma(__builtin_fma(-den, r, 1.0), r, r);
   const double t = num * r;
@@ -365,7 +363,7 @@ __device__ __forceinline__ double acl_atan_b(double x, const double* tab) {
   p = ACL_FMA_K(z, p, -1.0 / 7.0);
   p = ACL_FMA_K(z, p, 1.0 / 5.0);
   p = ACL_FMA_K(z, p, -1.0 / 3.0);
-  const double res = rw.y + __builtin_fma(t * z, p, t);
+  const double res = rw[4] + __builtin_fma(t * z, p, t);
   return (ax == __builtin_inf()) ? copysign(1.57079632679489655800e+00, x) : copysign(res, x);
 }
 

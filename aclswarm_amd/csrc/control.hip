@@ -761,16 +761,18 @@ __device__ __forceinline__ bool ca_resolve_serial(int nslot, double* caA, signed
 #define CPROF_T(v)
 #define CPROF_ADD(acc, x)
 #endif
-// The collision list's counters (WsLayout::cacount: [0] entries, [1]
-// workgroups done) are zero between calls, so a persistent workspace needs no
-// memset per solve (acl_solve_args_t::ws_persistent): the launch's first
-// max(count, 1) workgroups each add one to [1] when they are done (every one
-// of them read the count at its start, before its own increment, so all read
-// the same count), and the last of them zeroes both. A workgroup past them
-// reads either that count or 0 and takes no part either way -- so an
-// uncrowded launch costs one atomic, not one per workgroup (8 192 same-address
-// returning atomics had made the C3 launch 6 -> 97 us). The count is clamped
-// to the batch: a list is never longer than B.
+// The collision list's counters (WsLayout::cacount, kCaCounterBytes) are zero
+// between calls, so a persistent workspace needs no memset per solve
+// (acl_solve_args_t::ws_persistent). The launch's first max(entries, 1)
+// workgroups take part (each read the entry count at its start, before its
+// increment below, so all read the same count; a workgroup past them reads
+// either that count or 0 and takes no part either way -- an uncrowded launch
+// costs one atomic): each adds one to its group's counter (workgroup b in
+// group b mod kCaGroups), the group's last zeroes that counter and adds one to
+// [1], and the last group zeroes [1] and the entry count. (One counter for
+// every workgroup had made the C3 launch 6 -> 97 us: 8 192 returning atomics
+// on one address.) The count is clamped to the batch: a list is never longer
+// than B.
 __device__ __forceinline__ unsigned ca_list_count(const CtlParams& P) {
   const unsigned c = *P.ca_count;
   return c < (unsigned)P.B ? c : (unsigned)P.B;
@@ -780,9 +782,18 @@ __device__ __forceinline__ void ca_list_release(const CtlParams& P, unsigned cou
   const unsigned g = gridDim.x, parts = count == 0u ? 1u : (count < g ? count : g);
   if (blockIdx.x >= parts) return;  // workgroup-uniform
   __syncthreads();
-  if (threadIdx.x == 0 && atomicAdd(P.ca_count + 1, 1u) == parts - 1u) {
-    atomicExch(P.ca_count, 0u);
-    atomicExch(P.ca_count + 1, 0u);
+  if (threadIdx.x == 0) {
+    const unsigned grp = blockIdx.x % kCaGroups;
+    const unsigned gsize = (parts - 1u - grp) / kCaGroups + 1u;  // members grp, grp + 64, ... < parts
+    unsigned* gc = P.ca_count + kCaGroupStride * (1 + grp);
+    if (atomicAdd(gc, 1u) == gsize - 1u) {
+      atomicExch(gc, 0u);
+      const unsigned ng = parts < (unsigned)kCaGroups ? parts : (unsigned)kCaGroups;
+      if (atomicAdd(P.ca_count + 1, 1u) == ng - 1u) {
+        atomicExch(P.ca_count, 0u);
+        atomicExch(P.ca_count + 1, 0u);
+      }
+    }
   }
 }
 

@@ -24,8 +24,8 @@ constexpr int kCtlBlock = 256;
 #if ACL_GAIN_FASTMATH
 #define ACL_GAIN_SQRT sqrt_nr1
 #define ACL_GAIN_ATAN acl_atan_b
-#define ACL_ATAB_N 68  // {c_k, a_k} of kAtanBTab's 34 rows
-#define ACL_ATAB_AT(k) kAtanBTab[(k) >> 1][((k) & 1) ? 4 : 2]
+#define ACL_ATAB_N 170  // kAtanBTab's 34 rows of 5
+#define ACL_ATAB_AT(k) kAtanBTab[(k) / 5][(k) % 5]
 #else
 #define ACL_GAIN_SQRT sqrt_nr
 #define ACL_GAIN_ATAN acl_atan_tab

@@ -45,7 +45,8 @@ constexpr int kMaxNWide = 512;  // tables-in-HBM auction kernel (solve_wide.hip)
 //   u       [B][n][3] f64 DistCntrl output when the caller passes u = NULL
 //   calist  [B]    u32    swarms with a vehicle whose collisionAvoidance must
 //                         finish (appended once per swarm)
-//   cacount u32           entries of calist
+//   cacount u32           entries of calist, then the workgroup counters
+//                         (kCaCounterBytes, below)
 //   camask  [B][NW] u64   the swarm's vehicles within d_avoid_thresh of
 //                         another (bit v of word v/64; every word rewritten
 //                         by each control step's epilogue)
@@ -56,6 +57,13 @@ constexpr int kMaxNWide = 512;  // tables-in-HBM auction kernel (solve_wide.hip)
 //           align_kernel's results for the n <= 128 auction kernel; for
 //           n > 128 align_wide_kernel's (out [n][6] per vehicle, vadj
 //           [NW][n] u64, u64 gap, u32 flags)
+// The collision list's counters (WsLayout::cacount), u32 words: [0] entries,
+// [1] groups done, [kCaGroupStride (1 + g)] workgroups done of group g (the
+// collision-avoidance launch's workgroups g, g + kCaGroups, ...: 128 bytes
+// apart, so the groups' atomics meet in different cache lines)
+constexpr int kCaGroups = 64, kCaGroupStride = 32;
+constexpr size_t kCaCounterBytes = (size_t)kCaGroupStride * (1 + kCaGroups) * 4;
+
 struct WsLayout {
   size_t pt, mode, rows, vvalid, u, calist, cacount, camask, wide, wide_stride, align, align_stride,
       total;
@@ -73,7 +81,7 @@ __host__ __device__ inline WsLayout ws_layout(int n, int B) {
   W.vvalid = o;  o = ws_al(o + bb * nb);  // [B][n] u8: vehicle's own table valid (rows swarms)
   W.u = o;       o = ws_al(o + bb * nb * 3 * 8);
   W.calist = o;  o = ws_al(o + bb * 4);
-  W.cacount = o; o = ws_al(o + 16);
+  W.cacount = o; o = ws_al(o + kCaCounterBytes);
   W.camask = o;  o = ws_al(o + bb * (size_t)((n + 63) >> 6) * 8);
   W.wide = o;
   W.wide_stride = n > kMaxN ? ws_al((size_t)((n + 7) >> 3) * ((n + 7) >> 3) * 64 * 2) : 0;

@@ -424,7 +424,7 @@ extern "C" acl_status_t acl_episode_batch(const acl_formations_t* F, const acl_e
     if (r != ACL_OK) return r;
     C.keep = reinterpret_cast<const uint8_t*>(a->est) + offsetof(acl_episode_status_t, per_vehicle);
     C.keep_stride = (int)sizeof(acl_episode_status_t);
-    if (hipMemsetAsync(C.ca_count, 0, 2 * sizeof(unsigned), s) != hipSuccess)
+    if (hipMemsetAsync(C.ca_count, 0, kCaCounterBytes, s) != hipSuccess)
       return acl__set_error("hipMemsetAsync failed");
     if (launch_control_prep(C, a->P, B, s) != hipSuccess)
       return acl__set_error("control_prep launch failed");

@@ -306,7 +306,7 @@ extern "C" acl_status_t acl_solve_batch(const acl_formations_t* F, const acl_sol
     C.gate_margin = a->gate_margin;
     // the list counters ([0] entries, [1] workgroups done): zero unless the
     // caller keeps them zero between calls (ws_persistent)
-    if (!a->ws_persistent && hipMemsetAsync(C.ca_count, 0, 2 * sizeof(unsigned), s) != hipSuccess)
+    if (!a->ws_persistent && hipMemsetAsync(C.ca_count, 0, kCaCounterBytes, s) != hipSuccess)
       return acl__set_error("hipMemsetAsync failed");
   }
   // The control phase runs inside the auction's workgroups (one launch, the
@@ -379,7 +379,7 @@ acl_status_t acl_amd::run_control(const acl_formations_t* F, const acl_control_a
   const acl_status_t st = ctl_params(F, a, C);
   if (st != ACL_OK || a->B == 0) return st;
   if (flags & CTL_MIXED) C.all_uniform = 0;
-  if ((flags & CTL_RESET) && hipMemsetAsync(C.ca_count, 0, 2 * sizeof(unsigned), s) != hipSuccess)
+  if ((flags & CTL_RESET) && hipMemsetAsync(C.ca_count, 0, kCaCounterBytes, s) != hipSuccess)
     return acl__set_error("hipMemsetAsync failed");
   hipError_t e = hipSuccess;
   if (flags & CTL_PREP) {

@@ -683,7 +683,7 @@ extern "C" acl_status_t acl_trial_init(const acl_trial_args_t* a, int32_t n, voi
   if (a->B == 0) return ACL_OK;
   const TrialDev D = trial_dev(a, n);
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(D.ca_count, 0, 2 * sizeof(unsigned), s) != hipSuccess)
+  if (hipMemsetAsync(D.ca_count, 0, kCaCounterBytes, s) != hipSuccess)
     return acl__set_error("hipMemsetAsync failed");
   hipLaunchKernelGGL(trial_init_kernel, dim3(a->B), dim3(kTrBlock), 0, s, D);
   if (hipGetLastError() != hipSuccess) return acl__set_error("trial_init_kernel launch failed");
@@ -732,7 +732,7 @@ extern "C" acl_status_t acl_trial_batch(const acl_formations_t* F, const acl_tri
   cs.ca_flag = const_cast<uint8_t*>(D.ca);
   cs.status = D.cst;
   cs.workspace = wc; cs.cntrl = a->cntrl; cs.safety = a->safety;
-  if (hipMemsetAsync(D.ca_count, 0, 2 * sizeof(unsigned), s) != hipSuccess)
+  if (hipMemsetAsync(D.ca_count, 0, kCaCounterBytes, s) != hipSuccess)
     return acl__set_error("hipMemsetAsync failed");
 
   const acl_episode_params_t& ep = a->tp.ep;
