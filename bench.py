@@ -106,6 +106,13 @@ def algorithmic_bytes(w, lo, hi):
     return auction, gain, 0, E / used.numel()
 
 
+def graph_group(requested, steps):
+    """Steps captured per HIP graph: the largest divisor of `steps` not above
+    `requested` (at least 1), so that exactly `steps` steps are timed."""
+    top = max(1, min(int(requested), int(steps)))
+    return max(g for g in range(1, top + 1) if steps % g == 0)
+
+
 def committed_profile(prefix, n, B, kernel):
     """The newest committed PMC summary profiles/r*_{prefix}.json measured on
     this same configuration that has `kernel`; (entry, path) or (None, None)."""
@@ -506,9 +513,7 @@ def main():
                              margin=margin, persistent=not args.no_persistent)
                 D.gather_results(out["P_out"], out["status"])
             torch.cuda.synchronize()
-            # G steps per graph (G divides K: exactly K steps are timed)
-            G = max(g for g in range(1, max(1, min(args.graph_steps, args.steps)) + 1)
-                    if args.steps % g == 0)
+            G = graph_group(args.graph_steps, args.steps)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=gs):
                 for _ in range(G):

@@ -48,3 +48,21 @@ def test_gpus4_c4_shard_sizes():
 def test_world_size_mismatch_is_an_error():
     r = _run(["--gpus", "1", "--dry-run", "--steps", "1"], env={"WORLD_SIZE": "2", "RANK": "0"})
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_graph_group_times_exactly_the_steps():
+    """--graph-steps G: the timed K steps are K / G' replays of a graph of G'
+    steps, G' the largest divisor of K not above G (so no step is dropped or
+    added)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.graph_group(10, 20) == 10
+    assert bench.graph_group(10, 25) == 5
+    assert bench.graph_group(10, 7) == 7
+    assert bench.graph_group(10, 13) == 1
+    assert bench.graph_group(1, 20) == 1
+    assert bench.graph_group(0, 20) == 1
+    for K in range(1, 60):
+        for G in range(0, 15):
+            g = bench.graph_group(G, K)
+            assert K % g == 0 and 1 <= g <= max(1, G)
