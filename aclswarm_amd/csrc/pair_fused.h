@@ -41,6 +41,18 @@
 
 #include "control_dev.h"
 
+// diagnostic bounds (wrong results, A/B builds only): the pair loop without
+// its scale terms / without its record reads / without its tiles
+#ifndef ACL_DIAG_NOPAIR
+#define ACL_DIAG_NOPAIR 0
+#endif
+#ifndef ACL_DIAG_NOLOADS
+#define ACL_DIAG_NOLOADS 0
+#endif
+#ifndef ACL_DIAG_NOLOOP
+#define ACL_DIAG_NOLOOP 0
+#endif
+
 namespace acl_amd {
 
 struct FusedLayout {
@@ -320,7 +332,7 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
     // the lane's (column, component) slot of the packed column sums
     const int colk = 3 * c + ((lane >> 4) == 0 ? 0 : ((lane >> 4) == 1 ? 2 : 1));
     const int NT = nb * (nb + 1) / 2;
-    const int t0 = (wave * NT) / kW, t1 = ((wave + 1) * NT) / kW;
+    const int t0 = (wave * NT) / kW, t1 = ACL_DIAG_NOLOOP ? t0 : ((wave + 1) * NT) / kW;
     double* myacc = acc + wave * R * 3;
 
     // tile t -> (I, J), J >= I, row block by row block
@@ -343,7 +355,12 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
     };
     auto rec_load = [&](unsigned x, int s, unsigned long long m, Rec5& R) {
       const unsigned e = (x >> 8) + (unsigned)__popc(x & ((1u << s) - 1u));
+#if ACL_DIAG_NOLOADS  // diagnostic bound (wrong results): records without HBM reads
+      const double d = (double)(lanebit_u64(m) ? (e & 7u) : 0u) * 0.125;
+      R.a[0] = d; R.a[1] = -d; R.a[2] = d; R.a[3] = d; R.a[4] = -d;
+#else
       load_rec5(grs, lanebit_u64(m) ? (int)__umul24(e, 40u) : 0x40000000, R);
+#endif
     };
     Rec5 X, Y;
     unsigned long long mx = 0ull, my = 0ull;
@@ -393,7 +410,7 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
       }
       const unsigned long long many = mx | my;
       double Fxy = 0.0, Fz = 0.0;
-      if (lanebit_u64(many)) {
+      if (!ACL_DIAG_NOPAIR && lanebit_u64(many)) {
         const double4 bi = pi[1], bj = pj[1];  // {p.y, p.z, pn_xy, pn_z}
         const double pix = ai.w, piy = bi.x, piz = bi.y, pjx = aj.w, pjy = bj.x, pjz = bj.y;
         double e_xy, e_z;
