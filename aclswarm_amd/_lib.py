@@ -22,7 +22,7 @@ FLAG_CHANGED = 0x04
 FLAG_NONFINITE = 0x08
 FLAG_BAD_INPUT = 0x10
 FLAG_CA_ACTIVE = 0x20
-ABI_VERSION = 10  # include/aclswarm_amd.h ACL_ABI_VERSION
+ABI_VERSION = 11  # include/aclswarm_amd.h ACL_ABI_VERSION
 FLAG_FRAGILE = 0x40
 FRAGILE_MARGIN = 1e-6
 
@@ -36,7 +36,7 @@ EXPORTS = (
     "acl_formations_init", "acl_max_vehicles", "acl_abi_version", "acl_solve_workspace_bytes", "acl_solve_batch", "acl_swarm_stats", "acl_count_edges", "acl_pack_adjacency",
     "acl_pack_gains", "acl_gain_planes", "acl_pack_gains_planes", "acl_tile_gains", "acl_admm_solve_batch", "acl_device_count", "acl_set_device",
     "acl_control_batch", "acl_write_assignment_log", "acl_read_assignment_log",
-    "acl_hungarian_batch",
+    "acl_hungarian_batch", "acl_cbaa_step_batch",
     "acl_default_episode_params", "acl_episode_workspace_bytes", "acl_episode_batch",
     "acl_default_trial_params", "acl_trial_workspace_bytes", "acl_trial_init", "acl_trial_batch",
     "acl_generate_formation_groups",
@@ -100,6 +100,14 @@ class HungarianArgs(ct.Structure):
     _fields_ = [("B", ct.c_int32), ("fidx", ct.c_void_p), ("q", ct.c_void_p),
                 ("P_last", ct.c_void_p), ("P_cmp", ct.c_void_p), ("P_opt", ct.c_void_p),
                 ("cost", ct.c_void_p), ("align_Rt", ct.c_void_p), ("status", ct.c_void_p)]
+
+
+class CbaaStepArgs(ct.Structure):
+    """acl_cbaa_step_args_t (ABI 11): one CBAA bid iteration per vehicle
+    (auctioneer.cpp:182-306,469-542)."""
+    _fields_ = [("V", ct.c_int32)] + [(n, ct.c_void_p) for n in (
+        "fidx", "vehid", "q", "Rt", "start", "price", "who", "cand_off", "cand_vehid",
+        "cand_price", "cand_who", "task", "flags")]
 
 
 class EpisodeParams(ct.Structure):
@@ -240,6 +248,8 @@ def lib():
     L.acl_generate_formation_groups.restype = ct.c_int
     L.acl_hungarian_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(HungarianArgs), VP]
     L.acl_hungarian_batch.restype = ct.c_int
+    L.acl_cbaa_step_batch.argtypes = [ct.POINTER(Formations), ct.POINTER(CbaaStepArgs), VP]
+    L.acl_cbaa_step_batch.restype = ct.c_int
     L.acl_write_assignment_log.argtypes = [ct.c_char_p, I32, VP, VP, VP, VP, VP, VP]
     L.acl_write_assignment_log.restype = ct.c_int
     L.acl_read_assignment_log.argtypes = [ct.c_char_p, ct.POINTER(I32), VP, VP, VP, VP, VP, VP]

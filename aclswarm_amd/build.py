@@ -18,7 +18,7 @@ DRIVER = os.path.join(HERE, "lib", "libfacade_driver.so")
 # the codegen-compatible ADMM entry points driven as aclswarm/src/admm.cpp does
 CG_DRIVER_SRC = os.path.join(ROOT, "tests", "codegen_driver.cpp")
 CG_DRIVER = os.path.join(HERE, "lib", "libcodegen_driver.so")
-SOURCES = ["solve.hip", "auction.hip", "solve_wide.hip", "control.hip", "admm.hip", "hungarian.hip", "episode.hip",
+SOURCES = ["solve.hip", "auction.hip", "solve_wide.hip", "control.hip", "admm.hip", "hungarian.hip", "cbaa_step.hip", "episode.hip",
            "trial.hip", "formation_gen.hip", "api.cpp"]
 # The generated ADMM library's C++ entry points (ADMMGainDesign3D and the
 # generic MATLAB-Coder emx utilities) live in their own shim library linked to

@@ -332,6 +332,37 @@ def hungarian(table, fidx, q, P_last=None, P_cmp=None, want_Rt=False, stream=Non
     return out
 
 
+def cbaa_step(table, fidx, vehid, q, Rt, start, price, who, cand_off, cand_vehid=None,
+              cand_price=None, cand_who=None, stream=None):
+    """acl_cbaa_step_batch (ABI 11): one CBAA bid iteration for each of V
+    vehicles -- the START bid (start[k] = 1) or updateTaskAssignment over its
+    candidates then selectTaskAssignment when outbid (auctioneer.cpp:182-306,
+    469-542). Device tensors: fidx / vehid [V] i32, q [V][3] f64, Rt [V][6]
+    f64, start [V] u8, price [V][n] f32 and who [V][n] i32 (updated in
+    place), cand_off [V + 1] i32, cand_vehid [K] i32, cand_price [K][n] f32,
+    cand_who [K][n] i32. Returns (task [V] i32, flags [V] i32)."""
+    lib = L.lib()
+    V = int(vehid.shape[0])
+    dev = vehid.device
+    task = torch.empty((V,), dtype=torch.int32, device=dev)
+    flags = torch.empty((V,), dtype=torch.int32, device=dev)
+    a = L.CbaaStepArgs()
+    a.V = V
+    a.fidx = fidx.data_ptr(); a.vehid = vehid.data_ptr(); a.q = q.data_ptr()
+    a.Rt = Rt.data_ptr(); a.start = start.data_ptr(); a.price = price.data_ptr()
+    a.who = who.data_ptr(); a.cand_off = cand_off.data_ptr()
+    a.cand_vehid = cand_vehid.data_ptr() if cand_vehid is not None else None
+    a.cand_price = cand_price.data_ptr() if cand_price is not None else None
+    a.cand_who = cand_who.data_ptr() if cand_who is not None else None
+    a.task = task.data_ptr(); a.flags = flags.data_ptr()
+    F = table.struct()
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    L.check(lib.acl_cbaa_step_batch(ct.byref(F), ct.byref(a), ct.c_void_p(stream)),
+            "acl_cbaa_step_batch")
+    return task, flags
+
+
 def write_assignment_log(path, q, adj, lastP, p, align_Rt, P):
     """Auctioneer::logAssignment's binary record (auctioneer.cpp:577-597),
     host arrays: q, p [n][3]; adj [n][n] (adj[i][j] = adjmat(i,j)); lastP, P

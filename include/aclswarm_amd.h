@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define ACL_ABI_VERSION 10
+#define ACL_ABI_VERSION 11
 
 typedef enum {
   ACL_OK = 0,
@@ -446,6 +446,67 @@ typedef struct {
 
 acl_status_t acl_hungarian_batch(const acl_formations_t* formations,
                                  const acl_hungarian_args_t* args, void* stream);
+
+/* ---- one vehicle's CBAA bid iteration, batched (ABI 11) -------------------
+ * The message-level protocol of the per-vehicle Auctioneer, for vehicles
+ * that exchange bids with their neighbours iteration by iteration
+ * (Auctioneer::enqueueBid / tick / processBid, auctioneer.cpp:124-160,
+ * 182-306) instead of running the whole consensus in acl_solve_batch: the
+ * tally a vehicle runs once it holds all its neighbours' bids of an
+ * iteration. For vehicle k of V (any swarms, one formation table):
+ *   start[k] = 1  reset its table (price 0, who -1; auctioneer.cpp:448-465)
+ *                 and make the START bid (selectTaskAssignment, :517-542);
+ *   start[k] = 0  updateTaskAssignment (:469-513) over the candidates --
+ *                 its own table and the neighbours' bids of the iteration,
+ *                 the caller's std::map bids_curr_ after :475's insert of its
+ *                 own bid, ascending vehid -- then selectTaskAssignment when
+ *                 it was outbid.
+ * Prices: getPrice(q_k, aligned_j) (:546-549) with aligned = (R p_j + t,
+ * p_j.z) from the vehicle's alignment (acl_solve_batch's align_Rt row of
+ * that vehicle, :400-414), evaluated on the device in the reference's f64
+ * order: the same floats as acl_solve_batch's prices.
+ * Device pointers:
+ *   fidx       [V]        formation of vehicle k's swarm
+ *   vehid      [V]        the vehicle's id in its swarm, < n
+ *   q          [V][3]     its position (the auction's snapshot)
+ *   Rt         [V][6]     its alignment {R00, R01, R10, R11, tx, ty}
+ *   start      [V]        1: START bid, 0: a bid iteration
+ *   price      [V][n]     in/out f32: its table's prices (Bid::price)
+ *   who        [V][n]     in/out i32: its table's holders (Bid::who, -1 none)
+ *   cand_off   [V + 1]    vehicle k's candidates are rows cand_off[k] ..
+ *                         cand_off[k + 1] - 1 (>= 1 row unless start[k])
+ *   cand_vehid [K]        each candidate's vehid, strictly ascending per vehicle
+ *   cand_price [K][n] f32, cand_who [K][n] i32: the candidates' tables
+ *                         (may be NULL when every start[k] is 1)
+ *   task       [V]        out: the task the select took, -1 if none ran or
+ *                         none was eligible
+ *   flags      [V]        out: ACL_CBAA_* bits (BAD_INPUT: a vehid, fidx or
+ *                         the candidate order is invalid; the table is left
+ *                         as it was)
+ * Stream-ordered, no workspace. */
+#define ACL_CBAA_OUTBID    0x01 /* a task it held went to another vehicle */
+#define ACL_CBAA_SELECTED  0x02 /* selectTaskAssignment took a task */
+#define ACL_CBAA_BAD_INPUT 0x10
+
+typedef struct {
+  int32_t V;
+  const int32_t* fidx;
+  const int32_t* vehid;
+  const double* q;
+  const double* Rt;
+  const uint8_t* start;
+  float* price;
+  int32_t* who;
+  const int32_t* cand_off;
+  const int32_t* cand_vehid;
+  const float* cand_price;
+  const int32_t* cand_who;
+  int32_t* task;
+  int32_t* flags;
+} acl_cbaa_step_args_t;
+
+acl_status_t acl_cbaa_step_batch(const acl_formations_t* formations,
+                                 const acl_cbaa_step_args_t* args, void* stream);
 
 /* ---- closed-loop batched episodes ---------------------
  * B swarms flown for `steps` control periods in lockstep: the discrete-time

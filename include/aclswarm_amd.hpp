@@ -41,6 +41,18 @@
  *    CBAA.msg per auction (coordination_ros.cpp:308-318); the per-round bids
  *    never leave the GPU. enqueueBid/tick accept and drop bids, and isIdle()
  *    is true whenever start() is not running.
+ *    Exchange mode (setBidExchange(true), ABI 11) is the reference's message
+ *    protocol instead, for fleets that mix these objects with other
+ *    vehicles' Auctioneers: start() aligns on the GPU (acl_solve_batch, this
+ *    vehicle's align_Rt row), makes the START bid and sends it (iter 0);
+ *    enqueueBid queues neighbours' bids, tick() processes one as processBid
+ *    does (auctioneer.cpp:182-306: iteration buckets, the START-bid bucket,
+ *    bidIterComplete over the neighbours of this vehicle's own assignment),
+ *    and each completed iteration's tally -- updateTaskAssignment and, when
+ *    outbid, selectTaskAssignment -- runs on the GPU (acl_cbaa_step_batch,
+ *    V = 1); after 2n iterations the vehicle adopts its table as above. With
+ *    every vehicle starting from one snapshot the outcome equals the
+ *    one-call consensus bit for bit (tests/test_gpu_facade.py).
  *  - Errors. The reference has none (asserts only). Auctioneer::start keeps
  *    that shape: a call it cannot run (no formation, q not n x 3, a GPU-layer
  *    failure) runs no auction, calls no handler and leaves the assignment as
@@ -68,6 +80,7 @@
 #include <functional>
 #include <algorithm>
 #include <iostream>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -380,6 +393,9 @@ class Auctioneer {
   void setFormationColMajor(const double* p_colmajor, const uint8_t* adj_colmajor) {
     form_.upload(n_, p_colmajor, adj_colmajor, nullptr);
     form_p_ = detail::rows_xyz(n_, p_colmajor);
+    adj_.assign(adj_colmajor, adj_colmajor + (size_t)n_ * n_);
+    cbaa_max_iter_ = 2 * n_;  // n * diameter, diameter = 2 (auctioneer.cpp:50-51)
+    reset_x();
     auction_open_ = false;
     formation_just_received_ = true;
     for (int i = 0; i < n_; ++i) P_[i] = Pt_[i] = (vehidx_t)i;
@@ -401,6 +417,10 @@ class Auctioneer {
     if (form_.n != n_) {
       last_status_ = ACL_ERR_INVALID_ARG;
       last_error_ = "Auctioneer::start before setFormation";
+      return;
+    }
+    if (exchange_) {
+      start_exchange(q_colmajor);
       return;
     }
     AuctionOut r;
@@ -510,14 +530,48 @@ class Auctioneer {
 
  public:
 
-  /* Accepted and dropped: the consensus ran inside start(). */
-  void enqueueBid(vehidx_t, uint32_t, uint32_t, const Bid&) {
-    std::lock_guard<std::mutex> lock(queue_mtx_);
+  /* Exchange mode (see the file header): off by default, where the whole
+   * consensus runs inside start(). Set it before the first start(). */
+  void setBidExchange(bool on) {
+    std::lock_guard<std::mutex> lock(auction_mtx_);
+    exchange_ = on;
   }
-  void tick() { std::lock_guard<std::mutex> lock(auction_mtx_); }
+  bool bidExchange() const { return exchange_; }
+
+  /* auctioneer.cpp:124-135. Default mode: accepted and dropped (the
+   * consensus ran inside start()); exchange mode: queued for tick(). */
+  void enqueueBid(vehidx_t vehid, uint32_t auctionid, uint32_t iter, const Bid& bid) {
+    std::lock_guard<std::mutex> lock(queue_mtx_);
+    if (exchange_) rxbids_.push_back(BidPkt{vehid, auctionid, iter, bid});
+  }
+  /* auctioneer.cpp:139-160: exchange mode processes the oldest queued bid
+   * (processBid, :182-306) while an auction is open. */
+  void tick() {
+    std::lock_guard<std::mutex> lock(auction_mtx_);
+    if (!exchange_ || !auction_open_) return;
+    BidPkt pkt;
+    {
+      std::lock_guard<std::mutex> qlock(queue_mtx_);
+      if (rxbids_.empty()) return;
+      pkt = rxbids_.front();
+      rxbids_.erase(rxbids_.begin());
+    }
+    processBid(pkt);
+  }
+  /* bids waiting for tick() (exchange mode) */
+  size_t queuedBids() {
+    std::lock_guard<std::mutex> lock(queue_mtx_);
+    return rxbids_.size();
+  }
 
   /* auctioneer.cpp:65-74 */
   void flush() {
+    reset_x();
+    bids_zero_.clear();
+    {
+      std::lock_guard<std::mutex> lock(queue_mtx_);
+      rxbids_.clear();
+    }
     auction_open_ = false;
     invalid_assignment_ = false;
   }
@@ -578,9 +632,172 @@ class Auctioneer {
     if (handler_) handler_(toPerm(P_));
   }
 
+  // ---- exchange mode (auctioneer.cpp:78-125,182-306,419-465) ----
+  struct BidPkt {
+    vehidx_t vehid;
+    uint32_t auctionid, iter;
+    Bid bid;
+  };
+
+  /* reset (auctioneer.cpp:448-465) */
+  void reset_x() {
+    auction_open_ = false;
+    biditer_ = 0;
+    bid_.price.assign(n_, 0.0f);
+    bid_.who.assign(n_, -1);
+    bids_curr_.clear();
+    bids_next_.clear();
+  }
+
+  void notifySendBid() {
+    if (send_bid_) send_bid_((uint32_t)auctionid_, (uint32_t)biditer_, std::make_shared<const Bid>(bid_));
+  }
+
+  /* start (auctioneer.cpp:78-120): alignment on the GPU, the START bid */
+  void start_exchange(const double* q_colmajor) {
+    reset_x();
+    bids_curr_ = bids_zero_;
+    bids_zero_.clear();
+    try {
+      const AuctionOut r = run_auction(q_colmajor);  // this vehicle's align_Rt row
+      q_self_[0] = r.q[(size_t)3 * vehid_];
+      q_self_[1] = r.q[(size_t)3 * vehid_ + 1];
+      q_self_[2] = r.q[(size_t)3 * vehid_ + 2];
+      std::copy(r.Rt.begin() + (size_t)6 * vehid_, r.Rt.begin() + (size_t)6 * vehid_ + 6, rt_self_);
+      step(true);
+      last_status_ = ACL_OK;
+      last_error_.clear();
+    } catch (const std::exception& e) {
+      last_status_ = ACL_ERR_HIP;
+      last_error_ = e.what();
+      reset_x();
+      return;
+    }
+    auction_open_ = true;  // (run_auction counted the auction id)
+    notifySendBid();
+  }
+
+  /* bidIterComplete (auctioneer.cpp:419-437): a bid from every neighbour of
+   * this vehicle's formation point under its own assignment */
+  bool bidIterComplete() const {
+    const int i = P_[vehid_];
+    for (int j = 0; j < n_; ++j)
+      if (adj_[(size_t)j * n_ + i] && bids_curr_.find(Pt_[j]) == bids_curr_.end()) return false;
+    return true;
+  }
+
+  /* processBid (auctioneer.cpp:182-306) */
+  void processBid(const BidPkt& pkt) {
+    if (verbose_)
+      std::cout << "A" << auctionid_ << "B" << biditer_ << ": Processing a" << pkt.auctionid
+                << "b" << pkt.iter << " from " << static_cast<int>(pkt.vehid) << std::endl;
+    if (pkt.iter == 0) bids_zero_.insert({pkt.vehid, pkt.bid});
+    if (pkt.iter == (uint32_t)biditer_) bids_curr_.insert({pkt.vehid, pkt.bid});
+    else if (pkt.iter == (uint32_t)biditer_ + 1) bids_next_.insert({pkt.vehid, pkt.bid});
+    else if (verbose_)
+      std::cout << "!! Threw away a" << pkt.auctionid << "b" << pkt.iter << " from "
+                << static_cast<int>(pkt.vehid) << std::endl;
+    if (!bidIterComplete()) return;
+    try {
+      step(false);  // updateTaskAssignment, then selectTaskAssignment if outbid
+    } catch (const std::exception& e) {
+      last_status_ = ACL_ERR_HIP;
+      last_error_ = e.what();
+      reset_x();
+      return;
+    }
+    ++biditer_;
+    bids_curr_ = bids_next_;
+    bids_next_.clear();
+    if (biditer_ == 1) bids_zero_.clear();
+    if (biditer_ >= cbaa_max_iter_) {  // hasReachedConsensus (:442-444)
+      std::vector<uint16_t> who(n_);
+      for (int j = 0; j < n_; ++j)
+        who[j] = (bid_.who[j] >= 0 && bid_.who[j] < n_) ? (uint16_t)bid_.who[j] : (uint16_t)0xFFFF;
+      finish(who);  // (:256-292) adoption, the new-assignment handler
+      reset_x();    // (:295) idle for the next auction
+    } else {
+      notifySendBid();
+    }
+  }
+
+  /* One tally of this vehicle on the GPU (acl_cbaa_step_batch, V = 1): the
+   * START bid, or the candidates = bids_curr_ with its own bid inserted
+   * (:475, std::map order) */
+  void step(bool start) {
+    const int n = n_;
+    std::vector<int32_t> cv;
+    std::vector<float> cp;
+    std::vector<int32_t> cw;
+    if (!start) {
+      std::map<vehidx_t, Bid> cand = bids_curr_;
+      cand.insert({vehid_, bid_});
+      for (const auto& kv : cand) {
+        if ((int)kv.second.price.size() != n || (int)kv.second.who.size() != n)
+          throw std::runtime_error("Auctioneer: a bid's tables are not n long");
+        cv.push_back((int32_t)kv.first);
+        cp.insert(cp.end(), kv.second.price.begin(), kv.second.price.end());
+        cw.insert(cw.end(), kv.second.who.begin(), kv.second.who.end());
+      }
+    }
+    const int K = (int)cv.size();
+    const int32_t fidx = 0, vid = vehid_;
+    const int32_t off[2] = {0, K};
+    const uint8_t st = start ? 1 : 0;
+    std::vector<int32_t> who(bid_.who.begin(), bid_.who.end());
+    x_fidx_.upload(&fidx, 4);
+    x_vehid_.upload(&vid, 4);
+    x_q_.upload(q_self_, 24);
+    x_rt_.upload(rt_self_, 48);
+    x_start_.upload(&st, 1);
+    x_price_.upload(bid_.price.data(), (size_t)n * 4);
+    x_who_.upload(who.data(), (size_t)n * 4);
+    x_off_.upload(off, 8);
+    if (K) {
+      x_cv_.upload(cv.data(), (size_t)K * 4);
+      x_cp_.upload(cp.data(), cp.size() * 4);
+      x_cw_.upload(cw.data(), cw.size() * 4);
+    }
+    x_out_.reserve(8);
+    acl_cbaa_step_args_t a;
+    std::memset(&a, 0, sizeof(a));
+    a.V = 1;
+    a.fidx = x_fidx_.as<const int32_t>();
+    a.vehid = x_vehid_.as<const int32_t>();
+    a.q = x_q_.as<const double>();
+    a.Rt = x_rt_.as<const double>();
+    a.start = x_start_.as<const uint8_t>();
+    a.price = x_price_.as<float>();
+    a.who = x_who_.as<int32_t>();
+    a.cand_off = x_off_.as<const int32_t>();
+    a.cand_vehid = K ? x_cv_.as<const int32_t>() : nullptr;
+    a.cand_price = K ? x_cp_.as<const float>() : nullptr;
+    a.cand_who = K ? x_cw_.as<const int32_t>() : nullptr;
+    a.task = x_out_.as<int32_t>();
+    a.flags = x_out_.as<int32_t>() + 1;
+    const acl_formations_t F = form_.table();
+    detail::check(acl_cbaa_step_batch(&F, &a, nullptr));
+    int32_t out[2] = {0, 0};
+    detail::check(acl_memcpy_d2h(bid_.price.data(), x_price_.get(), (size_t)n * 4, nullptr));
+    detail::check(acl_memcpy_d2h(who.data(), x_who_.get(), (size_t)n * 4, nullptr));
+    detail::check(acl_memcpy_d2h(out, x_out_.get(), 8, nullptr));
+    detail::check(acl_stream_synchronize(nullptr));
+    if (out[1] & ACL_CBAA_BAD_INPUT) throw std::runtime_error("acl_cbaa_step_batch: bad input");
+    bid_.who.assign(who.begin(), who.end());
+  }
+
   int n_;
   vehidx_t vehid_;
   bool verbose_;
+  bool exchange_ = false;
+  int biditer_ = 0, cbaa_max_iter_ = 0;
+  Bid bid_;
+  std::map<vehidx_t, Bid> bids_zero_, bids_curr_, bids_next_;
+  std::vector<BidPkt> rxbids_;  // FIFO (std::queue in the reference)
+  std::vector<uint8_t> adj_;    // AdjMat, column-major
+  double q_self_[3] = {0.0, 0.0, 0.0}, rt_self_[6] = {1.0, 0.0, 0.0, 1.0, 0.0, 0.0};
+  detail::DeviceBuffer x_fidx_, x_vehid_, x_q_, x_rt_, x_start_, x_price_, x_who_, x_off_, x_cv_,
+      x_cp_, x_cw_, x_out_;
   std::vector<vehidx_t> P_, Pt_;
   int auctionid_ = 0;
   bool auction_open_ = false;

@@ -270,3 +270,112 @@ extern "C" int facade_admm_codegen(int n, const double* pts_nx3, const uint8_t* 
   }
   return 0;
 }
+
+// Exchange mode (Auctioneer::setBidExchange, the reference's message
+// protocol): n vehicles whose send-bid handlers publish to a message bus that
+// delivers each bid to the vehicles subscribed to its sender (the neighbours
+// of their own formation points, connectToNeighbors, coordination_ros.cpp:
+// 392-430), in an order drawn from `seed`; the first `late` vehicles of a
+// shuffled order start only after the others' bids have been flowing (their
+// START bids wait in the queues: tick() processes nothing before start, and
+// processBid keeps iteration-0 bids, auctioneer.cpp:139-160,195-206).
+// Inputs column-major as facade_run's; outputs per vehicle: P_out[n][n]
+// (adopted assignment), invalid[n], sends[n] (send-bid calls), handler[n],
+// last_iter[n] (iter of its last sent bid), who_out[n][n] (that bid's who).
+extern "C" int facade_exchange(int n, const double* p_cm, const uint8_t* adj_cm,
+                               const double* q_cm, const uint8_t* Pin, uint32_t seed, int late,
+                               uint8_t* P_out, uint8_t* invalid_out, int32_t* sends_out,
+                               int32_t* handler_out, int32_t* last_iter_out, int32_t* who_out) {
+  try {
+    amd::PtsMat p(n, 3), q(n, 3);
+    amd::AdjMat adj(n, n);
+    std::copy(p_cm, p_cm + (size_t)3 * n, p.data());
+    std::copy(q_cm, q_cm + (size_t)3 * n, q.data());
+    std::copy(adj_cm, adj_cm + (size_t)n * n, adj.data());
+    uint64_t rng = 0x9E3779B97F4A7C15ull ^ seed;
+    auto rnd = [&](uint32_t m) {  // splitmix64
+      rng += 0x9E3779B97F4A7C15ull;
+      uint64_t z = rng;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      return (uint32_t)((z ^ (z >> 31)) % m);
+    };
+    struct Msg {
+      int from;
+      uint32_t auction, iter;
+      amd::Auctioneer::Bid bid;
+    };
+    std::vector<Msg> bus;
+    struct Veh {
+      std::unique_ptr<amd::Auctioneer> a;
+      std::vector<int> subs;  // vehicles whose bids it receives
+      int sends = 0, handler = 0;
+      int32_t last_iter = -1;
+      std::vector<int32_t> last_who;
+    };
+    std::vector<Veh> veh(n);
+    amd::AssignmentPerm P0(amd::Map<const amd::AssignmentVec>(Pin, (size_t)n));
+    for (int v = 0; v < n; ++v) {
+      Veh& x = veh[v];
+      x.a.reset(new amd::Auctioneer((amd::vehidx_t)v, (uint8_t)n, false));
+      x.a->setBidExchange(true);
+      x.a->setFormation(p, adj);
+      x.a->setAssignment(P0);
+      x.a->setNewAssignmentHandler([&x](const amd::AssignmentPerm&) { ++x.handler; });
+      x.a->setSendBidHandler([&bus, &x, v](uint32_t aid, uint32_t iter,
+                                           const amd::Auctioneer::BidConstPtr& b) {
+        ++x.sends;
+        x.last_iter = (int32_t)iter;
+        x.last_who.assign(b->who.begin(), b->who.end());
+        bus.push_back(Msg{v, aid, iter, *b});
+      });
+      // connectToNeighbors (coordination_ros.cpp:392-410) under P0
+      const int i = P0.indices()(v);
+      for (int j = 0; j < n; ++j)
+        if (adj(i, j)) x.subs.push_back(P0.transpose().indices()(j));
+    }
+    std::vector<int> order(n);
+    for (int v = 0; v < n; ++v) order[v] = v;
+    for (int k = n - 1; k > 0; --k) std::swap(order[k], order[rnd((uint32_t)k + 1)]);
+    for (int k = late; k < n; ++k) veh[order[k]].a->start(q);
+    auto pump = [&](size_t steps) {
+      for (size_t s = 0; s < steps && !bus.empty(); ++s) {
+        const size_t m = rnd((uint32_t)bus.size());
+        const Msg msg = bus[m];
+        bus.erase(bus.begin() + (long)m);
+        for (int u = 0; u < n; ++u) {
+          const auto& sb = veh[u].subs;
+          if (u != msg.from && std::find(sb.begin(), sb.end(), msg.from) != sb.end())
+            veh[u].a->enqueueBid((amd::vehidx_t)msg.from, msg.auction, msg.iter, msg.bid);
+        }
+        const int t = (int)rnd((uint32_t)n);
+        for (int r = 0, c = 1 + (int)rnd(3); r < c; ++r) veh[(t + r) % n].a->tick();
+      }
+    };
+    pump((size_t)n * 4);
+    for (int k = 0; k < late; ++k) veh[order[k]].a->start(q);
+    for (size_t guard = 0; guard < 100000000; ++guard) {
+      pump(1);
+      bool busy = !bus.empty();
+      for (int v = 0; v < n && !busy; ++v) busy = veh[v].a->queuedBids() > 0;
+      if (!busy) break;
+      for (int v = 0; v < n; ++v) veh[v].a->tick();
+    }
+    for (int v = 0; v < n; ++v) {
+      Veh& x = veh[v];
+      if (!x.a->isIdle()) throw std::runtime_error("exchange: an auction is still open");
+      if (x.a->lastStatus() != ACL_OK) throw std::runtime_error("exchange: " + x.a->lastError());
+      const amd::AssignmentPerm P = x.a->getAssignment();
+      for (int k = 0; k < n; ++k) P_out[(size_t)v * n + k] = P.indices()(k);
+      invalid_out[v] = x.a->didConvergeOnInvalidAssignment() ? 1 : 0;
+      sends_out[v] = x.sends;
+      handler_out[v] = x.handler;
+      last_iter_out[v] = x.last_iter;
+      for (int k = 0; k < n; ++k) who_out[(size_t)v * n + k] = x.last_who.empty() ? -2 : x.last_who[k];
+    }
+  } catch (const std::exception& e) {
+    fprintf(stderr, "facade_exchange: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}

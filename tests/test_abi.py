@@ -122,19 +122,19 @@ def test_status_record_is_16_bytes():
 
 
 def test_abi_version_and_formations_init():
-    """ABI 10 (ABI 5: gains_tiled in acl_formations_t, margin in the status,
+    """ABI 11 (ABI 5: gains_tiled in acl_formations_t, margin in the status,
     gate margins, the episode's auction latency and pending state; ABI 6:
     acl_admm_params_t.basis; ABI 7: acl_solve_args_t.skip_margin, appended;
     ABI 8: acl_solve_args_t.P_rows / P_rows_on, appended; ABI 9:
     acl_episode_params_t.assignment appended, the trial entry points; ABI 10:
-    acl_solve_args_t.ws_persistent, appended):
+    acl_solve_args_t.ws_persistent, appended; ABI 11: acl_cbaa_step_batch):
     acl_formations_init zero-fills the struct so no optional pointer
     is left as garbage; the solve rejects an empty formation table."""
     from aclswarm_amd import _lib as L
     with open(os.path.join(ROOT, "include", "aclswarm_amd.h")) as f:
-        assert "#define ACL_ABI_VERSION 10" in f.read()
+        assert "#define ACL_ABI_VERSION 11" in f.read()
     lib = L.lib()
-    assert lib.acl_abi_version() == 10 == L.ABI_VERSION  # the load-time check's inputs
+    assert lib.acl_abi_version() == 11 == L.ABI_VERSION  # the load-time check's inputs
     assert L.EpisodeParams.assignment.offset == L.EpisodeParams.avg_active_ca_thr.offset + 8
     assert L.SolveArgs.skip_margin.offset == L.SolveArgs.gate_margin.offset + 8
     assert L.SolveArgs.P_rows.offset == L.SolveArgs.skip_margin.offset + 8  # (4 B padding)

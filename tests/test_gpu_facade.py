@@ -182,3 +182,63 @@ def test_facade_admm_wrapper_class_codegen():
     for c in [c for c in AC.load() if c["p"].shape[0] <= 20][:4]:
         A = run(c["p"], c["adj"])
         assert AC.rel_err(A, AC.assemble(c["Axy"], c["Az"])) < 1e-5, c["name"]
+
+
+def _exchange(p, adj, q, P_in, seed, late):
+    n = p.shape[0]
+    lib = ct.CDLL(LIB)
+    f = lib.facade_exchange
+    f.restype = ct.c_int
+    P = np.zeros((n, n), np.uint8)
+    inv = np.zeros(n, np.uint8)
+    sends, handler, last_iter = (np.zeros(n, np.int32) for _ in range(3))
+    who = np.zeros((n, n), np.int32)
+    pc = np.asfortranarray(p, np.float64)
+    qc = np.asfortranarray(q, np.float64)
+    ac = np.asfortranarray(np.asarray(adj, np.uint8))
+    Pi = np.ascontiguousarray(P_in, np.uint8)
+    ptr = lambda a: a.ctypes.data_as(ct.c_void_p)  # noqa: E731
+    f.argtypes = [ct.c_int] + [ct.c_void_p] * 4 + [ct.c_uint32, ct.c_int] + [ct.c_void_p] * 6
+    assert f(n, ptr(pc), ptr(ac), ptr(qc), ptr(Pi), seed, late, ptr(P), ptr(inv), ptr(sends),
+             ptr(handler), ptr(last_iter), ptr(who)) == 0
+    return dict(P=P, invalid=inv, sends=sends, handler=handler, last_iter=last_iter, who=who)
+
+
+@pytest.mark.parametrize("case,seed,late", [("swarm6", 1, 0), ("swarm6", 2, 3),
+                                            ("simform20_nc", 3, 0), ("simform20_nc", 4, 7),
+                                            ("simform20_fc", 5, 19)])
+def test_facade_bid_exchange(case, seed, late):
+    """Exchange mode (Auctioneer::setBidExchange, ABI 11): every vehicle runs
+    the reference's message protocol -- START bid, enqueueBid / tick /
+    processBid with iteration buckets, its tallies on the GPU
+    (acl_cbaa_step_batch) -- over a bus that delivers bids in a seeded random
+    order, some vehicles starting late (their neighbours' START bids wait in
+    their queues). Each vehicle adopts the same assignment as the one-call
+    consensus (the oracle's tables, adopted as auctioneer.cpp:250-295 does),
+    sends 2n bids (iterations 0 .. 2n - 1), and its last bid equals the
+    lockstep protocol's table after 2n - 1 iterations (the CPU restatement)."""
+    import cbaa_step_oracle as S
+    rng = np.random.RandomState(seed)
+    if case == "swarm6":
+        pts, adjs, gains, q0 = H.swarm6()
+        p, adj, g = pts[1], adjs[1], gains[1]
+        q = q0 + rng.normal(0, 0.3, q0.shape)
+    else:
+        Pf, Af = H.simform(case)
+        p, adj = Pf[seed % Pf.shape[0], 0], Af[seed % Af.shape[0]]
+        g = H.synth_gains(rng, adj)
+        q = H.random_positions(rng, p.shape[0], 20.0)
+    n = p.shape[0]
+    P_in = H.random_perm(rng, n)
+    got = _exchange(p, adj, q, P_in, seed, late)
+    P, inv, _ = _expect(p, adj, g, q, np.zeros_like(q), P_in)
+    np.testing.assert_array_equal(got["invalid"], inv)
+    np.testing.assert_array_equal(got["handler"], 1 - inv)
+    for v in range(n):
+        if not inv[v]:
+            np.testing.assert_array_equal(got["P"][v], P[v], err_msg=f"vehicle {v}")
+    np.testing.assert_array_equal(got["sends"], np.full(n, 2 * n))
+    np.testing.assert_array_equal(got["last_iter"], np.full(n, 2 * n - 1))
+    C, _ = O.prices(q, p, adj, np.asarray(P_in, np.uint16))
+    who, _ = S.lockstep(C, adj, P_in, rounds=2 * n - 1)
+    np.testing.assert_array_equal(got["who"], who)
