@@ -275,7 +275,8 @@ extern "C" int facade_admm_codegen(int n, const double* pts_nx3, const uint8_t* 
 // protocol): n vehicles whose send-bid handlers publish to a message bus that
 // delivers each bid to the vehicles subscribed to its sender (the neighbours
 // of their own formation points, connectToNeighbors, coordination_ros.cpp:
-// 392-430), in an order drawn from `seed`; the first `late` vehicles of a
+// 392-430), senders interleaved in an order drawn from `seed` (each sender's
+// bids in order); the first `late` vehicles of a
 // shuffled order start only after the others' bids have been flowing (their
 // START bids wait in the queues: tick() processes nothing before start, and
 // processBid keeps iteration-0 bids, auctioneer.cpp:139-160,195-206).
@@ -340,7 +341,16 @@ extern "C" int facade_exchange(int n, const double* p_cm, const uint8_t* adj_cm,
     for (int k = late; k < n; ++k) veh[order[k]].a->start(q);
     auto pump = [&](size_t steps) {
       for (size_t s = 0; s < steps && !bus.empty(); ++s) {
-        const size_t m = rnd((uint32_t)bus.size());
+        // a random sender's oldest bid: per-link FIFO, as ROS topics deliver
+        // (the protocol relies on it: a vehicle that held every neighbour's
+        // last-iteration bid before finishing the one before would wait for
+        // a trigger that never comes)
+        size_t m = rnd((uint32_t)bus.size());
+        for (size_t k = 0; k < m; ++k)
+          if (bus[k].from == bus[m].from) {
+            m = k;
+            break;
+          }
         const Msg msg = bus[m];
         bus.erase(bus.begin() + (long)m);
         for (int u = 0; u < n; ++u) {
