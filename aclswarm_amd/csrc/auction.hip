@@ -578,7 +578,10 @@ __device__ __forceinline__ void align_chunk(int n, const double* pq, const unsig
 }
 
 template <int NC>
-__global__ void __launch_bounds__(64) align_kernel(const SolveParams P) {
+#ifndef ACL_ALIGN_OCC
+#define ACL_ALIGN_OCC 1  // min waves per SIMD align_kernel is built for (1: the compiler's choice)
+#endif
+__global__ void __launch_bounds__(64, ACL_ALIGN_OCC) align_kernel(const SolveParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = P.n;
   const AlignLayout L = make_align_layout(n);
@@ -651,6 +654,14 @@ __global__ void __launch_bounds__(64) align_kernel(const SolveParams P) {
 // FUSE: phase 5, the control law of a swarm whose vehicles all adopted one
 // assignment, runs in this workgroup right after its auction (see below);
 // GM: the fused phase also reports the gate margin.
+// A/B knobs: the control phase's wave issue priority (s_setprio 0-3), and
+// the CBAA phase's (set at the kernel's start, lowered again for control)
+#ifndef ACL_CTL_PRIO
+#define ACL_CTL_PRIO 0
+#endif
+#ifndef ACL_CBAA_PRIO
+#define ACL_CBAA_PRIO 0
+#endif
 #ifndef ACL_AUCTION_OCC_SMALL
 #define ACL_AUCTION_OCC_SMALL 6  // waves per SIMD the 128-thread (n <= 32) instantiation is built for
 #endif
@@ -1011,6 +1022,7 @@ __global__ void __launch_bounds__(kAB, kAB == 128 ? ACL_AUCTION_OCC_SMALL : 6)
   ACL_AUCTION_STOP_AT(4);
 
   // ---------------- phase 3: CBAA -------------------------------------------
+  if (ACL_CBAA_PRIO) __builtin_amdgcn_s_setprio(ACL_CBAA_PRIO);
   bool okv[NC];
   unsigned long long okm[NC];
   unsigned okk[NC];  // key mask: all ones for real vehicles, 0 past n
@@ -1534,6 +1546,7 @@ __global__ void __launch_bounds__(kAB, kAB == 128 ? ACL_AUCTION_OCC_SMALL : 6)
                                    offsetof(SolveParams, ctl));
     asm volatile("" : "+s"(pc));
     if (!ACL_FUSED_PREFETCH) fused_prefetch(*pc, b, f, tid, fpre);
+    if (ACL_CTL_PRIO || ACL_CBAA_PRIO) __builtin_amdgcn_s_setprio(ACL_CTL_PRIO);
     pair_gain_fused<kAW, GM>(pc, b, f, smem, tid, kAB, fpre);
     stamp_phase(P, b, tid, 7);  // diagnostic: end of the control phase
   }

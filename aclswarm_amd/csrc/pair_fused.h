@@ -309,8 +309,12 @@ __device__ __forceinline__ void pair_gain_fused(KCtlParams* Pp, int b, int f,
     if (lane == 0) rowb[R] = base;
   }
   __syncthreads();
+  // k / nb as a multiply-shift: exact for k < R nb <= 2048 and nb <= 16 (the
+  // error k (m - 2^16 / nb) / 2^16 < 1/32 stays below the 1/nb gap to the
+  // next integer); a 32-bit division is ~30 vector instructions per entry
+  const unsigned nbm = (65536u + (unsigned)nb - 1u) / (unsigned)nb;
   for (int k = tid; k < R * nb; k += nthreads) {
-    const int i = k / nb, J = k - i * nb;
+    const int i = (int)(((unsigned)k * nbm) >> 16), J = k - i * nb;
     const int w = J >> 3, sh = (8 * J) & 63;
     const unsigned long long word = adjF[2 * i + w];
     const unsigned below = (unsigned)__popcll(sh ? (word & ((1ull << sh) - 1ull)) : 0ull) +
