@@ -344,6 +344,24 @@ def cbaa_step(table, fidx, vehid, q, Rt, start, price, who, cand_off, cand_vehid
     lib = L.lib()
     V = int(vehid.shape[0])
     dev = vehid.device
+    n = table.n
+    want = {"fidx": (fidx, torch.int32, (V,)), "vehid": (vehid, torch.int32, (V,)),
+            "q": (q, torch.float64, (V, 3)), "Rt": (Rt, torch.float64, (V, 6)),
+            "start": (start, torch.uint8, (V,)), "price": (price, torch.float32, (V, n)),
+            "who": (who, torch.int32, (V, n)), "cand_off": (cand_off, torch.int32, (V + 1,))}
+    K = None
+    for name, t in (("cand_vehid", cand_vehid), ("cand_price", cand_price), ("cand_who", cand_who)):
+        if t is not None:
+            K = int(t.shape[0])
+    if K is not None:
+        want["cand_vehid"] = (cand_vehid, torch.int32, (K,))
+        want["cand_price"] = (cand_price, torch.float32, (K, n))
+        want["cand_who"] = (cand_who, torch.int32, (K, n))
+    for name, (t, dt, shape) in want.items():
+        if t is None or t.dtype != dt or tuple(t.shape) != shape or not t.is_contiguous() \
+                or t.device != dev:
+            raise ValueError(f"cbaa_step: {name} must be a contiguous {dt} tensor of shape "
+                             f"{shape} on {dev}")
     task = torch.empty((V,), dtype=torch.int32, device=dev)
     flags = torch.empty((V,), dtype=torch.int32, device=dev)
     a = L.CbaaStepArgs()

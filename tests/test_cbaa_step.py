@@ -60,3 +60,26 @@ def test_step_rules():
     cn = (0, np.array([np.nan, 0, 0, 0], np.float32), np.array([1, -1, -1, -1], np.int32))
     pr, wh, task, ob = S.step(2, False, own[0], own[1], [cn, c2], row)
     assert np.isnan(pr[0]) and wh[0] == 1 and not ob and task == -1
+
+
+def test_engine_step_rejects_bad_tensors():
+    """engine.cbaa_step checks dtype, shape, contiguity and device before any
+    pointer reaches the library (no GPU needed: it raises first)."""
+    import types
+
+    import torch
+    from aclswarm_amd import engine
+    V, n = 3, 5
+    T = types.SimpleNamespace(n=n)
+    good = dict(fidx=torch.zeros(V, dtype=torch.int32), vehid=torch.zeros(V, dtype=torch.int32),
+                q=torch.zeros(V, 3, dtype=torch.float64), Rt=torch.zeros(V, 6, dtype=torch.float64),
+                start=torch.ones(V, dtype=torch.uint8), price=torch.zeros(V, n),
+                who=torch.zeros(V, n, dtype=torch.int32), cand_off=torch.zeros(V + 1, dtype=torch.int32))
+    bad = [("price", torch.zeros(V, n, dtype=torch.float64)),        # dtype
+           ("who", torch.zeros(n, V, dtype=torch.int32).t()),        # not contiguous
+           ("q", torch.zeros(V, 2, dtype=torch.float64)),            # shape
+           ("cand_off", torch.zeros(V, dtype=torch.int32))]          # V + 1 entries
+    for name, t in bad:
+        kw = dict(good, **{name: t})
+        with pytest.raises(ValueError, match=name):
+            engine.cbaa_step(T, **kw)
