@@ -147,25 +147,6 @@ __device__ __forceinline__ void for_members(int n, const double* pq,
   }
 }
 
-// a_k += v_k in the lanes of `mask` only (the others keep a_k): exec is
-// narrowed around the four adds, so non-members cost no selects and leave no
-// trace in the sums (Eigen's sums run over the members only)
-__device__ __forceinline__ void masked_add4(unsigned long long mask, double& a0, double& a1,
-                                            double& a2, double& a3, double v0, double v1,
-                                            double v2, double v3) {
-  unsigned long long sv;
-  asm volatile(
-      "s_and_saveexec_b64 %[sv], %[m]\n\t"
-      "v_add_f64 %[a0], %[a0], %[v0]\n\t"
-      "v_add_f64 %[a1], %[a1], %[v1]\n\t"
-      "v_add_f64 %[a2], %[a2], %[v2]\n\t"
-      "v_add_f64 %[a3], %[a3], %[v3]\n\t"
-      "s_mov_b64 exec, %[sv]"
-      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3), [sv] "=&s"(sv)
-      : [m] "s"(mask), [v0] "v"(v0), [v1] "v"(v1), [v2] "v"(v2), [v3] "v"(v3)
-      : "scc");  // s_and_saveexec writes SCC
-}
-
 // diagnostic: s_memtime at phase ends (scripts/phase_profile.py)
 __device__ __forceinline__ void stamp_phase(const SolveParams& P, int b, int tid, int k) {
   if (P.stamps && tid == 0) P.stamps[(size_t)b * kStampStride + k] = __builtin_amdgcn_s_memtime();

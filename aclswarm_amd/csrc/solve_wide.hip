@@ -45,6 +45,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/aclswarm_amd.h"
 #include "common.h"
 #include "control_params.h"
@@ -668,11 +670,12 @@ __global__ void __launch_bounds__(kWABlock, 2) align_wide_kernel(const SolvePara
       if (lane == 0) vadj[c * n + v] = m;  // word-major: lanes over vehicles read consecutive words
     }
   }
-  // alignment sums, ascending members, branch-free: -0.0 is the exact
+  // alignment sums, ascending members: a lane adds a member's terms only if
+  // the member is in its neighbourhood (exec narrowed to those lanes around
+  // the four adds, masked_add4: no selects), starting from -0.0, the exact
   // identity of IEEE addition (-0 + x == x for every x, signed zeros
-  // included), so starting from it and adding -0.0 for a non-neighbour gives
-  // the bits of "first term, then acc + term". Lane = vehicle v; the four
-  // chains of a pass (x and y of p, of q) are independent.
+  // included), which gives the bits of "first term, then acc + term". Lane =
+  // vehicle v; the four chains of a pass (x and y of p, of q) are independent.
   double galign = 1.0;
   for (int v = tid; v < n; v += kWABlock) {
     const int i = Pin[v];
@@ -697,11 +700,7 @@ __global__ void __launch_bounds__(kWABlock, 2) align_wide_kernel(const SolvePara
           int j = 64 * w + 32 * hf + jb;
           j = j < n ? j : 0;
           const double px = p[3 * j], py = p[3 * j + 1], qx = qf[3 * j], qy = qf[3 * j + 1];
-          const bool m = (h >> jb) & 1u;
-          s0 = s0 + (m ? px : -0.0);
-          s1 = s1 + (m ? py : -0.0);
-          s2 = s2 + (m ? qx : -0.0);
-          s3 = s3 + (m ? qy : -0.0);
+          masked_add4(__ballot((h >> jb) & 1u), s0, s1, s2, s3, px, py, qx, qy);
         }
       }
     }
@@ -715,29 +714,34 @@ __global__ void __launch_bounds__(kWABlock, 2) align_wide_kernel(const SolvePara
     // c = 2 di + sj: (q_di - dm_di) (p_sj - sm_sj)
     const double z0 = lazy ? -0.0 : 0.0;
     double c0 = z0, c1 = z0, c2 = z0, c3 = z0;
+    // lazy lanes scale the q deviations by 1/k; 1.0 * x == x bit for bit, so
+    // the others multiply by 1.0, and a wave without a lazy lane (every one
+    // at C4's k ~ 500) skips the products (no per-lane selects either way)
+    const double scale = lazy ? oon : 1.0;
+    auto pass2 = [&](auto scaled) {
 #pragma unroll
-    for (int w = 0; w < kWMaxW; ++w) {
-      if (w >= NW) break;
-      for (int hf = 0; hf < 2; ++hf) {
-        const unsigned h = (unsigned)(rowb[w] >> (32 * hf));
+      for (int w = 0; w < kWMaxW; ++w) {
+        if (w >= NW) break;
+        for (int hf = 0; hf < 2; ++hf) {
+          const unsigned h = (unsigned)(rowb[w] >> (32 * hf));
 #pragma unroll 4
-        for (int jb = 0; jb < 32; ++jb) {
-          int j = 64 * w + 32 * hf + jb;
-          j = j < n ? j : 0;
-          const double e0 = p[3 * j] - sm[0], e1 = p[3 * j + 1] - sm[1];
-          double d0 = qf[3 * j] - dm[0], d1 = qf[3 * j + 1] - dm[1];
-          if (lazy) {
-            d0 = oon * d0;
-            d1 = oon * d1;
+          for (int jb = 0; jb < 32; ++jb) {
+            int j = 64 * w + 32 * hf + jb;
+            j = j < n ? j : 0;
+            const double e0 = p[3 * j] - sm[0], e1 = p[3 * j + 1] - sm[1];
+            double d0 = qf[3 * j] - dm[0], d1 = qf[3 * j + 1] - dm[1];
+            if (decltype(scaled)::value) {
+              d0 = scale * d0;
+              d1 = scale * d1;
+            }
+            masked_add4(__ballot((h >> jb) & 1u), c0, c1, c2, c3, d0 * e0, d0 * e1, d1 * e0,
+                        d1 * e1);
           }
-          const bool m = (h >> jb) & 1u;
-          c0 = c0 + (m ? d0 * e0 : -0.0);
-          c1 = c1 + (m ? d0 * e1 : -0.0);
-          c2 = c2 + (m ? d1 * e0 : -0.0);
-          c3 = c3 + (m ? d1 * e1 : -0.0);
         }
       }
-    }
+    };
+    if (__any(lazy)) pass2(std::true_type{});
+    else pass2(std::false_type{});
     if (!lazy) {
       c0 = c0 * oon; c1 = c1 * oon; c2 = c2 * oon; c3 = c3 * oon;
     }
