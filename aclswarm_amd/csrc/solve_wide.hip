@@ -446,15 +446,18 @@ __device__ __forceinline__ void wide_control(KCtlParams* Pp, int b, int f, unsig
           Nj = pjx * pjx + pjy * pjy;
           Nzj = pjz * pjz;
         }
-        double e_xy, e_z;
-        pair_e(q0, q1, q2, Ni, Nj, Nzi, Nzj, pix, piy, piz, pjx, pjy, pjz, pair_s2(q0, q1), e_xy,
-               e_z);
-        bool gxy, gz;
-        gate_decide_t<GM>(fcst(cst, FC_TXY), fcst(cst, FC_TZ), fcst(cst, FC_WIN), e_xy, e_z, q0, q1,
-                          q2, Ni, Nj, Nzi, Nzj, pix, piy, piz, pjx, pjy, pjz, gxy, gz, gmxy, gmz);
         double Fxy = 0.0, Fz = 0.0;
-        if (gxy) Fxy = fcst(cst, FC_K1XY) * ACL_GAIN_ATAN(fcst(cst, FC_K2XY) * e_xy, atab);
-        if (gz) Fz = fcst(cst, FC_K1Z) * ACL_GAIN_ATAN(fcst(cst, FC_K2Z) * e_z, atab);
+        if (!ACL_DIAG_NOPAIR) {
+          double e_xy, e_z;
+          pair_e(q0, q1, q2, Ni, Nj, Nzi, Nzj, pix, piy, piz, pjx, pjy, pjz, pair_s2(q0, q1), e_xy,
+                 e_z);
+          bool gxy, gz;
+          gate_decide_t<GM>(fcst(cst, FC_TXY), fcst(cst, FC_TZ), fcst(cst, FC_WIN), e_xy, e_z, q0,
+                            q1, q2, Ni, Nj, Nzi, Nzj, pix, piy, piz, pjx, pjy, pjz, gxy, gz, gmxy,
+                            gmz);
+          if (gxy) Fxy = fcst(cst, FC_K1XY) * ACL_GAIN_ATAN(fcst(cst, FC_K2XY) * e_xy, atab);
+          if (gz) Fz = fcst(cst, FC_K1Z) * ACL_GAIN_ATAN(fcst(cst, FC_K2Z) * e_z, atab);
+        }
         if (qfin) {  // A q + F q (kp per vehicle); the structural zeros drop (pair_fused.h)
           a0 += X.a[1] * q1 + (X.a[0] * q0 + Fxy * q0);
           a1 += X.a[3] * q1 + (X.a[2] * q0 + Fxy * q1);
@@ -1507,6 +1510,9 @@ __global__ void __launch_bounds__(kWBlock, 4) solve_wide_kernel(const SolveParam
   wstamp(P, b, 6);
   if constexpr (FUSE) {
     if (!uniform_all) return;  // workgroup-uniform: gain_kernel takes per-vehicle rows
+#ifdef ACL_EXP_SKIP_GAIN
+    return;  // diagnostic builds: the fused kernel without its control phase
+#endif
     __syncthreads();           // the auction's tables and the hand-off reads are done
     KCtlParams* pc = (KCtlParams*)((const __attribute__((address_space(4))) char*)
                                        __builtin_amdgcn_kernarg_segment_ptr() +
