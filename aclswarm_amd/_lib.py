@@ -105,7 +105,7 @@ class HungarianArgs(ct.Structure):
 class CbaaStepArgs(ct.Structure):
     """acl_cbaa_step_args_t (ABI 11): one CBAA bid iteration per vehicle
     (auctioneer.cpp:182-306,469-542)."""
-    _fields_ = [("V", ct.c_int32)] + [(n, ct.c_void_p) for n in (
+    _fields_ = [("V", ct.c_int32), ("K", ct.c_int32)] + [(n, ct.c_void_p) for n in (
         "fidx", "vehid", "q", "Rt", "start", "price", "who", "cand_off", "cand_vehid",
         "cand_price", "cand_who", "task", "flags")]
 

@@ -34,7 +34,7 @@ extern "C" acl_status_t acl__set_error(const char* msg);
 namespace acl_amd {
 
 struct StepParams {
-  int n, V, F;
+  int n, V, K, F;
   const double* p;
   const int32_t* fidx;
   const int32_t* vehid;
@@ -81,7 +81,8 @@ __global__ void __launch_bounds__(64 * kStepWaves) cbaa_step_kernel(const StepPa
   // argument checks (wave-uniform): the vehicle, its formation, and the
   // candidates strictly ascending by vehid inside [0, n)
   bool bad = v < 0 || v >= n || f < 0 || f >= P.F ||
-             (!st && (c1 <= c0 || !P.cand_vehid || !P.cand_price || !P.cand_who));
+             (!st && (c0 < 0 || c1 <= c0 || c1 > P.K || !P.cand_vehid || !P.cand_price ||
+                      !P.cand_who));
   if (!bad && !st) {
     for (int c = c0 + lane; c < c1; c += 64) {
       const int u = P.cand_vehid[c];
@@ -189,13 +190,13 @@ extern "C" acl_status_t acl_cbaa_step_batch(const acl_formations_t* F, const acl
   if (!F || !a) return acl__set_error("acl_cbaa_step_batch: null argument");
   const int n = F->n;
   if (n < 1 || n > 512) return acl__set_error("acl_cbaa_step_batch: n out of range [1, 512]");
-  if (a->V < 0) return acl__set_error("acl_cbaa_step_batch: V < 0");
+  if (a->V < 0 || a->K < 0) return acl__set_error("acl_cbaa_step_batch: V < 0 or K < 0");
   if (a->V == 0) return ACL_OK;
   if (!F->p || F->n_formations < 1 || !a->fidx || !a->vehid || !a->q || !a->Rt || !a->start ||
       !a->price || !a->who || !a->cand_off || !a->task || !a->flags)
     return acl__set_error("acl_cbaa_step_batch: required pointer is NULL");
   StepParams P;
-  P.n = n; P.V = a->V; P.F = F->n_formations; P.p = F->p;
+  P.n = n; P.V = a->V; P.K = a->K; P.F = F->n_formations; P.p = F->p;
   P.fidx = a->fidx; P.vehid = a->vehid; P.q = a->q; P.Rt = a->Rt; P.start = a->start;
   P.price = a->price; P.who = a->who; P.cand_off = a->cand_off; P.cand_vehid = a->cand_vehid;
   P.cand_price = a->cand_price; P.cand_who = a->cand_who; P.task = a->task; P.flags = a->flags;

@@ -366,6 +366,7 @@ def cbaa_step(table, fidx, vehid, q, Rt, start, price, who, cand_off, cand_vehid
     flags = torch.empty((V,), dtype=torch.int32, device=dev)
     a = L.CbaaStepArgs()
     a.V = V
+    a.K = K if K is not None else 0
     a.fidx = fidx.data_ptr(); a.vehid = vehid.data_ptr(); a.q = q.data_ptr()
     a.Rt = Rt.data_ptr(); a.start = start.data_ptr(); a.price = price.data_ptr()
     a.who = who.data_ptr(); a.cand_off = cand_off.data_ptr()

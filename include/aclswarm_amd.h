@@ -474,15 +474,16 @@ acl_status_t acl_hungarian_batch(const acl_formations_t* formations,
  *   price      [V][n]     in/out f32: its table's prices (Bid::price)
  *   who        [V][n]     in/out i32: its table's holders (Bid::who, -1 none)
  *   cand_off   [V + 1]    vehicle k's candidates are rows cand_off[k] ..
- *                         cand_off[k + 1] - 1 (>= 1 row unless start[k])
+ *                         cand_off[k + 1] - 1 (>= 1 row unless start[k]),
+ *                         0 <= cand_off[k] <= cand_off[k + 1] <= K
  *   cand_vehid [K]        each candidate's vehid, strictly ascending per vehicle
  *   cand_price [K][n] f32, cand_who [K][n] i32: the candidates' tables
  *                         (may be NULL when every start[k] is 1)
  *   task       [V]        out: the task the select took, -1 if none ran or
  *                         none was eligible
- *   flags      [V]        out: ACL_CBAA_* bits (BAD_INPUT: a vehid, fidx or
- *                         the candidate order is invalid; the table is left
- *                         as it was)
+ *   flags      [V]        out: ACL_CBAA_* bits (BAD_INPUT: a vehid, fidx,
+ *                         candidate range or candidate order is invalid; the
+ *                         table is left as it was)
  * Stream-ordered, no workspace. */
 #define ACL_CBAA_OUTBID    0x01 /* a task it held went to another vehicle */
 #define ACL_CBAA_SELECTED  0x02 /* selectTaskAssignment took a task */
@@ -490,6 +491,7 @@ acl_status_t acl_hungarian_batch(const acl_formations_t* formations,
 
 typedef struct {
   int32_t V;
+  int32_t K;  /* rows of cand_vehid / cand_price / cand_who (cand_off[V] <= K) */
   const int32_t* fidx;
   const int32_t* vehid;
   const double* q;

@@ -762,6 +762,7 @@ class Auctioneer {
     acl_cbaa_step_args_t a;
     std::memset(&a, 0, sizeof(a));
     a.V = 1;
+    a.K = K;
     a.fidx = x_fidx_.as<const int32_t>();
     a.vehid = x_vehid_.as<const int32_t>();
     a.q = x_q_.as<const double>();

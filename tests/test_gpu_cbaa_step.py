@@ -165,3 +165,27 @@ def test_protocol_on_gpu_equals_one_call_consensus(name, b):
         assert not (fl & 0x10).any()
     who_1 = np.where(who_1 == 0xFFFF, -1, who_1)
     np.testing.assert_array_equal(wh, who_1)
+
+
+def test_step_candidate_range_checked():
+    """A candidate range outside [0, K] (cand_off[k + 1] > K, or a reversed
+    range) is BAD_INPUT: nothing past the candidate arrays is read and the
+    tables are left as they were."""
+    import torch
+    from aclswarm_amd import engine
+    n, V, K = 5, 3, 2
+    ps = [np.column_stack([np.arange(n, dtype=float), np.zeros(n), np.ones(n)])]
+    T = engine.FormationTable.from_host(ps, [np.ones((n, n), np.uint8)], None, device=_dev())
+    price = np.full((V, n), 0.25, np.float32)
+    who = np.full((V, n), -1, np.int32)
+    pr_d, wh_d = _t(price, np.float32), _t(who, np.int32)
+    off = np.array([0, 3, 2, 2], np.int32)  # vehicle 0: rows 0..2 (> K); 1: reversed; 2: empty
+    task, flags = engine.cbaa_step(
+        T, _t(np.zeros(V), np.int32), _t([0, 1, 2], np.int32), _t(np.zeros((V, 3)), np.float64),
+        _t(np.tile([1.0, 0, 0, 1.0, 0, 0], (V, 1)), np.float64), _t(np.zeros(V), np.uint8),
+        pr_d, wh_d, _t(off, np.int32), _t([0, 1], np.int32), _t(np.zeros((K, n)), np.float32),
+        _t(np.zeros((K, n)), np.int32))
+    torch.cuda.synchronize()
+    assert (flags.cpu().numpy() == 0x10).all() and (task.cpu().numpy() == -1).all()
+    np.testing.assert_array_equal(pr_d.cpu().numpy(), price)
+    np.testing.assert_array_equal(wh_d.cpu().numpy(), who)
