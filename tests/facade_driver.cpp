@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <functional>
+#include <map>
 #include <memory>
 #include <vector>
 
@@ -385,6 +386,237 @@ extern "C" int facade_exchange(int n, const double* p_cm, const uint8_t* adj_cm,
     }
   } catch (const std::exception& e) {
     fprintf(stderr, "facade_exchange: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}
+
+// A CPU stand-in for a vehicle that runs the reference's own Auctioneer
+// (test infrastructure: auctioneer.cpp:78-125 start, :139-160 tick, :182-306
+// processBid, :419-437 bidIterComplete, :448-465 reset, :469-542 the CBAA
+// tally, restated over plain vectors; its price row C[v][.] is getPrice from
+// its alignment, given by the caller from the CPU oracle). It speaks the same
+// bids as the facade's exchange mode, so a fleet can mix the two.
+struct RefVehicle {
+  using Bid = amd::Auctioneer::Bid;
+  struct Pkt {
+    int from;
+    uint32_t auction, iter;
+    Bid bid;
+  };
+  int n = 0, vehid = 0, biditer = 0, auctionid = 0;
+  bool open = false, invalid = false;
+  std::vector<uint8_t> adj;  // column-major AdjMat
+  std::vector<int> P, Pt;
+  std::vector<float> C;  // its getPrice row
+  Bid bid;
+  std::map<int, Bid> zero, curr, next;
+  std::vector<Pkt> queue;
+  std::function<void(uint32_t, uint32_t, const Bid&)> send;
+
+  void reset() {
+    open = false;
+    biditer = 0;
+    bid.price.assign(n, 0.0f);
+    bid.who.assign(n, -1);
+    curr.clear();
+    next.clear();
+  }
+  void select() {  // selectTaskAssignment (:517-542)
+    float mx = 0.0f;
+    int task = -1;
+    for (int j = 0; j < n; ++j)
+      if (C[j] > mx && C[j] > bid.price[j]) {
+        mx = C[j];
+        task = j;
+      }
+    if (task >= 0) {
+      bid.price[task] = mx;
+      bid.who[task] = vehid;
+    }
+  }
+  void start() {
+    reset();
+    curr = zero;
+    zero.clear();
+    select();
+    open = true;
+    ++auctionid;
+    send((uint32_t)auctionid, 0u, bid);
+  }
+  bool complete() const {
+    const int i = P[vehid];
+    for (int j = 0; j < n; ++j)
+      if (adj[(size_t)j * n + i] && curr.find(Pt[j]) == curr.end()) return false;
+    return true;
+  }
+  void tick() {
+    if (!open || queue.empty()) return;
+    const Pkt k = queue.front();
+    queue.erase(queue.begin());
+    if (k.iter == 0) zero.insert({k.from, k.bid});
+    if (k.iter == (uint32_t)biditer) curr.insert({k.from, k.bid});
+    else if (k.iter == (uint32_t)biditer + 1) next.insert({k.from, k.bid});
+    if (!complete()) return;
+    curr.insert({vehid, bid});  // updateTaskAssignment (:469-513)
+    bool outbid = false;
+    for (int j = 0; j < n; ++j) {
+      auto mx = curr.cbegin();
+      for (auto it = curr.cbegin(); it != curr.cend(); ++it)
+        if (it->second.price[j] > mx->second.price[j]) mx = it;
+      if (bid.who[j] == vehid && mx->second.who[j] != vehid) outbid = true;
+      bid.who[j] = mx->second.who[j];
+      bid.price[j] = mx->second.price[j];
+    }
+    if (outbid) select();
+    ++biditer;
+    curr = next;
+    next.clear();
+    if (biditer == 1) zero.clear();
+    if (biditer >= 2 * n) {  // consensus: adopt a valid table (:250-292)
+      std::vector<int> seen(n, 0);
+      bool ok = true;
+      for (int j = 0; j < n && ok; ++j) {
+        const int w = bid.who[j];
+        ok = w >= 0 && w < n && !seen[w];
+        if (ok) seen[w] = 1;
+      }
+      if (ok)
+        for (int j = 0; j < n; ++j) {
+          Pt[j] = bid.who[j];
+          P[bid.who[j]] = j;
+        }
+      else
+        invalid = true;
+      reset();
+    } else {
+      send((uint32_t)auctionid, (uint32_t)biditer, bid);
+    }
+  }
+};
+
+// A mixed fleet: vehicle v is an exchange-mode facade when facade_mask[v],
+// else a RefVehicle (price row C[v], row-major [n][n] from the CPU oracle);
+// one bus as in facade_exchange (senders interleaved by `seed`, each
+// sender's bids in order). Outputs per vehicle: P_out[n][n], invalid[n],
+// sends[n], last_iter[n], who_out[n][n] (its last sent bid's who).
+extern "C" int facade_mixed(int n, const double* p_cm, const uint8_t* adj_cm, const double* q_cm,
+                            const uint8_t* Pin, const float* C, const uint8_t* facade_mask,
+                            uint32_t seed, uint8_t* P_out, uint8_t* invalid_out,
+                            int32_t* sends_out, int32_t* last_iter_out, int32_t* who_out) {
+  try {
+    amd::PtsMat p(n, 3), q(n, 3);
+    amd::AdjMat adj(n, n);
+    std::copy(p_cm, p_cm + (size_t)3 * n, p.data());
+    std::copy(q_cm, q_cm + (size_t)3 * n, q.data());
+    std::copy(adj_cm, adj_cm + (size_t)n * n, adj.data());
+    uint64_t rng = 0xD1B54A32D192ED03ull ^ seed;
+    auto rnd = [&](uint32_t m) {  // splitmix64
+      rng += 0x9E3779B97F4A7C15ull;
+      uint64_t z = rng;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      return (uint32_t)((z ^ (z >> 31)) % m);
+    };
+    struct Msg {
+      int from;
+      uint32_t auction, iter;
+      amd::Auctioneer::Bid bid;
+    };
+    std::vector<Msg> bus;
+    std::vector<std::unique_ptr<amd::Auctioneer>> fac(n);
+    std::vector<RefVehicle> ref(n);
+    std::vector<std::vector<int>> subs(n);
+    std::vector<int> sends(n, 0), last_iter(n, -1);
+    std::vector<std::vector<int32_t>> last_who(n);
+    amd::AssignmentPerm P0(amd::Map<const amd::AssignmentVec>(Pin, (size_t)n));
+    for (int v = 0; v < n; ++v) {
+      auto sent = [&bus, &sends, &last_iter, &last_who, v](uint32_t aid, uint32_t iter,
+                                                          const amd::Auctioneer::Bid& b) {
+        ++sends[v];
+        last_iter[v] = (int)iter;
+        last_who[v].assign(b.who.begin(), b.who.end());
+        bus.push_back(Msg{v, aid, iter, b});
+      };
+      if (facade_mask[v]) {
+        fac[v].reset(new amd::Auctioneer((amd::vehidx_t)v, (uint8_t)n, false));
+        fac[v]->setBidExchange(true);
+        fac[v]->setFormation(p, adj);
+        fac[v]->setAssignment(P0);
+        fac[v]->setSendBidHandler(
+            [sent](uint32_t aid, uint32_t iter, const amd::Auctioneer::BidConstPtr& b) {
+              sent(aid, iter, *b);
+            });
+      } else {
+        RefVehicle& r = ref[v];
+        r.n = n;
+        r.vehid = v;
+        r.adj.assign(adj_cm, adj_cm + (size_t)n * n);
+        r.P.resize(n);
+        r.Pt.resize(n);
+        for (int k = 0; k < n; ++k) {
+          r.P[k] = Pin[k];
+          r.Pt[Pin[k]] = k;
+        }
+        r.C.assign(C + (size_t)v * n, C + (size_t)(v + 1) * n);
+        r.reset();
+        r.send = sent;
+      }
+      const int i = P0.indices()(v);
+      for (int j = 0; j < n; ++j)
+        if (adj(i, j)) subs[v].push_back(P0.transpose().indices()(j));
+    }
+    auto tick = [&](int v) {
+      if (fac[v]) fac[v]->tick();
+      else ref[v].tick();
+    };
+    auto queued = [&](int v) { return fac[v] ? fac[v]->queuedBids() : ref[v].queue.size(); };
+    for (int v = 0; v < n; ++v) {
+      if (fac[v]) fac[v]->start(q);
+      else ref[v].start();
+    }
+    for (size_t guard = 0; guard < 100000000; ++guard) {
+      if (!bus.empty()) {
+        size_t m = rnd((uint32_t)bus.size());
+        for (size_t k = 0; k < m; ++k)
+          if (bus[k].from == bus[m].from) {
+            m = k;
+            break;
+          }
+        const Msg msg = bus[m];
+        bus.erase(bus.begin() + (long)m);
+        for (int u = 0; u < n; ++u) {
+          const auto& sb = subs[u];
+          if (u == msg.from || std::find(sb.begin(), sb.end(), msg.from) == sb.end()) continue;
+          if (fac[u]) fac[u]->enqueueBid((amd::vehidx_t)msg.from, msg.auction, msg.iter, msg.bid);
+          else ref[u].queue.push_back(RefVehicle::Pkt{msg.from, msg.auction, msg.iter, msg.bid});
+        }
+      }
+      bool busy = !bus.empty();
+      for (int v = 0; v < n && !busy; ++v) busy = queued(v) > 0;
+      if (!busy) break;
+      for (int v = 0; v < n; ++v) tick(v);
+    }
+    for (int v = 0; v < n; ++v) {
+      std::vector<int> Pv(n);
+      if (fac[v]) {
+        if (!fac[v]->isIdle()) throw std::runtime_error("mixed: a facade auction is still open");
+        if (fac[v]->lastStatus() != ACL_OK) throw std::runtime_error(fac[v]->lastError());
+        for (int k = 0; k < n; ++k) Pv[k] = fac[v]->getAssignmentIndices()[k];
+        invalid_out[v] = fac[v]->didConvergeOnInvalidAssignment() ? 1 : 0;
+      } else {
+        if (ref[v].open) throw std::runtime_error("mixed: a reference-protocol auction is still open");
+        Pv = ref[v].P;
+        invalid_out[v] = ref[v].invalid ? 1 : 0;
+      }
+      for (int k = 0; k < n; ++k) P_out[(size_t)v * n + k] = (uint8_t)Pv[k];
+      sends_out[v] = sends[v];
+      last_iter_out[v] = last_iter[v];
+      for (int k = 0; k < n; ++k)
+        who_out[(size_t)v * n + k] = last_who[v].empty() ? -2 : last_who[v][k];
+    }
+  } catch (const std::exception& e) {
+    fprintf(stderr, "facade_mixed: %s\n", e.what());
     return 1;
   }
   return 0;

@@ -242,3 +242,54 @@ def test_facade_bid_exchange(case, seed, late):
     C, _ = O.prices(q, p, adj, np.asarray(P_in, np.uint16))
     who, _ = S.lockstep(C, adj, P_in, rounds=2 * n - 1)
     np.testing.assert_array_equal(got["who"], who)
+
+
+@pytest.mark.parametrize("case,seed,mask", [("swarm6", 11, "alternate"), ("swarm6", 12, "one"),
+                                            ("simform20_nc", 13, "alternate"),
+                                            ("simform20_fc", 14, "half")])
+def test_facade_mixed_fleet(case, seed, mask):
+    """A mixed fleet (some vehicles on the reference's own
+    Auctioneer): exchange-mode facades (GPU tallies) and CPU stand-ins of the
+    reference's protocol (tests/facade_driver.cpp RefVehicle, its prices from
+    the CPU oracle) on one bus. Every vehicle, of either kind, adopts the
+    one-call consensus's assignment and sends 2n bids; the last bids equal
+    the lockstep protocol's tables after 2n - 1 iterations."""
+    import cbaa_step_oracle as S
+    rng = np.random.RandomState(seed)
+    if case == "swarm6":
+        pts, adjs, gains, q0 = H.swarm6()
+        p, adj, g = pts[1], adjs[1], gains[1]
+        q = q0 + rng.normal(0, 0.3, q0.shape)
+    else:
+        Pf, Af = H.simform(case)
+        p, adj = Pf[seed % Pf.shape[0], 0], Af[seed % Af.shape[0]]
+        g = H.synth_gains(rng, adj)
+        q = H.random_positions(rng, p.shape[0], 20.0)
+    n = p.shape[0]
+    P_in = H.random_perm(rng, n)
+    fm = {"alternate": np.arange(n) % 2 == 0, "one": np.arange(n) == 3,
+          "half": np.arange(n) < n // 2}[mask].astype(np.uint8)
+    C, _ = O.prices(q, p, adj, np.asarray(P_in, np.uint16))
+    lib = ct.CDLL(LIB)
+    f = lib.facade_mixed
+    f.restype = ct.c_int
+    f.argtypes = [ct.c_int] + [ct.c_void_p] * 6 + [ct.c_uint32] + [ct.c_void_p] * 5
+    Pout = np.zeros((n, n), np.uint8)
+    inv = np.zeros(n, np.uint8)
+    sends, last_iter = np.zeros(n, np.int32), np.zeros(n, np.int32)
+    who = np.zeros((n, n), np.int32)
+    arrs = [np.asfortranarray(p, np.float64), np.asfortranarray(np.asarray(adj, np.uint8)),
+            np.asfortranarray(q, np.float64), np.ascontiguousarray(P_in, np.uint8),
+            np.ascontiguousarray(C, np.float32), fm]
+    ptr = lambda a: a.ctypes.data_as(ct.c_void_p)  # noqa: E731
+    assert f(n, *[ptr(a) for a in arrs], seed, ptr(Pout), ptr(inv), ptr(sends), ptr(last_iter),
+             ptr(who)) == 0
+    P, inv_e, _ = _expect(p, adj, g, q, np.zeros_like(q), P_in)
+    np.testing.assert_array_equal(inv, inv_e)
+    for v in range(n):
+        if not inv_e[v]:
+            np.testing.assert_array_equal(Pout[v], P[v], err_msg=f"vehicle {v} ({mask})")
+    np.testing.assert_array_equal(sends, np.full(n, 2 * n))
+    np.testing.assert_array_equal(last_iter, np.full(n, 2 * n - 1))
+    who_l, _ = S.lockstep(C, adj, P_in, rounds=2 * n - 1)
+    np.testing.assert_array_equal(who, who_l)
