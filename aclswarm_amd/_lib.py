@@ -194,6 +194,11 @@ def lib():
         raise RuntimeError(
             f"aclswarm_amd: native library {LIB_PATH} is missing. Build it with "
             "`python -m aclswarm_amd.build` (hipcc --offload-arch=gfx950).")
+    # torch before the library: torch bundles its own libamdhip64 under the
+    # same SONAME, and whichever loads first is the process's HIP runtime;
+    # loading torch first keeps it usable next to this library (the other
+    # order leaves torch without a device)
+    import torch  # noqa: F401
     L = ct.CDLL(LIB_PATH)
     VP, I32, I64, SZ = ct.c_void_p, ct.c_int32, ct.c_int64, ct.c_size_t
     L.acl_default_cntrl_gains.argtypes = [ct.POINTER(CntrlGains)]

@@ -741,49 +741,60 @@ class Auctioneer {
       }
     }
     const int K = (int)cv.size();
-    const int32_t fidx = 0, vid = vehid_;
+    // one staging image each way (one copy up, one down): doubles first,
+    // then the table (price, who) and the outputs (task, flags) contiguous,
+    // then the small ints and the candidates
+    const size_t o_q = 0, o_rt = 24, o_price = 72, o_who = o_price + (size_t)4 * n,
+                 o_out = o_who + (size_t)4 * n, o_i = o_out + 8, o_off = o_i + 8, o_st = o_off + 8,
+                 o_cv = o_st + 8, o_cp = o_cv + (size_t)4 * K,
+                 o_cw = o_cp + (size_t)4 * K * n, total = o_cw + (size_t)4 * K * n;
+    std::vector<unsigned char> h(total, 0);
+    const int32_t ids[2] = {0, (int32_t)vehid_};  // fidx, vehid
     const int32_t off[2] = {0, K};
-    const uint8_t st = start ? 1 : 0;
-    std::vector<int32_t> who(bid_.who.begin(), bid_.who.end());
-    x_fidx_.upload(&fidx, 4);
-    x_vehid_.upload(&vid, 4);
-    x_q_.upload(q_self_, 24);
-    x_rt_.upload(rt_self_, 48);
-    x_start_.upload(&st, 1);
-    x_price_.upload(bid_.price.data(), (size_t)n * 4);
-    x_who_.upload(who.data(), (size_t)n * 4);
-    x_off_.upload(off, 8);
-    if (K) {
-      x_cv_.upload(cv.data(), (size_t)K * 4);
-      x_cp_.upload(cp.data(), cp.size() * 4);
-      x_cw_.upload(cw.data(), cw.size() * 4);
+    std::memcpy(&h[o_q], q_self_, 24);
+    std::memcpy(&h[o_rt], rt_self_, 48);
+    std::memcpy(&h[o_price], bid_.price.data(), (size_t)4 * n);
+    for (int j = 0; j < n; ++j) {
+      const int32_t w = bid_.who[j];
+      std::memcpy(&h[o_who + (size_t)4 * j], &w, 4);
     }
-    x_out_.reserve(8);
+    std::memcpy(&h[o_i], ids, 8);
+    std::memcpy(&h[o_off], off, 8);
+    h[o_st] = start ? 1 : 0;
+    if (K) {
+      std::memcpy(&h[o_cv], cv.data(), (size_t)4 * K);
+      std::memcpy(&h[o_cp], cp.data(), cp.size() * 4);
+      std::memcpy(&h[o_cw], cw.data(), cw.size() * 4);
+    }
+    x_stage_.upload(h.data(), total);
+    unsigned char* d = x_stage_.as<unsigned char>();
     acl_cbaa_step_args_t a;
     std::memset(&a, 0, sizeof(a));
     a.V = 1;
     a.K = K;
-    a.fidx = x_fidx_.as<const int32_t>();
-    a.vehid = x_vehid_.as<const int32_t>();
-    a.q = x_q_.as<const double>();
-    a.Rt = x_rt_.as<const double>();
-    a.start = x_start_.as<const uint8_t>();
-    a.price = x_price_.as<float>();
-    a.who = x_who_.as<int32_t>();
-    a.cand_off = x_off_.as<const int32_t>();
-    a.cand_vehid = K ? x_cv_.as<const int32_t>() : nullptr;
-    a.cand_price = K ? x_cp_.as<const float>() : nullptr;
-    a.cand_who = K ? x_cw_.as<const int32_t>() : nullptr;
-    a.task = x_out_.as<int32_t>();
-    a.flags = x_out_.as<int32_t>() + 1;
+    a.fidx = reinterpret_cast<const int32_t*>(d + o_i);
+    a.vehid = reinterpret_cast<const int32_t*>(d + o_i) + 1;
+    a.q = reinterpret_cast<const double*>(d + o_q);
+    a.Rt = reinterpret_cast<const double*>(d + o_rt);
+    a.start = d + o_st;
+    a.price = reinterpret_cast<float*>(d + o_price);
+    a.who = reinterpret_cast<int32_t*>(d + o_who);
+    a.cand_off = reinterpret_cast<const int32_t*>(d + o_off);
+    a.cand_vehid = K ? reinterpret_cast<const int32_t*>(d + o_cv) : nullptr;
+    a.cand_price = K ? reinterpret_cast<const float*>(d + o_cp) : nullptr;
+    a.cand_who = K ? reinterpret_cast<const int32_t*>(d + o_cw) : nullptr;
+    a.task = reinterpret_cast<int32_t*>(d + o_out);
+    a.flags = reinterpret_cast<int32_t*>(d + o_out) + 1;
     const acl_formations_t F = form_.table();
     detail::check(acl_cbaa_step_batch(&F, &a, nullptr));
-    int32_t out[2] = {0, 0};
-    detail::check(acl_memcpy_d2h(bid_.price.data(), x_price_.get(), (size_t)n * 4, nullptr));
-    detail::check(acl_memcpy_d2h(who.data(), x_who_.get(), (size_t)n * 4, nullptr));
-    detail::check(acl_memcpy_d2h(out, x_out_.get(), 8, nullptr));
+    detail::check(acl_memcpy_d2h(&h[o_price], d + o_price, o_i - o_price, nullptr));
     detail::check(acl_stream_synchronize(nullptr));
+    int32_t out[2];
+    std::memcpy(out, &h[o_out], 8);
     if (out[1] & ACL_CBAA_BAD_INPUT) throw std::runtime_error("acl_cbaa_step_batch: bad input");
+    std::memcpy(bid_.price.data(), &h[o_price], (size_t)4 * n);
+    std::vector<int32_t> who(n);
+    std::memcpy(who.data(), &h[o_who], (size_t)4 * n);
     bid_.who.assign(who.begin(), who.end());
   }
 
@@ -797,8 +808,7 @@ class Auctioneer {
   std::vector<BidPkt> rxbids_;  // FIFO (std::queue in the reference)
   std::vector<uint8_t> adj_;    // AdjMat, column-major
   double q_self_[3] = {0.0, 0.0, 0.0}, rt_self_[6] = {1.0, 0.0, 0.0, 1.0, 0.0, 0.0};
-  detail::DeviceBuffer x_fidx_, x_vehid_, x_q_, x_rt_, x_start_, x_price_, x_who_, x_off_, x_cv_,
-      x_cp_, x_cw_, x_out_;
+  detail::DeviceBuffer x_stage_;  // acl_cbaa_step_batch's staging image (step())
   std::vector<vehidx_t> P_, Pt_;
   int auctionid_ = 0;
   bool auction_open_ = false;

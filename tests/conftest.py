@@ -2,6 +2,13 @@ import os
 import sys
 
 import pytest
+# torch first: it bundles its own libamdhip64 (same SONAME as /opt/rocm's,
+# which libaclswarm_amd.so links). Loaded first, torch's copy is the one HIP
+# runtime of the process and the in-tree libraries bind to it; a test that
+# ctypes-loads a driver library before torch would instead bring in
+# /opt/rocm's runtime, and torch then finds no device ("No HIP GPUs are
+# available", seen when tests/test_gpu_facade.py ran before any torch test).
+import torch  # noqa: F401,E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
