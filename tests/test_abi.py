@@ -159,9 +159,9 @@ def test_cpp_facade_compiles_and_exports():
     compiles warning-free as C++17 and the built exerciser exports facade_run."""
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    subprocess.check_call(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror",
-                           "-I" + os.path.join(root, "include"),
-                           os.path.join(root, "tests", "facade_driver.cpp")])
+    for src in ("facade_driver.cpp", "exchange_asan_main.cpp"):
+        subprocess.check_call(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror",
+                               "-I" + os.path.join(root, "include"), os.path.join(root, "tests", src)])
     from aclswarm_amd import build
     so = build.build_driver()
     assert hasattr(ct.CDLL(so), "facade_run")
