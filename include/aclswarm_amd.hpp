@@ -79,6 +79,7 @@
 #include <cstring>
 #include <functional>
 #include <algorithm>
+#include <atomic>
 #include <iostream>
 #include <map>
 #include <memory>
@@ -444,7 +445,8 @@ class Auctioneer {
     if (send_bid_) send_bid_((uint32_t)auctionid_, (uint32_t)(2 * n_), finalBid(r.q, r.who, r.Rt));
   }
   /* the outcome of the last start(): ACL_OK, or why no auction ran
-   * (lastError() says what) */
+   * (lastError() says what); in exchange mode also a tally that failed or a
+   * malformed bid that processBid dropped (ACL_ERR_INVALID_ARG) */
   acl_status_t lastStatus() const { return last_status_; }
   const std::string& lastError() const { return last_error_; }
 
@@ -688,6 +690,12 @@ class Auctioneer {
 
   /* processBid (auctioneer.cpp:182-306) */
   void processBid(const BidPkt& pkt) {
+    if ((int)pkt.bid.price.size() != n_ || (int)pkt.bid.who.size() != n_) {
+      // a malformed bid (the reference would index past its tables): dropped
+      last_status_ = ACL_ERR_INVALID_ARG;
+      last_error_ = "Auctioneer: dropped a bid whose tables are not n long";
+      return;
+    }
     if (verbose_)
       std::cout << "A" << auctionid_ << "B" << biditer_ << ": Processing a" << pkt.auctionid
                 << "b" << pkt.iter << " from " << static_cast<int>(pkt.vehid) << std::endl;
@@ -801,7 +809,7 @@ class Auctioneer {
   int n_;
   vehidx_t vehid_;
   bool verbose_;
-  bool exchange_ = false;
+  std::atomic<bool> exchange_{false};  // read by enqueueBid without the auction mutex
   int biditer_ = 0, cbaa_max_iter_ = 0;
   Bid bid_;
   std::map<vehidx_t, Bid> bids_zero_, bids_curr_, bids_next_;
